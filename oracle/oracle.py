@@ -1,0 +1,205 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes front-end of the plain-C restatement (``satenv_oracle.c``) plus numpy /
+torch-CPU restatements of the learning-side hot path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module; the product package never does (and fails loudly without its HIP
+library instead of falling back here).
+
+Reference citations are ``file:line`` in qiaobeibei/PPO-RL-Satellite.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle_satenv.so")
+
+PYINT, I64, F32, F64 = 0, 1, 2, 3
+
+
+class OrcEnv(C.Structure):
+    _fields_ = [("Pp", C.c_double * 3), ("Pv", C.c_double * 3), ("Ep", C.c_double * 3),
+                ("Ev", C.c_double * 3), ("fuel_c", C.c_double), ("fuel_t", C.c_double),
+                ("dis", C.c_double), ("dz", C.c_int32), ("fuel_c_mode", C.c_int32),
+                ("fuel_t_mode", C.c_int32), ("vel_int", C.c_int32), ("flag", C.c_int32)]
+
+
+class OrcParams(C.Structure):
+    _fields_ = [("d_capture", C.c_double), ("d_range", C.c_double), ("win_reward", C.c_double),
+                ("burn_reward", C.c_double), ("max_episode_steps", C.c_int32), ("mu", C.c_double),
+                ("R_cw", C.c_double * 3), ("V_cw", C.c_double * 3), ("stm", C.c_double * 36)]
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc); returns the .so path."""
+    subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        dp = C.POINTER(C.c_double)
+        fp = C.POINTER(C.c_float)
+        ip = C.POINTER(C.c_int32)
+        L.orc_default_params.argtypes = [C.POINTER(OrcParams), C.c_double, C.c_int32]
+        L.orc_stm.argtypes = [C.c_double, dp]
+        L.orc_env_init.argtypes = [C.POINTER(OrcEnv)]
+        L.orc_reset.argtypes = [C.POINTER(OrcEnv), C.c_int32, dp]
+        L.orc_step.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcEnv), fp, fp, C.c_int32, dp, dp, ip]
+        L.orc_step.restype = C.c_int
+        L.orc_danger_zone.argtypes = [dp, dp, dp, dp, C.c_double, C.c_int32, ip]
+        L.orc_danger_zone.restype = C.c_int
+        L.orc_orbital_elements.argtypes = [C.c_double, dp, dp, dp]
+        L.orc_orbital_elements.restype = C.c_int
+        L.orc_solve_alpha.argtypes = [C.c_double] * 7 + [ip]
+        L.orc_solve_alpha.restype = C.c_double
+        L.orc_rollout.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcEnv), C.c_int64, C.c_int32,
+                                  fp, fp, ip, dp, ip, C.c_int32]
+        L.orc_rollout.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def params(d_capture=15000.0, max_episode_steps=1000, d_range=100000.0):
+    p = OrcParams()
+    lib().orc_default_params(C.byref(p), float(d_capture), int(max_episode_steps))
+    p.d_range = float(d_range)
+    return p
+
+
+def stm(t=100.0):
+    out = np.zeros(36)
+    lib().orc_stm(float(t), _dp(out))
+    return out.reshape(6, 6)
+
+
+def solve_alpha(u, dvm, theta, v1x, v1y, h, guess):
+    nfev = C.c_int32(0)
+    x = lib().orc_solve_alpha(u, dvm, theta, v1x, v1y, h, guess, C.byref(nfev))
+    return x, nfev.value
+
+
+def orbital_elements(R, V, mu=3.986e14):
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    V = np.ascontiguousarray(V, dtype=np.float64)
+    out = np.zeros(6)
+    rc = lib().orc_orbital_elements(mu, _dp(R), _dp(V), _dp(out))
+    return rc, out
+
+
+def danger_zone(Rc, Vc, Rt, Vt, fuel, fuel_mode):
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (Rc, Vc, Rt, Vt)]
+    cnt = C.c_int32(0)
+    rc = lib().orc_danger_zone(*[_dp(a) for a in arrs], float(fuel), int(fuel_mode), C.byref(cnt))
+    return rc, cnt.value
+
+
+class OracleEnv:
+    """N=1 environment on the C restatement (environment.py:8-343 semantics)."""
+
+    def __init__(self, d_capture=15000.0, max_episode_steps=1000, d_range=100000.0):
+        self.p = params(d_capture, max_episode_steps, d_range)
+        self.e = OrcEnv()
+        lib().orc_env_init(C.byref(self.e))
+
+    def reset(self, flag=0):
+        obs = np.zeros(18)
+        lib().orc_reset(C.byref(self.e), int(flag), _dp(obs))
+        return obs
+
+    def step(self, pa, ea, episode_count):
+        pa = np.ascontiguousarray(pa, dtype=np.float32)
+        ea = np.ascontiguousarray(ea, dtype=np.float32)
+        obs = np.zeros(18)
+        r = C.c_double(0)
+        d = C.c_int32(0)
+        rc = lib().orc_step(C.byref(self.p), C.byref(self.e), pa.ctypes.data_as(C.POINTER(C.c_float)),
+                            ea.ctypes.data_as(C.POINTER(C.c_float)), int(episode_count), _dp(obs),
+                            C.byref(r), C.byref(d))
+        if rc != 0:
+            raise RuntimeError(f"oracle step error {rc}")
+        return obs, r.value, bool(d.value)
+
+    def get_state(self):
+        e = self.e
+        return dict(Pp=np.array(e.Pp[:]), Pv=np.array(e.Pv[:]), Ep=np.array(e.Ep[:]), Ev=np.array(e.Ev[:]),
+                    fuel_c=e.fuel_c, fuel_t=e.fuel_t, dis=e.dis, dz=e.dz, fuel_c_mode=e.fuel_c_mode,
+                    fuel_t_mode=e.fuel_t_mode, vel_int=e.vel_int, flag=e.flag)
+
+    def set_state(self, st):
+        e = self.e
+        for k in ("Pp", "Pv", "Ep", "Ev"):
+            getattr(e, k)[:] = [float(v) for v in st[k]]
+        for k in ("fuel_c", "fuel_t", "dis"):
+            setattr(e, k, float(st[k]))
+        for k in ("dz", "fuel_c_mode", "fuel_t_mode", "vel_int", "flag"):
+            setattr(e, k, int(st[k]))
+
+
+def rollout(n_envs, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=1, flag=0):
+    """Batched replay from reset (CPU baseline).  pa/ea: float32 [steps, n, 3]."""
+    p = params(d_capture, max_episode_steps)
+    envs = (OrcEnv * n_envs)()
+    for i in range(n_envs):
+        lib().orc_env_init(C.byref(envs[i]))
+        lib().orc_reset(C.byref(envs[i]), flag, None)
+    cnt = np.zeros(n_envs, dtype=np.int32)
+    rew = np.zeros((steps, n_envs))
+    done = np.zeros((steps, n_envs), dtype=np.int32)
+    pa = np.ascontiguousarray(pa, dtype=np.float32)
+    ea = np.ascontiguousarray(ea, dtype=np.float32)
+    rc = lib().orc_rollout(C.byref(p), envs, n_envs, steps, pa.ctypes.data_as(C.POINTER(C.c_float)),
+                           ea.ctypes.data_as(C.POINTER(C.c_float)),
+                           cnt.ctypes.data_as(C.POINTER(C.c_int32)), _dp(rew),
+                           done.ctypes.data_as(C.POINTER(C.c_int32)), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("oracle rollout error")
+    return rew, done
+
+
+# --------------------------------------------------------------------------
+# Learning-side restatements (ppo_continuous.py)
+# --------------------------------------------------------------------------
+def gae_flat(r, vs, vs_, dw, done, gamma=0.99, lamda=0.95):
+    """ppo_continuous.py:198-210 on one flat buffer (float32 like the reference)."""
+    r = np.asarray(r, np.float32).reshape(-1)
+    vs = np.asarray(vs, np.float32).reshape(-1)
+    vs_ = np.asarray(vs_, np.float32).reshape(-1)
+    dw = np.asarray(dw, np.float32).reshape(-1)
+    done = np.asarray(done, np.float32).reshape(-1)
+    # torch f32: r + (g*(1-dw))*vs_ - vs, python scalars rounded to f32
+    deltas = ((r + (np.float32(gamma) * (np.float32(1.0) - dw)) * vs_) - vs).astype(np.float32)
+    adv = np.zeros_like(deltas)
+    # gamma*lamda is a python float; times an np.float32 it rounds to f32 (NEP 50)
+    c = np.float32(gamma * lamda)
+    gae = np.float32(0.0)
+    for t in range(len(deltas) - 1, -1, -1):
+        gae = np.float32(deltas[t] + np.float32(np.float32(c * gae) * np.float32(np.float32(1.0) - done[t])))
+        adv[t] = gae
+    return adv
+
+
+def gae_time_major(r, vs, vs_, dw, done, gamma=0.99, lamda=0.95):
+    """Per-env reverse scan over T of [T, N] arrays; each column is one flat
+    reference buffer (ppo_continuous.py:204-206)."""
+    T, N = np.shape(r)
+    out = np.zeros((T, N), np.float32)
+    for i in range(N):
+        out[:, i] = gae_flat(r[:, i], vs[:, i], vs_[:, i], dw[:, i], done[:, i], gamma, lamda)
+    return out

@@ -1,0 +1,545 @@
+/*
+ * oracle/satenv_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (FP64, -ffp-contract=off) of the reference env hot path,
+ * one C function per reference function, each citing the reference
+ * file:line it follows (paths relative to the reference repo root).
+ *
+ * Floating-point orderings follow what numpy/OpenBLAS actually execute in
+ * the reference (probed in the build container, see DESIGN.md "Oracle"):
+ *   - np.dot / np.linalg.norm of 3-vectors (OpenBLAS ddot)  = fma chain
+ *     fma(x2,y2, fma(x1,y1, x0*y0))
+ *   - np.dot(M6x6, x6) (OpenBLAS dgemv_t, SkylakeX)          =
+ *     (((p0+p2)+(p1+p3))+p4)+p5 with p_j = M_ij*x_j
+ *   - np.linalg.norm of a float32 3-vector (OpenBLAS sdot)   =
+ *     f32 products summed in double, cast to float, sqrtf
+ *   - python/numpy SCALAR x ** 2                             = pow(x, 2.0)
+ * Transcendentals use glibc; numpy's SVML arccos/arctan differ from glibc
+ * by <=1 ulp on a few % of inputs, which the parity tests bound.
+ *
+ * fsolve -> MINPACK hybrd (scipy 1.15.3 scipy/optimize/__minpack.h, not part
+ * of the reference repo) is restated for n == 1 with fsolve's defaults
+ * (xtol 1.49012e-8, maxfev 400, epsfcn DBL_EPSILON, factor 100, mode 1).
+ */
+#include "satenv_oracle.h"
+#include <math.h>
+#include <float.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static const double ORC_PI = 3.141592653589793;      /* np.pi */
+static const double ORC_2PI = 6.283185307179586;     /* 2 * np.pi */
+
+/* ---- numpy/OpenBLAS primitive orderings ------------------------------ */
+static double dot3(const double a[3], const double b[3]) {
+    return fma(a[2], b[2], fma(a[1], b[1], a[0] * b[0]));
+}
+static double norm3(const double a[3]) { return sqrt(dot3(a, a)); }
+/* python/numpy scalar `x ** 2` is libm pow(x, 2.0) (not x*x: differs by 1 ulp
+ * on ~0.05% of inputs); numpy ARRAY ** 2 would be x*x. */
+static double sq2(double x) { return pow(x, 2.0); }
+static void cross3(const double a[3], const double b[3], double c[3]) {
+    /* numpy.cross, 3-vector path: cp0 = a1*b2 - a2*b1 ... */
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+static float norm3f(const float a[3]) {
+    double s = (double)(a[0] * a[0]);
+    s += (double)(a[1] * a[1]);
+    s += (double)(a[2] * a[2]);
+    return sqrtf((float)s);
+}
+
+/* ---- satellite_function.py:753-781 Clohessy_Wiltshire.State_transition_matrix */
+void orc_stm(double t, double M[36]) {
+    const double R = (double)((__int128)42164000 * 42164000 * 42164000);   /* r ** 3 */
+    const double omega = sqrt(3.986e14 / R);                                /* :761 */
+    const double tau = omega * t, s = sin(tau), c = cos(tau);
+    const double m[36] = {
+        4 - 3 * c, 0, 0, s / omega, 2 * (1 - c) / omega, 0,
+        6 * (s - tau), 1, 0, -2 * (1 - c) / omega, 4 * s / omega - 3 * tau, 0,  /* [1][4] as in :768 */
+        0, 0, c, 0, 0, s / omega,
+        3 * omega * s, 0, 0, c, 2 * s, 0,
+        6 * omega * (c - 1), 0, 0, -2 * s, 4 * c - 3, 0,
+        0, 0, -omega * s, 0, 0, c};
+    memcpy(M, m, sizeof(m));
+}
+
+static void stm_apply(const double M[36], const double x[6], double y[6]) {
+    for (int i = 0; i < 6; ++i) {
+        const double* r = M + 6 * i;
+        double p0 = r[0] * x[0], p1 = r[1] * x[1], p2 = r[2] * x[2];
+        double p3 = r[3] * x[3], p4 = r[4] * x[4], p5 = r[5] * x[5];
+        y[i] = (((p0 + p2) + (p1 + p3)) + p4) + p5;
+    }
+}
+
+/* ---- satellite_function.py:161-255 calculate_orbital_elements ---------- */
+int orc_orbital_elements(double miu, const double R0[3], const double V0[3], double out[6]) {
+    const double r_norm = norm3(R0), v_norm = norm3(V0), r_dot_v = dot3(R0, V0);
+    const double en = 2 / r_norm - sq2(v_norm) / miu;              /* :186 */
+    if (en == 0) return -5;                                        /* parabolic branch :253 */
+    const double a = 1 / fabs(en);                                 /* :188 */
+    const double c1 = sq2(v_norm) / miu - 1 / r_norm, c2 = r_dot_v / miu;
+    double E[3];
+    for (int k = 0; k < 3; ++k) E[k] = c1 * R0[k] - c2 * V0[k];    /* :193 */
+    const double e = norm3(E);
+    if (e == 0) return -4;                                         /* circular branch :251 */
+    double H[3], N[3];
+    cross3(R0, V0, H);                                             /* :197 */
+    const double h = norm3(H);
+    const double Z[3] = {0, 0, 1}, X[3] = {1, 0, 0}, Y[3] = {0, 1, 0};
+    cross3(Z, H, N);                                               /* :206 */
+    const double n = norm3(N);
+    const double inc = acos(dot3(Z, H) / h);                       /* :210 */
+    double omega;
+    if (n != 0 && e != 0) omega = acos(dot3(N, E) / n / e);        /* :214-217 */
+    else omega = 0.0;
+    if (dot3(Z, E) < 0) omega = ORC_2PI - omega;                   /* :221 */
+    double Omega = (n != 0) ? acos(dot3(X, N) / n) : 0.0;          /* :230-233 */
+    if (dot3(Y, N) < 0) Omega = ORC_2PI - Omega;                   /* :237 */
+    double f = acos(dot3(E, R0) / e / r_norm);                     /* :242 */
+    if (r_dot_v < 0) f = ORC_2PI - f;                              /* :243 */
+    out[0] = a; out[1] = e; out[2] = inc; out[3] = omega; out[4] = Omega; out[5] = f;
+    return 0;
+}
+
+/* ---- scalar MINPACK hybrd (n = 1), fsolve defaults ---------------------- */
+typedef struct { double A, sin_t, dvm; } alpha_fn;
+/* satellite_function.py:559-562 P_fai_equation; A is alpha-independent */
+static double p_fai(const alpha_fn* f, double alpha) {
+    return f->A * (f->dvm * cos(alpha)) + f->sin_t * (-f->dvm * sin(alpha));
+}
+
+static double hybrd1(const alpha_fn* fn, double x, int32_t* nfev_out) {
+    const double epsmch = DBL_EPSILON, xtol = 1.49012e-08, factor = 100.0;
+    const int maxfev = 400;
+    double fvec = p_fai(fn, x);
+    int nfev = 1;
+    double fnorm = fabs(fvec);
+    int iter = 1, ncsuc = 0, ncfail = 0, nslow1 = 0, nslow2 = 0;
+    double diag = 0, delta = 0, xnorm = 0, fjac = 0, r = 0, qtf = 0;
+    for (;;) {                                               /* outer loop */
+        int jeval = 1;
+        /* fdjac1, dense branch */
+        const double eps = sqrt(fmax(DBL_EPSILON, epsmch));
+        double hstep = eps * fabs(x);
+        if (hstep == 0) hstep = eps;
+        const double wa1f = p_fai(fn, x + hstep);
+        double J = (wa1f - fvec) / hstep;
+        nfev += 1;
+        /* qrfac (m = n = 1, no pivoting) */
+        const double acnorm = fabs(J);
+        double ajnorm = fabs(J);
+        double a = J;
+        if (ajnorm != 0) {
+            if (a < 0) ajnorm = -ajnorm;
+            a = a / ajnorm;
+            a = a + 1.0;
+        }
+        const double rdiag = -ajnorm;
+        if (iter == 1) {
+            diag = acnorm;
+            if (acnorm == 0) diag = 1.0;
+            xnorm = fabs(diag * x);
+            delta = factor * xnorm;
+            if (delta == 0) delta = factor;
+        }
+        /* qtf = Q^T fvec */
+        qtf = fvec;
+        if (a != 0) {
+            double sum = 0.0 + a * qtf;
+            double temp = -sum / a;
+            qtf = qtf + a * temp;
+        }
+        r = rdiag;
+        /* qform */
+        {
+            double wa = a;
+            double q = 1.0;
+            if (wa != 0) {
+                double sum = 0.0 + q * wa;
+                double temp = sum / wa;
+                q = q - temp * wa;
+            }
+            fjac = q;
+        }
+        diag = (diag > acnorm || acnorm != acnorm) ? diag : acnorm;   /* dmax1 */
+        for (;;) {                                           /* inner loop */
+            /* dogleg */
+            double p;
+            {
+                double temp = r;
+                if (temp == 0) {
+                    temp = fabs(r) > 0 ? fabs(r) : 0.0;
+                    temp = epsmch * temp;
+                    if (temp == 0) temp = epsmch;
+                }
+                double gn = (qtf - 0.0) / temp;
+                double qnorm = fabs(diag * gn);
+                if (qnorm <= delta) {
+                    p = gn;
+                } else {
+                    double w1 = 0.0 + r * qtf;
+                    w1 = w1 / diag;
+                    double gnorm = fabs(w1);
+                    double sgnorm = 0.0;
+                    double alpha = delta / qnorm;
+                    if (gnorm != 0) {
+                        w1 = (w1 / gnorm) / diag;
+                        double w2 = 0.0 + r * w1;
+                        double tn = fabs(w2);
+                        sgnorm = (gnorm / tn) / tn;
+                        alpha = 0.0;
+                        if (sgnorm < delta) {
+                            double bnorm = fabs(qtf);
+                            double dq = delta / qnorm, sd = sgnorm / delta;
+                            double t1 = (bnorm / gnorm) * (bnorm / qnorm) * sd;
+                            t1 = t1 - dq * (sd * sd) +
+                                 sqrt((t1 - dq) * (t1 - dq) + (1.0 - dq * dq) * (1.0 - sd * sd));
+                            alpha = (dq * (1.0 - sd * sd)) / t1;
+                        }
+                    }
+                    double t2 = (1.0 - alpha) * (sgnorm < delta ? sgnorm : delta);
+                    p = t2 * w1 + alpha * gn;
+                }
+            }
+            const double w1 = -p;
+            double w2 = x + w1;
+            const double w3s = diag * w1;
+            const double pnorm = fabs(w3s);
+            if (iter == 1) delta = (delta < pnorm) ? delta : pnorm;
+            const double wa4 = p_fai(fn, w2);
+            nfev += 1;
+            const double fnorm1 = fabs(wa4);
+            double actred = -1.0;
+            if (fnorm1 < fnorm) actred = 1.0 - (fnorm1 / fnorm) * (fnorm1 / fnorm);
+            const double w3 = qtf + (0.0 + r * w1);
+            const double tq = fabs(w3);
+            double prered = 0.0;
+            if (tq < fnorm) prered = 1.0 - (tq / fnorm) * (tq / fnorm);
+            double ratio = 0.0;
+            if (prered > 0) ratio = actred / prered;
+            if (ratio < 0.1) {
+                ncsuc = 0; ncfail += 1; delta = 0.5 * delta;
+            } else {
+                ncfail = 0; ncsuc += 1;
+                if (ratio >= 0.5 || ncsuc > 1) {
+                    double t = pnorm / 0.5;
+                    delta = (delta > t || t != t) ? delta : t;
+                }
+                if (fabs(ratio - 1.0) <= 0.1) delta = pnorm / 0.5;
+            }
+            if (ratio >= 1e-4) {
+                x = w2;
+                w2 = diag * x;
+                fvec = wa4;
+                xnorm = fabs(w2);
+                fnorm = fnorm1;
+                iter += 1;
+            }
+            nslow1 += 1;
+            if (actred >= 0.001) nslow1 = 0;
+            if (jeval) nslow2 += 1;
+            if (ratio >= 0.1) nslow2 = 0;
+            if (delta <= xtol * xnorm || fnorm == 0) goto done;
+            {
+                int info = 0;
+                if (nfev >= maxfev) info = 2;
+                double m1 = 0.1 * delta;
+                double mx = (m1 > pnorm || pnorm != pnorm) ? m1 : pnorm;
+                if (0.1 * mx <= epsmch * xnorm) info = 3;
+                if (nslow2 == 5) info = 4;
+                if (nslow1 == 10) info = 5;
+                if (info) goto done;
+            }
+            if (ncfail == 2) break;                          /* re-evaluate jacobian */
+            {
+                double sum = 0.0 + fjac * wa4;
+                double v = (sum - w3) / pnorm;
+                double u = diag * ((diag * w1) / pnorm);
+                if (ratio >= 1e-4) qtf = sum;
+                r = r + v * u;                               /* r1updt, n = 1 */
+            }
+            jeval = 0;
+        }
+    }
+done:
+    if (nfev_out) *nfev_out = nfev;
+    return x;
+}
+
+double orc_solve_alpha(double u, double dvm, double theta, double v1x, double v1y, double h,
+                       double guess, int32_t* nfev) {
+    alpha_fn fn;
+    /* satellite_function.py:560: ((2*u*(1-cos t))/(h*v1y) - v1x*sin t/v1y) */
+    fn.A = (2 * u * (1 - cos(theta))) / (h * v1y) - v1x * sin(theta) / v1y;
+    fn.sin_t = sin(theta);
+    fn.dvm = dvm;
+    return hybrd1(&fn, guess, nfev);
+}
+
+/* ---- satellite_function.py:18-99 + 317-373 + 462-556 -------------------- */
+typedef struct {
+    double u, dv2;
+    double a_c, e_c, i_c, omega_c, Omega_c, f0_c, r_c, p_c;
+    double a_t, e_t, i_t, omega_t, Omega_t, f0_t, r_t, p_t;
+} tw_state;
+
+static double fuel_sq(double fuel, int mode) {     /* self.Delta_V_c ** 2 by numpy type */
+    if (mode == ORC_F32) return (double)powf((float)fuel, 2.0f);   /* np.float32 ** 2 */
+    if (mode == ORC_F64) return sq2(fuel);
+    return fuel * fuel;                                          /* int ** 2, exact */
+}
+
+/* satellite_function.py:462-556 rf_extreme_point('orbit_c1'/'orbit_c2') */
+static void rf_extreme_point(const tw_state* s, double f_c, double* rf_max_o, double* rf_min_o) {
+    const double u = s->u, e = s->e_c, f0 = s->f0_c, p = s->p_c;
+    const double d = f_c - s->f0_c;
+    const double X = 1 + e * cos(f0);
+    const double sd = sin(d);
+    const double temp1 = sq2(sd) / (u * sq2(X) / (p * s->dv2) - 1);        /* :466 */
+    if (!(0 <= temp1)) { *rf_max_o = 0; *rf_min_o = 0; return; }           /* :477-478 */
+    const double fai = 0.0;
+    const double beta = atan(tan(fai) / sd);                               /* :469 */
+    const double sb = sin(beta);
+    const double dvm = sqrt(s->dv2 - u * sq2(X) * sq2(sb) / p);            /* :470 */
+    double theta = 0;
+    if ((-2 * ORC_PI <= d && d < -ORC_PI) || (0 <= d && d < ORC_PI))       /* :473 */
+        theta = acos(cos(d) * cos(fai));
+    else if ((-ORC_PI <= d && d < 0) || (ORC_PI <= d && d < 2 * ORC_PI))  /* :475 */
+        theta = ORC_2PI - acos(cos(d) * cos(fai));
+    const double sq = sqrt(u / p);
+    double rf[2];
+    for (int k = 0; k < 2; ++k) {
+        const double ag = (k == 0) ? ORC_PI / 2 : -ORC_PI / 2;            /* :516, :534 */
+        const double v1x = sq * e * sin(f0) + dvm * cos(ag);               /* :518 */
+        const double v1y = sq * X * cos(beta) + dvm * sin(ag);             /* :519 */
+        const double h = s->r_c * v1y;                                     /* :521 */
+        const double al = orc_solve_alpha(u, dvm, theta, v1x, v1y, h, ag, 0);
+        const double vx = sq * e * sin(f0) + dvm * cos(al);               /* :525 */
+        const double vy = sq * X * cos(beta) + dvm * sin(al);
+        const double hm = s->r_c * vy;
+        rf[k] = sq2(hm) / (u * (1 - cos(theta)) + hm * vy * cos(theta) - hm * vx * sin(theta));
+    }
+    double rmax = fabs(rf[0]), rmin = fabs(rf[1]);                         /* :549-554 */
+    if (rmax < rmin) { double t = rmin; rmin = rmax; rmax = t; }
+    *rf_max_o = rmax; *rf_min_o = rmin;
+}
+
+int orc_danger_zone(const double R0_c[3], const double V0_c[3], const double R0_t[3],
+                    const double V0_t[3], double fuel, int32_t fuel_mode, int32_t* count) {
+    tw_state s;
+    double el[6];
+    s.u = 3.986e14;
+    s.dv2 = fuel_sq(fuel, fuel_mode);
+    int rc = orc_orbital_elements(s.u, R0_c, V0_c, el);                    /* :52 */
+    if (rc) return rc;
+    s.a_c = el[0]; s.e_c = el[1]; s.i_c = el[2]; s.omega_c = el[3]; s.Omega_c = el[4]; s.f0_c = el[5];
+    s.r_c = s.a_c * (1 - sq2(s.e_c)) / (1 + s.e_c * cos(s.f0_c));          /* :57 */
+    s.p_c = s.a_c * (1 - sq2(s.e_c));                                      /* :58 */
+    rc = orc_orbital_elements(s.u, R0_t, V0_t, el);                        /* :81 */
+    if (rc) return rc;
+    s.a_t = el[0]; s.e_t = el[1]; s.i_t = el[2]; s.omega_t = el[3]; s.Omega_t = el[4]; s.f0_t = el[5];
+    s.r_t = s.a_t * (1 - sq2(s.e_t)) / (1 + s.e_t * cos(s.f0_t));
+    s.p_t = s.a_t * (1 - sq2(s.e_t));
+    /* :317-339 calculate_latitudinal_angle */
+    double temp1 = (sin(s.i_t) * sin(s.Omega_c - s.Omega_t)) /
+                   (cos(s.i_t) * sin(s.i_c) - sin(s.i_t) * cos(s.i_c) * cos(s.Omega_c - s.Omega_t));
+    double temp2 = (sin(s.i_c) * sin(s.Omega_t - s.Omega_c)) /
+                   (cos(s.i_c) * sin(s.i_t) - sin(s.i_c) * cos(s.i_t) * cos(s.Omega_t - s.Omega_c));
+    if (isnan(temp1) || isnan(temp2)) temp1 = temp2 = 1;                   /* :331-332 */
+    const double u_c1 = atan(temp1), u_c2 = ORC_PI + u_c1;
+    const double u_t1 = atan(temp2), u_t2 = u_t1 + ORC_PI;
+    /* :341-373 calculate_number_of_hanger_area */
+    const double f_c1 = u_c1 - s.omega_c, f_c2 = u_c2 - s.omega_c;
+    const double f_t1 = u_t1 - s.omega_t, f_t2 = u_t2 - s.omega_t;
+    double mx1, mn1, mx2, mn2;
+    rf_extreme_point(&s, f_c1, &mx1, &mn1);
+    rf_extreme_point(&s, f_c2, &mx2, &mn2);
+    const double r_ft1 = (s.a_t * (1 - sq2(s.e_t))) / (1 + s.e_t * cos(f_t2));      /* :363 (cross-wired) */
+    const double r_ft2 = (s.a_t * (1 - sq2(s.e_t))) / (1 + s.e_t * cos(f_t1));      /* :365 */
+    const int in1 = (mn1 <= r_ft1 && r_ft1 <= mx1), in2 = (mn2 <= r_ft2 && r_ft2 <= mx2);
+    *count = (in1 && in2) ? 2 : ((in1 || in2) ? 1 : 0);
+    return 0;
+}
+
+/* ---- environment.py ------------------------------------------------------- */
+void orc_default_params(orc_params* p, double d_capture, int32_t max_episode_steps) {
+    p->d_capture = d_capture;            /* train_* overwrite env.d_capture (CPPO_main.py:98) */
+    p->d_range = 100000;                 /* environment.py:28 */
+    p->win_reward = 100; p->burn_reward = 0;          /* :39-40 */
+    p->max_episode_steps = max_episode_steps;         /* :46 */
+    p->mu = 3.986e14;
+    p->R_cw[0] = 27098000; p->R_cw[1] = 32306000; p->R_cw[2] = 0;   /* :338 */
+    p->V_cw[0] = -2350; p->V_cw[1] = 1970; p->V_cw[2] = 0;          /* :339 */
+    orc_stm(100, p->stm);                                            /* :121 */
+}
+
+void orc_env_init(orc_env* e) {
+    memset(e, 0, sizeof(*e));
+    e->fuel_c = 320; e->fuel_t = 320;                 /* :42-43 */
+    e->fuel_c_mode = ORC_PYINT; e->fuel_t_mode = ORC_PYINT;
+    e->dis = INFINITY;                                /* :44 */
+    e->dz = 0;                                        /* :41 */
+    e->vel_int = 1;
+}
+
+static void make_obs(const orc_env* e, double obs[18]) {   /* environment.py:76-77 */
+    for (int k = 0; k < 3; ++k) {
+        obs[k] = e->Pp[k] - e->Ep[k];
+        obs[3 + k] = e->Pv[k] - e->Ev[k];
+        obs[6 + k] = e->Pp[k]; obs[9 + k] = e->Pv[k];
+        obs[12 + k] = e->Ep[k]; obs[15 + k] = e->Ev[k];
+    }
+}
+
+void orc_reset(orc_env* e, int32_t flag, double obs[18]) {          /* environment.py:66-79 */
+    for (int k = 0; k < 3; ++k) { e->Pp[k] = 0; e->Pv[k] = 0; e->Ep[k] = 0; e->Ev[k] = 0; }
+    e->Pp[0] = 200000; e->Ep[0] = 18000;
+    e->vel_int = 1;
+    e->flag = flag;
+    if (obs) make_obs(e, obs);
+}
+
+static float clipf(float a) {                                        /* np.clip(a,-1.6,1.6) in f32 */
+    const float lo = -1.6f, hi = 1.6f;
+    return a < lo ? lo : (a > hi ? hi : a);
+}
+
+/* fuel -= |a0|+|a1|+|a2| with numpy scalar promotion (environment.py:106-107, :200-203) */
+static void fuel_sub(double* fuel, int32_t* mode, int zero_int_action, float s32) {
+    if (zero_int_action) {              /* action list [0,0,0]: np.int64(0) */
+        if (*mode == ORC_PYINT) *mode = ORC_I64;
+        else if (*mode == ORC_F32) *mode = ORC_F64;
+        return;                         /* value unchanged */
+    }
+    switch (*mode) {
+    case ORC_PYINT: case ORC_F32: *fuel = (double)((float)*fuel - s32); *mode = ORC_F32; break;
+    case ORC_I64: case ORC_F64: default: *fuel = *fuel - (double)s32; *mode = ORC_F64; break;
+    }
+}
+
+static void add_dv(double v[3], const float a[3], int vel_int) {  /* Vector[i] += action[i] */
+    for (int k = 0; k < 3; ++k) {
+        double t = v[k] + (double)a[k];
+        v[k] = vel_int ? trunc(t) : t;                            /* int64 array truncates */
+    }
+}
+
+/* environment.py:346-396 reward_of_action1..4 */
+static double cos_sim(const double a[3], const double b[3]) {
+    double na = norm3(a), nb = norm3(b);
+    double ua[3] = {a[0] / na, a[1] / na, a[2] / na};
+    double ub[3] = {b[0] / nb, b[1] / nb, b[2] / nb};
+    return dot3(ua, ub);
+}
+static double reward_of_action4(const double rel[3], const float act[3], int zeroed) {
+    if (zeroed) return 0;                                          /* [0,0,0] list */
+    if (!(act[0] != 0 && act[1] != 0 && act[2] != 0)) return 0;   /* :388 */
+    double nr = norm3(rel);
+    double ur[3] = {rel[0] / nr, rel[1] / nr, rel[2] / nr};
+    float na = norm3f(act);
+    double ua[3] = {(double)(act[0] / na), (double)(act[1] / na), (double)(act[2] / na)};
+    return -dot3(ur, ua);
+}
+
+int orc_step(const orc_params* p, orc_env* e, const float pa_in[3], const float ea_in[3],
+             int32_t episode_count, double obs[18], double* reward, int32_t* done) {
+    float pa[3], ea[3];
+    for (int k = 0; k < 3; ++k) { pa[k] = clipf(pa_in[k]); ea[k] = clipf(ea_in[k]); }
+    double rel[3] = {e->Pp[0] - e->Ep[0], e->Pp[1] - e->Ep[1], e->Pp[2] - e->Ep[2]};
+    const double dis_prev = norm3(rel);                            /* :89 */
+    int p_zero = 0, e_zero = 0;
+    const int flag = e->flag;
+    if (flag == 0) {
+        if (e->dis < p->d_range && e->dz != 0) {                   /* :91-97 */
+            add_dv(e->Ev, ea, e->vel_int);
+            p_zero = 1;
+        } else {                                                   /* :98-104 */
+            add_dv(e->Pv, pa, e->vel_int);
+            add_dv(e->Ev, ea, e->vel_int);
+        }
+    } else {
+        if (e->dz != 0) {                                          /* :190-193 */
+            add_dv(e->Pv, pa, e->vel_int);
+            add_dv(e->Ev, ea, e->vel_int);
+        } else {                                                   /* :194-198 */
+            add_dv(e->Pv, pa, e->vel_int);
+            e_zero = 1;
+        }
+    }
+    float sp = (fabsf(pa[0]) + fabsf(pa[1])) + fabsf(pa[2]);
+    float se = (fabsf(ea[0]) + fabsf(ea[1])) + fabsf(ea[2]);
+    fuel_sub(&e->fuel_c, &e->fuel_c_mode, p_zero, sp);             /* :106 */
+    fuel_sub(&e->fuel_t, &e->fuel_t_mode, e_zero, se);             /* :107 */
+    /* CW STM :117-121, :130-132 */
+    double xc[6] = {e->Pp[0], e->Pp[1], e->Pp[2], e->Pv[0], e->Pv[1], e->Pv[2]};
+    double xt[6] = {e->Ep[0], e->Ep[1], e->Ep[2], e->Ev[0], e->Ev[1], e->Ev[2]};
+    double yc[6], yt[6];
+    stm_apply(p->stm, xc, yc);
+    stm_apply(p->stm, xt, yt);
+    for (int k = 0; k < 3; ++k) {
+        e->Pp[k] = yc[k]; e->Pv[k] = yc[3 + k]; e->Ep[k] = yt[k]; e->Ev[k] = yt[3 + k];
+    }
+    e->vel_int = 0;
+    for (int k = 0; k < 3; ++k) rel[k] = e->Pp[k] - e->Ep[k];
+    e->dis = norm3(rel);
+    make_obs(e, obs);
+    if (e->dis <= p->d_capture) {                                   /* :139-142, :221-225 */
+        *reward = (flag == 0) ? p->win_reward : -150.0; *done = 1; return 0;
+    }
+    if (episode_count >= p->max_episode_steps) {                    /* :144-147, :227-231 */
+        *reward = (flag == 0) ? p->burn_reward : p->win_reward; *done = 1; return 0;
+    }
+    /* :317-332 calculate_number_hanger_area */
+    double Rc[3], Vc[3], Rt[3], Vt[3];
+    for (int k = 0; k < 3; ++k) {
+        Rc[k] = p->R_cw[k] + e->Pp[k]; Vc[k] = p->V_cw[k] + e->Pv[k];
+        Rt[k] = p->R_cw[k] + e->Ep[k]; Vt[k] = p->V_cw[k] + e->Ev[k];
+    }
+    int32_t cnt = 0;
+    int rc = orc_danger_zone(Rc, Vc, Rt, Vt, e->fuel_c, e->fuel_c_mode, &cnt);
+    if (rc) return rc;
+    e->dz = cnt;
+    /* :161-175 shaped reward */
+    double r = (e->dis < dis_prev) ? 1 : -1;
+    r += (p->d_capture <= e->dis && e->dis <= 4 * p->d_capture) ? -1 : -2;
+    r += (e->dz == 0) ? -1 : e->dz * 0.5;
+    const double pv1 = cos_sim(e->Pp, e->Ep);                      /* reward_of_action3 */
+    const double pv2 = cos_sim(e->Pv, e->Ev);                      /* reward_of_action1 */
+    const double pv3 = cos_sim(rel, e->Pv);                        /* reward_of_action2 */
+    const double pv4 = reward_of_action4(rel, pa, p_zero);
+    r += 1 * pv1;
+    r += 0.6 * pv2;
+    r += 0.2 * pv3;
+    r += 2 * pv4;
+    *reward = (flag == 0) ? r : -r;                                /* :251 */
+    *done = 0;
+    return 0;
+}
+
+int orc_rollout(const orc_params* p, orc_env* envs, int64_t n, int32_t steps, const float* pa,
+                const float* ea, int32_t* episode_count, double* reward_out, int32_t* done_out,
+                int32_t nthreads) {
+    int err = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static) reduction(| : err)
+#endif
+    for (int64_t i = 0; i < n; ++i) {
+        double obs[18];
+        for (int32_t t = 0; t < steps; ++t) {
+            const int64_t k = (int64_t)t * n + i;
+            episode_count[i] += 1;
+            double r; int32_t d;
+            err |= (orc_step(p, &envs[i], pa + 3 * k, ea + 3 * k, episode_count[i], obs, &r, &d) != 0);
+            reward_out[k] = r; done_out[k] = d;
+            if (d) { orc_reset(&envs[i], envs[i].flag, obs); episode_count[i] = 0; }
+        }
+    }
+    return err ? -1 : 0;
+}
