@@ -1,0 +1,123 @@
+/*
+ * satenv.h -- C ABI of the MI355X vectorised satellite pursuit-evasion
+ * environment (one HIP lane per env, FP64 SoA state resident in HBM).
+ *
+ * Drop-in boundary for the reference's environment object
+ * (qiaobeibei/PPO-RL-Satellite environment.py):
+ *   satenv_create / satenv_set_params  <- satellites.__init__   environment.py:26-62
+ *   satenv_reset                       <- satellites.reset      environment.py:66-79
+ *   satenv_step                        <- satellites.step       environment.py:81-255 (Flag 0, 1)
+ *   satenv_step_autoreset              <- the CPPO_main.py:119-153 inner loop around step/reset
+ *   satenv_get_state / satenv_set_state<- attribute access (Pursuer_position, fuel_c, dis, ...)
+ *   satenv_default_params / satenv_stm <- ctor defaults + Clohessy_Wiltshire.State_transition_matrix
+ *                                          satellite_function.py:753-781
+ *
+ * Conventions: every pointer argument is a caller-owned DEVICE buffer unless
+ * stated otherwise; calls are asynchronous on `stream` (a hipStream_t, NULL =
+ * default stream) and capturable into a hipGraph; one handle per stream,
+ * not thread-safe.  Return 0 on success or a negative SATENV_ERR_* code
+ * (message via satenv_last_error()).  Device-side failures (the reference's
+ * crashing 4/5-element orbit branches) are sticky and reported by
+ * satenv_check().
+ */
+#ifndef SATENV_H
+#define SATENV_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SATENV_ABI_VERSION 1
+#define SATENV_OBS_DIM 18    /* [Pp-Ep, Pv-Ev, Pp, Pv, Ep, Ev]  environment.py:76-77 */
+#define SATENV_ACT_DIM 3
+#define SATENV_F64_PLANES 15 /* Pp[3] Pv[3] Ep[3] Ev[3] fuel_c fuel_t dis, each [num_envs] */
+#define SATENV_I32_PLANES 3  /* dangerous_zone, episode_count, bits (see below) */
+
+enum {
+    SATENV_OK = 0,
+    SATENV_ERR_ARG = -1,
+    SATENV_ERR_HIP = -2,
+    SATENV_ERR_ORBIT_CIRCULAR = -4,  /* calculate_orbital_elements e == 0 (satellite_function.py:251) */
+    SATENV_ERR_ORBIT_PARABOLIC = -5, /* 2/r - v^2/mu == 0 (satellite_function.py:253) */
+};
+
+/* numpy scalar type carried by the reference's fuel attributes; bits plane:
+ * [1:0] fuel_c type, [3:2] fuel_t type, [4] velocities are int64 (fresh
+ * after reset), [5] Flag (0 pursuer training, 1 evader training).        */
+enum { SATENV_NUM_PYINT = 0, SATENV_NUM_I64 = 1, SATENV_NUM_F32 = 2, SATENV_NUM_F64 = 3 };
+
+typedef struct satenv_params {
+    double d_capture;          /* environment.py:35; train_* overwrite it (CPPO_main.py:98)  */
+    double d_range;            /* environment.py:45 (ctor default 100000)                    */
+    double win_reward;         /* environment.py:40                                          */
+    double burn_reward;        /* environment.py:39                                          */
+    double mu;                 /* 3.986e14                                                    */
+    double R_cw[3], V_cw[3];   /* CW reference point, environment.py:338-339                 */
+    double stm[36];            /* row-major 6x6 STM, satellite_function.py:766-773, t=100 s  */
+    double fuel_c0, fuel_t0;   /* environment.py:42-43 (ctor 320)                             */
+    double init_kin[12];       /* ctor Pursuer/Escaper position, vector (environment.py:26-27)*/
+    int32_t max_episode_steps; /* args.max_episode_steps, environment.py:46                  */
+    int32_t flag;              /* Flag, environment.py:36                                     */
+    int32_t fuel_c0_mode;      /* SATENV_NUM_* of fuel_c0 (ctor: python int)                  */
+    int32_t fuel_t0_mode;
+} satenv_params;
+
+typedef struct satenv_env satenv_env;   /* opaque */
+
+/* host-only helpers */
+int satenv_default_params(satenv_params* p);
+int satenv_stm(double t, double* out36);          /* host pointer, row-major */
+const char* satenv_last_error(void);
+int satenv_abi_version(void);
+
+int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, int device);
+int satenv_destroy(satenv_env* h);
+int satenv_num_envs(const satenv_env* h, int64_t* n);                /* host int64 */
+int satenv_set_params(satenv_env* h, const satenv_params* p);        /* host struct */
+
+/* reset(Flag) for the envs whose env_mask byte is non-zero (NULL = all);
+ * writes obs of ALL envs (f32 [N][18] and/or f64 [N][18], either nullable). */
+int satenv_reset(satenv_env* h, int32_t flag, const uint8_t* env_mask, float* obs_out, double* obs64_out,
+                 void* stream);
+
+/* step(pursuer_action, escaper_action, epsiode_count) for all envs.
+ * pa/ea: f32 [N][3]; episode_count: int32 [N] (NULL = use and advance the
+ * device-side counters).  Outputs (nullable): obs f32 [N][18], obs f64
+ * [N][18], reward f64 [N], done u8 [N].  No automatic reset.              */
+int satenv_step(satenv_env* h, const float* pa, const float* ea, const int32_t* episode_count, float* obs_out,
+                double* obs64_out, double* reward_out, uint8_t* done_out, void* stream);
+
+/* vectorised training-loop step: episode counters live on the device; a
+ * done env is reset (Flag kept) inside the same kernel and obs_out carries
+ * the post-reset observation (what the policy sees next).  reward_out f32
+ * [N] as stored by ReplayBuffer (replaybuffer.py:34).  stats_out (nullable,
+ * f64[4], accumulated with atomics): finished episodes, sum of their
+ * returns, sum of rewards, captures.                                       */
+int satenv_step_autoreset(satenv_env* h, const float* pa, const float* ea, float* obs_out, float* reward_out,
+                          uint8_t* done_out, double* stats_out, void* stream);
+
+/* state transfer (device buffers): f64 [SATENV_F64_PLANES][N], i32 [SATENV_I32_PLANES][N] */
+int satenv_get_state(const satenv_env* h, double* f64_planes, int32_t* i32_planes, void* stream);
+int satenv_set_state(satenv_env* h, const double* f64_planes, const int32_t* i32_planes, void* stream);
+
+/* Time_window_of_danger_zone(R0_c, V0_c, R0_t, V0_t, Delta_V_c=fuel)
+ *   .calculate_number_of_hanger_area()   satellite_function.py:18-99,341-373
+ * on n independent absolute states: states f64 [n][12] = R_c V_c R_t V_t,
+ * fuel f64 [n], fuel_mode i32 [n] (SATENV_NUM_*), count_out i32 [n] (a
+ * negative entry = unsupported orbit branch).                              */
+int satenv_danger_zone(int64_t n, const double* states, const double* fuel, const int32_t* fuel_mode,
+                       int32_t* count_out, void* stream);
+
+/* Time_window_of_danger_zone.Numerical_iteration_method(Delta_Vm, theta,
+ * v_1x, v_1y, h, alpha_guess)  satellite_function.py:558-565 (fsolve) on n
+ * independent inputs: in f64 [n][6], alpha_out f64 [n].                    */
+int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* stream);
+
+/* synchronises the handle's device; *status = first sticky device error (0 = none) */
+int satenv_check(satenv_env* h, int32_t* status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SATENV_H */

@@ -1,0 +1,336 @@
+// satenv_device.h -- FP64 device math of one environment step, one lane per env.
+//
+// MI355X-native restatement of the reference env hot path:
+//   environment.py:81-255  satellites.step (Flag 0 / Flag 1)
+//   satellite_function.py:753-781  Clohessy_Wiltshire.State_transition_matrix(100)
+//   satellite_function.py:18-99,161-255,317-373,462-565  danger-zone count
+//   scipy.optimize.fsolve -> MINPACK hybrd (n = 1, fsolve defaults)
+//
+// Numerics contract (see DESIGN.md "Parity"): every product/sum the
+// reference evaluates through numpy/OpenBLAS is reproduced in the same
+// order, incl. the FMA chain of OpenBLAS ddot and the dgemv_t summation
+// tree; the file is compiled with -ffp-contract=off so nothing else fuses.
+// Transcendentals are OCML (gfx950), which differs from the reference's
+// numpy/glibc libm by <= 1-2 ulp; parity is therefore a tolerance on
+// continuous outputs and exact on counts/done except libm-sensitive ties.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "satenv.h"
+
+namespace satenv {
+
+constexpr double kPi = 3.141592653589793;    // np.pi
+constexpr double kTwoPi = 6.283185307179586; // 2 * np.pi
+constexpr double kEpsMch = 2.220446049250313e-16;
+
+// numpy scalar type of the reference's fuel attributes (environment.py:106-107)
+enum : int { kPyInt = 0, kI64 = 1, kF32 = 2, kF64 = 3 };
+
+// per-env int "bits" plane: [1:0] fuel_c mode, [3:2] fuel_t mode, [4] vel_int, [5] flag
+__device__ __forceinline__ int fc_mode(int b) { return b & 3; }
+__device__ __forceinline__ int ft_mode(int b) { return (b >> 2) & 3; }
+__device__ __forceinline__ int vel_int(int b) { return (b >> 4) & 1; }
+__device__ __forceinline__ int env_flag(int b) { return (b >> 5) & 1; }
+__device__ __forceinline__ int make_bits(int fc, int ft, int vi, int flag) {
+  return (fc & 3) | ((ft & 3) << 2) | ((vi & 1) << 4) | ((flag & 1) << 5);
+}
+
+using Params = satenv_params;   // include/satenv.h
+
+// OpenBLAS ddot, n = 3 (numpy np.dot / np.linalg.norm of 3-vectors)
+__device__ __forceinline__ double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
+  return fma(a2, b2, fma(a1, b1, a0 * b0));
+}
+__device__ __forceinline__ double norm3(double a0, double a1, double a2) {
+  return sqrt(dot3(a0, a1, a2, a0, a1, a2));
+}
+
+// ---------------------------------------------------------------------------
+// satellite_function.py:161-255 calculate_orbital_elements (6-element branch)
+// returns 0, or -4 (e == 0: circular branch) / -5 (parabolic branch): the
+// reference leaves attributes unset there and crashes later.
+// ---------------------------------------------------------------------------
+struct Elements { double a, e, i, omega, Omega, f; };
+
+__device__ __forceinline__ int orbital_elements(double mu, double R0, double R1, double R2, double V0,
+                                                double V1, double V2, Elements& out) {
+  const double r_norm = norm3(R0, R1, R2);
+  const double v_norm = norm3(V0, V1, V2);
+  const double r_dot_v = dot3(R0, R1, R2, V0, V1, V2);
+  const double v2 = v_norm * v_norm;                       // v_norm ** 2
+  const double en = 2.0 / r_norm - v2 / mu;                // :186
+  if (en == 0.0) return -5;
+  out.a = 1.0 / fabs(en);                                  // :188
+  const double c1 = v2 / mu - 1.0 / r_norm, c2 = r_dot_v / mu;
+  const double E0 = c1 * R0 - c2 * V0, E1 = c1 * R1 - c2 * V1, E2 = c1 * R2 - c2 * V2;   // :193
+  const double e = norm3(E0, E1, E2);
+  if (e == 0.0) return -4;
+  out.e = e;
+  // H = R x V (numpy.cross order), N = Z x H = [-H1, H0, 0]
+  const double H0 = R1 * V2 - R2 * V1, H1 = R2 * V0 - R0 * V2, H2 = R0 * V1 - R1 * V0;
+  const double h = norm3(H0, H1, H2);
+  const double N0 = 0.0 * H2 - 1.0 * H1, N1 = 1.0 * H0 - 0.0 * H2, N2 = 0.0 * H1 - 0.0 * H0;
+  const double n = norm3(N0, N1, N2);
+  out.i = acos(dot3(0.0, 0.0, 1.0, H0, H1, H2) / h);       // :210
+  double omega = (n != 0.0) ? acos(dot3(N0, N1, N2, E0, E1, E2) / n / e) : 0.0;   // :214-217
+  if (dot3(0.0, 0.0, 1.0, E0, E1, E2) < 0.0) omega = kTwoPi - omega;               // :221
+  double Omega = (n != 0.0) ? acos(dot3(1.0, 0.0, 0.0, N0, N1, N2) / n) : 0.0;      // :230-233
+  if (dot3(0.0, 1.0, 0.0, N0, N1, N2) < 0.0) Omega = kTwoPi - Omega;                // :237
+  double f = acos(dot3(E0, E1, E2, R0, R1, R2) / e / r_norm);                       // :242
+  if (r_dot_v < 0.0) f = kTwoPi - f;                                                // :243
+  out.omega = omega;
+  out.Omega = Omega;
+  out.f = f;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// fsolve(P_fai_equation, guess): MINPACK hybrd specialised to n = 1 with
+// scipy's fsolve defaults (xtol 1.49012e-8, maxfev 400, epsfcn = eps,
+// factor 100, mode 1).  Residual (satellite_function.py:559-562):
+//   g(a) = A * (dvm * cos a) + sin_t * (-dvm * sin a)
+// with A = (2u(1-cos t))/(h v1y) - v1x sin t / v1y hoisted (bit-neutral).
+// Bounded: every path increments nfev and stops at 400.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double resid(double A, double st, double dvm, double a) {
+  double s, c;
+  sincos(a, &s, &c);
+  return A * (dvm * c) + st * (-dvm * s);
+}
+
+__device__ __noinline__ double hybrd1(double A, double st, double dvm, double x) {
+  const double xtol = 1.49012e-08, factor = 100.0;
+  const double eps = 1.4901161193847656e-08;               // sqrt(max(epsfcn, epsmch))
+  double fvec = resid(A, st, dvm, x);
+  int nfev = 1;
+  double fnorm = fabs(fvec);
+  int iter = 1, ncsuc = 0, ncfail = 0, nslow1 = 0, nslow2 = 0;
+  double diag = 0.0, delta = 0.0, xnorm = 0.0;
+  for (;;) {
+    // fdjac1 (forward difference), qrfac, qform for a 1x1 Jacobian
+    double hs = eps * fabs(x);
+    if (hs == 0.0) hs = eps;
+    const double J = (resid(A, st, dvm, x + hs) - fvec) / hs;
+    nfev += 1;
+    const double acnorm = fabs(J);
+    double ajnorm = acnorm, a = J;
+    if (ajnorm != 0.0) {
+      if (a < 0.0) ajnorm = -ajnorm;
+      a = a / ajnorm + 1.0;
+    }
+    if (iter == 1) {
+      diag = (acnorm == 0.0) ? 1.0 : acnorm;
+      xnorm = fabs(diag * x);
+      delta = factor * xnorm;
+      if (delta == 0.0) delta = factor;
+    }
+    double qtf = fvec, fjac = 1.0;
+    if (a != 0.0) {
+      const double t = -(0.0 + a * qtf) / a;
+      qtf = qtf + a * t;
+      fjac = 1.0 - ((0.0 + 1.0 * a) / a) * a;
+    }
+    double r = -ajnorm;
+    diag = (diag > acnorm || acnorm != acnorm) ? diag : acnorm;
+    bool jeval = true;
+    for (;;) {
+      // dogleg
+      double tr = r;
+      if (tr == 0.0) tr = kEpsMch;                         // epsmch*max|r| == 0 -> epsmch
+      const double gn = (qtf - 0.0) / tr;
+      const double qnorm = fabs(diag * gn);
+      double p;
+      if (qnorm <= delta) {
+        p = gn;
+      } else {
+        double w1 = (0.0 + r * qtf) / diag;
+        const double gnorm = fabs(w1);
+        double sg = 0.0, al = delta / qnorm;
+        if (gnorm != 0.0) {
+          w1 = (w1 / gnorm) / diag;
+          const double tn = fabs(0.0 + r * w1);
+          sg = (gnorm / tn) / tn;
+          al = 0.0;
+          if (sg < delta) {
+            const double bn = fabs(qtf), dq = delta / qnorm, sd = sg / delta;
+            double t1 = (bn / gnorm) * (bn / qnorm) * sd;
+            t1 = t1 - dq * (sd * sd) + sqrt((t1 - dq) * (t1 - dq) + (1.0 - dq * dq) * (1.0 - sd * sd));
+            al = (dq * (1.0 - sd * sd)) / t1;
+          }
+        }
+        p = ((1.0 - al) * (sg < delta ? sg : delta)) * w1 + al * gn;
+      }
+      const double w1 = -p;
+      const double w2 = x + w1;
+      const double pnorm = fabs(diag * w1);
+      if (iter == 1) delta = (delta < pnorm) ? delta : pnorm;
+      const double wa4 = resid(A, st, dvm, w2);
+      nfev += 1;
+      const double fnorm1 = fabs(wa4);
+      double actred = -1.0;
+      if (fnorm1 < fnorm) actred = 1.0 - (fnorm1 / fnorm) * (fnorm1 / fnorm);
+      const double w3 = qtf + (0.0 + r * w1);
+      const double tq = fabs(w3);
+      double prered = 0.0;
+      if (tq < fnorm) prered = 1.0 - (tq / fnorm) * (tq / fnorm);
+      const double ratio = (prered > 0.0) ? actred / prered : 0.0;
+      if (ratio < 0.1) {
+        ncsuc = 0; ncfail += 1; delta = 0.5 * delta;
+      } else {
+        ncfail = 0; ncsuc += 1;
+        if (ratio >= 0.5 || ncsuc > 1) {
+          const double t = pnorm / 0.5;
+          delta = (delta > t || t != t) ? delta : t;
+        }
+        if (fabs(ratio - 1.0) <= 0.1) delta = pnorm / 0.5;
+      }
+      if (ratio >= 1e-4) {
+        x = w2;
+        xnorm = fabs(diag * x);
+        fvec = wa4;
+        fnorm = fnorm1;
+        iter += 1;
+      }
+      nslow1 += 1;
+      if (actred >= 0.001) nslow1 = 0;
+      if (jeval) nslow2 += 1;
+      if (ratio >= 0.1) nslow2 = 0;
+      if (delta <= xtol * xnorm || fnorm == 0.0) return x;
+      const double m1 = 0.1 * delta;
+      const double mx = (m1 > pnorm || pnorm != pnorm) ? m1 : pnorm;
+      if (nfev >= 400 || 0.1 * mx <= kEpsMch * xnorm || nslow2 == 5 || nslow1 == 10) return x;
+      if (ncfail == 2) break;                              // refresh the Jacobian
+      const double sum = 0.0 + fjac * wa4;                 // Broyden rank-1 (r1updt, n = 1)
+      const double v = (sum - w3) / pnorm;
+      const double u = diag * ((diag * w1) / pnorm);
+      if (ratio >= 1e-4) qtf = sum;
+      r = r + v * u;
+      jeval = false;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// satellite_function.py:462-556 rf_extreme_point('orbit_c1'/'orbit_c2'), fai = 0
+// ---------------------------------------------------------------------------
+struct Pursuer { double u, dv2, e, f0, p, r, sf0, X, sq; };
+
+__device__ __forceinline__ void rf_extreme(const Pursuer& P, double f_c, double& rmax, double& rmin) {
+  const double d = f_c - P.f0;
+  const double sd = sin(d);
+  const double temp1 = (sd * sd) / (P.u * (P.X * P.X) / (P.p * P.dv2) - 1.0);    // :466
+  if (!(0.0 <= temp1)) { rmax = 0.0; rmin = 0.0; return; }                       // :477
+  const double beta = atan(0.0 / sd);                                            // tan(fai)=0, :469
+  const double sb = sin(beta), cb = cos(beta);
+  const double dvm = sqrt(P.dv2 - P.u * (P.X * P.X) * (sb * sb) / P.p);          // :470
+  double theta = 0.0;
+  if ((-kTwoPi <= d && d < -kPi) || (0.0 <= d && d < kPi)) theta = acos(cos(d) * 1.0);          // :473
+  else if ((-kPi <= d && d < 0.0) || (kPi <= d && d < kTwoPi)) theta = kTwoPi - acos(cos(d) * 1.0);
+  double st, ct;
+  sincos(theta, &st, &ct);
+  const double vx0 = P.sq * P.e * P.sf0;                                         // :518
+  const double vy0 = P.sq * P.X * cb;                                            // :519
+  double rf[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double ag = k == 0 ? kPi / 2 : -kPi / 2;                               // :516, :534
+    double sg, cg;
+    sincos(ag, &sg, &cg);
+    const double v1x = vx0 + dvm * cg, v1y = vy0 + dvm * sg;
+    const double h = P.r * v1y;
+    const double A = (2.0 * P.u * (1.0 - ct)) / (h * v1y) - v1x * st / v1y;      // :560
+    const double al = hybrd1(A, st, dvm, ag);
+    double sa, ca;
+    sincos(al, &sa, &ca);
+    const double vx = vx0 + dvm * ca, vy = vy0 + dvm * sa;                       // :525-528
+    const double hm = P.r * vy;
+    rf[k] = (hm * hm) / (P.u * (1.0 - ct) + hm * vy * ct - hm * vx * st);        // :530
+  }
+  rmax = fabs(rf[0]);
+  rmin = fabs(rf[1]);
+  if (rmax < rmin) { const double t = rmin; rmin = rmax; rmax = t; }            // :549-554
+}
+
+// self.Delta_V_c ** 2 by numpy scalar type
+__device__ __forceinline__ double fuel_sq(double fuel, int mode) {
+  if (mode == kF32) { const float f = (float)fuel; return (double)(f * f); }
+  return fuel * fuel;
+}
+
+// environment.py:317-332 + satellite_function.py:18-99,317-373.  Returns 0 or <0.
+__device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
+                                           double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
+                                           double Ev1, double Ev2, double fuel, int fmode, int& count) {
+  const double u = 3.986e14;                                // Time_window_of_danger_zone default u
+  Elements C, T;
+  int rc = orbital_elements(u, prm.R_cw[0] + Pp0, prm.R_cw[1] + Pp1, prm.R_cw[2] + Pp2, prm.V_cw[0] + Pv0,
+                            prm.V_cw[1] + Pv1, prm.V_cw[2] + Pv2, C);
+  if (rc) return rc;
+  rc = orbital_elements(u, prm.R_cw[0] + Ep0, prm.R_cw[1] + Ep1, prm.R_cw[2] + Ep2, prm.V_cw[0] + Ev0,
+                        prm.V_cw[1] + Ev1, prm.V_cw[2] + Ev2, T);
+  if (rc) return rc;
+  Pursuer P;
+  P.u = u;
+  P.dv2 = fuel_sq(fuel, fmode);
+  P.e = C.e;
+  P.f0 = C.f;
+  double sf0, cf0;
+  sincos(C.f, &sf0, &cf0);
+  P.sf0 = sf0;
+  P.X = 1.0 + C.e * cf0;
+  P.p = C.a * (1.0 - C.e * C.e);                                                 // :58
+  P.r = P.p / P.X;                                                               // :57 (a(1-e^2)/(1+e cos f0))
+  P.sq = sqrt(u / P.p);
+  // :317-339 latitudinal angles
+  double s_it, c_it, s_ic, c_ic, s_d, c_d;
+  sincos(T.i, &s_it, &c_it);
+  sincos(C.i, &s_ic, &c_ic);
+  sincos(C.Omega - T.Omega, &s_d, &c_d);
+  const double s_dn = sin(T.Omega - C.Omega), c_dn = cos(T.Omega - C.Omega);
+  double temp1 = (s_it * s_d) / (c_it * s_ic - s_it * c_ic * c_d);
+  double temp2 = (s_ic * s_dn) / (c_ic * s_it - s_ic * c_it * c_dn);
+  if (temp1 != temp1 || temp2 != temp2) { temp1 = 1.0; temp2 = 1.0; }         // :331-332
+  const double u_c1 = atan(temp1), u_c2 = kPi + u_c1;
+  const double u_t1 = atan(temp2), u_t2 = u_t1 + kPi;
+  double mx1, mn1, mx2, mn2;
+  rf_extreme(P, u_c1 - C.omega, mx1, mn1);
+  rf_extreme(P, u_c2 - C.omega, mx2, mn2);
+  const double pt = T.a * (1.0 - T.e * T.e);
+  const double r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                  // :363 (cross-wired f_t2)
+  const double r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                  // :365
+  const bool in1 = (mn1 <= r_ft1 && r_ft1 <= mx1), in2 = (mn2 <= r_ft2 && r_ft2 <= mx2);
+  count = (in1 && in2) ? 2 : ((in1 || in2) ? 1 : 0);
+  return 0;
+}
+
+// np.clip(a, -1.6, 1.6) on np.float32
+__device__ __forceinline__ float clip16(float a) {
+  return a < -1.6f ? -1.6f : (a > 1.6f ? 1.6f : a);
+}
+
+// fuel -= |a0|+|a1|+|a2| under numpy scalar promotion (environment.py:106-107)
+__device__ __forceinline__ void fuel_sub(double& fuel, int& mode, bool zero_int_action, float s) {
+  if (zero_int_action) {
+    mode = (mode == kPyInt) ? kI64 : ((mode == kF32) ? kF64 : mode);
+    return;
+  }
+  if (mode == kPyInt || mode == kF32) { fuel = (double)((float)fuel - s); mode = kF32; }
+  else { fuel = fuel - (double)s; mode = kF64; }
+}
+
+__device__ __forceinline__ double cos_sim(double a0, double a1, double a2, double b0, double b1, double b2) {
+  const double na = norm3(a0, a1, a2), nb = norm3(b0, b1, b2);
+  return dot3(a0 / na, a1 / na, a2 / na, b0 / nb, b1 / nb, b2 / nb);
+}
+
+// float32 np.linalg.norm (OpenBLAS sdot: f32 products summed in double)
+__device__ __forceinline__ float norm3f(float a0, float a1, float a2) {
+  double s = (double)(a0 * a0);
+  s += (double)(a1 * a1);
+  s += (double)(a2 * a2);
+  return sqrtf((float)s);
+}
+
+}  // namespace satenv

@@ -1,0 +1,481 @@
+// satenv_kernels.hip -- gfx950 kernels + C-ABI implementation of include/satenv.h.
+//
+// Layout in HBM (per handle, num_envs = N):
+//   f64 planes [16][N]  Pp0..2 Pv0..2 Ep0..2 Ev0..2 fuel_c fuel_t dis ep_return
+//   i32 planes [3][N]   dangerous_zone, episode_count, bits
+// One lane per env; every plane access is a unit-stride (coalesced) 8-/4-B
+// load/store.  Actions [N][3] f32 and obs [N][18] f32 are row-major as the
+// policy GEMMs consume them.  The STM and scalars ride in the kernel's
+// argument segment (satenv_params by value -> SGPRs / constant cache).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "satenv.h"
+#include "satenv_device.h"
+
+using namespace satenv;
+
+namespace {
+
+constexpr int kF64Planes = 16;   // 15 public + per-env episode return
+constexpr int kI32Planes = 3;
+constexpr int kPlaneRet = 15;
+constexpr int kPlaneDz = 0, kPlaneCount = 1, kPlaneBits = 2;
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(SATENV_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct StepIO {
+  const float* pa;
+  const float* ea;
+  const int32_t* ext_count;   // nullptr -> device counters
+  float* obs;
+  double* obs64;
+  double* rew64;
+  float* rew32;
+  uint8_t* done;
+  double* stats;
+  int32_t* err;
+};
+
+__device__ __forceinline__ void write_obs(float* obs, double* obs64, int64_t i, const double (&k)[12]) {
+  // [Pp-Ep, Pv-Ev, Pp, Pv, Ep, Ev]  environment.py:76-77,177-178
+  double o[18];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    o[c] = k[c] - k[6 + c];
+    o[3 + c] = k[3 + c] - k[9 + c];
+    o[6 + c] = k[c];
+    o[9 + c] = k[3 + c];
+    o[12 + c] = k[6 + c];
+    o[15 + c] = k[9 + c];
+  }
+  if (obs) {
+    float2* dst = reinterpret_cast<float2*>(obs + i * 18);   // 8-B aligned rows
+#pragma unroll
+    for (int c = 0; c < 9; ++c) dst[c] = make_float2((float)o[2 * c], (float)o[2 * c + 1]);
+  }
+  if (obs64) {
+#pragma unroll
+    for (int c = 0; c < 18; ++c) obs64[i * 18 + c] = o[c];
+  }
+}
+
+__device__ __forceinline__ void reset_kin(const Params& p, double (&k)[12]) {
+  // environment.py:67-71 reset positions/velocities (int64 arrays)
+#pragma unroll
+  for (int c = 0; c < 12; ++c) k[c] = 0.0;
+  k[0] = 200000.0;
+  k[6] = 18000.0;
+}
+
+// wave-level reduction of the per-step stats, one f64 atomic per wave and counter
+__device__ __forceinline__ void wave_stats(double* stats, double fin, double fin_ret, double rew, double cap) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    fin += __shfl_xor(fin, off, 64);
+    fin_ret += __shfl_xor(fin_ret, off, 64);
+    rew += __shfl_xor(rew, off, 64);
+    cap += __shfl_xor(cap, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (fin != 0.0) atomicAdd(stats + 0, fin);
+    if (fin_ret != 0.0) atomicAdd(stats + 1, fin_ret);
+    atomicAdd(stats + 2, rew);
+    if (cap != 0.0) atomicAdd(stats + 3, cap);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One environment step (environment.py:81-255), one lane per env.
+// ---------------------------------------------------------------------------
+template <bool AUTORESET>
+__global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, double* __restrict__ f64,
+                                                   int32_t* __restrict__ i32, StepIO io) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
+  double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0, cap = 0.0;
+  if (live) {
+    double k[12];
+#pragma unroll
+    for (int c = 0; c < 12; ++c) k[c] = f64[c * n + i];
+    double fuel_c = f64[12 * n + i], fuel_t = f64[13 * n + i], dis = f64[14 * n + i];
+    int dz = i32[kPlaneDz * n + i];
+    int bits = i32[kPlaneBits * n + i];
+    int count;
+    if (AUTORESET || io.ext_count == nullptr) count = i32[kPlaneCount * n + i] + 1;
+    else count = io.ext_count[i];
+    const int flag = env_flag(bits);
+    const int vi = vel_int(bits);
+    int fcm = fc_mode(bits), ftm = ft_mode(bits);
+
+    float pa[3], ea[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      pa[c] = clip16(io.pa[i * 3 + c]);                                  // :86-87
+      ea[c] = clip16(io.ea[i * 3 + c]);
+    }
+    const double dis_prev = norm3(k[0] - k[6], k[1] - k[7], k[2] - k[8]);    // :89
+    bool p_zero = false, e_zero = false, move_p = true, move_e = true;
+    if (flag == 0) {
+      if (dis < prm.d_range && dz != 0) { move_p = false; p_zero = true; }  // :91-97
+    } else {
+      if (dz == 0) { move_e = false; e_zero = true; }                        // :194-198
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {                                            // Vector[i] += action[i]
+      if (move_p) { const double t = k[3 + c] + (double)pa[c]; k[3 + c] = vi ? trunc(t) : t; }
+      if (move_e) { const double t = k[9 + c] + (double)ea[c]; k[9 + c] = vi ? trunc(t) : t; }
+    }
+    fuel_sub(fuel_c, fcm, p_zero, (fabsf(pa[0]) + fabsf(pa[1])) + fabsf(pa[2]));   // :106
+    fuel_sub(fuel_t, ftm, e_zero, (fabsf(ea[0]) + fabsf(ea[1])) + fabsf(ea[2]));   // :107
+
+    // Clohessy-Wiltshire STM (satellite_function.py:776-779), OpenBLAS dgemv_t order
+    double y[12];
+#pragma unroll
+    for (int craft = 0; craft < 2; ++craft) {
+      const double* x = k + 6 * craft;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const double* M = prm.stm + 6 * r;
+        const double p0 = M[0] * x[0], p1 = M[1] * x[1], p2 = M[2] * x[2];
+        const double p3 = M[3] * x[3], p4 = M[4] * x[4], p5 = M[5] * x[5];
+        y[6 * craft + r] = (((p0 + p2) + (p1 + p3)) + p4) + p5;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 12; ++c) k[c] = y[c];
+    const double r0 = k[0] - k[6], r1 = k[1] - k[7], r2 = k[2] - k[8];
+    dis = norm3(r0, r1, r2);                                                // :132
+
+    double reward;
+    bool done;
+    if (dis <= prm.d_capture) {                                             // :139-142, :221-225
+      reward = flag == 0 ? prm.win_reward : -150.0;
+      done = true;
+      cap = 1.0;
+    } else if (count >= prm.max_episode_steps) {                           // :144-147, :227-231
+      reward = flag == 0 ? prm.burn_reward : prm.win_reward;
+      done = true;
+    } else {
+      int cnt = 0;
+      const int rc = danger_zone(prm, k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9], k[10], k[11],
+                                 fuel_c, fcm, cnt);                         // :150, :317-332
+      if (rc) atomicCAS(io.err, 0, rc);
+      dz = cnt;
+      double r = (dis < dis_prev) ? 1.0 : -1.0;                            // :161-164
+      r += (prm.d_capture <= dis && dis <= 4 * prm.d_capture) ? -1.0 : -2.0;
+      r += (dz == 0) ? -1.0 : dz * 0.5;
+      const double pv1 = cos_sim(k[0], k[1], k[2], k[6], k[7], k[8]);     // reward_of_action3
+      const double pv2 = cos_sim(k[3], k[4], k[5], k[9], k[10], k[11]);   // reward_of_action1
+      const double pv3 = cos_sim(r0, r1, r2, k[3], k[4], k[5]);           // reward_of_action2
+      double pv4 = 0.0;                                                    // reward_of_action4, :388
+      if (!p_zero && pa[0] != 0.0f && pa[1] != 0.0f && pa[2] != 0.0f) {
+        const double nr = norm3(r0, r1, r2);
+        const float na = norm3f(pa[0], pa[1], pa[2]);
+        pv4 = -dot3(r0 / nr, r1 / nr, r2 / nr, (double)(pa[0] / na), (double)(pa[1] / na), (double)(pa[2] / na));
+      }
+      r += 1 * pv1;
+      r += 0.6 * pv2;
+      r += 0.2 * pv3;
+      r += 2 * pv4;
+      reward = flag == 0 ? r : -r;                                          // :251
+      done = false;
+    }
+
+    if (io.rew64) io.rew64[i] = reward;
+    if (io.rew32) io.rew32[i] = (float)reward;
+    if (io.done) io.done[i] = done ? 1 : 0;
+    double ret = f64[kPlaneRet * n + i] + reward;
+    rew_acc = reward;
+    int vi_out = 0;
+    if (AUTORESET && done) {                                                // CPPO_main.py:149-153 -> reset(Flag)
+      fin = 1.0;
+      fin_ret = ret;
+      ret = 0.0;
+      reset_kin(prm, k);
+      vi_out = 1;
+      count = 0;
+    }
+    write_obs(io.obs, io.obs64, i, k);
+#pragma unroll
+    for (int c = 0; c < 12; ++c) f64[c * n + i] = k[c];
+    f64[12 * n + i] = fuel_c;
+    f64[13 * n + i] = fuel_t;
+    f64[14 * n + i] = dis;
+    f64[kPlaneRet * n + i] = ret;
+    i32[kPlaneDz * n + i] = dz;
+    i32[kPlaneCount * n + i] = count;
+    i32[kPlaneBits * n + i] = make_bits(fcm, ftm, vi_out, flag);
+  }
+  if (io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
+}
+
+__global__ void __launch_bounds__(256) reset_kernel(const Params prm, int64_t n, double* __restrict__ f64,
+                                                    int32_t* __restrict__ i32, int32_t flag, const uint8_t* mask,
+                                                    float* obs, double* obs64) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double k[12];
+  const bool hit = mask == nullptr || mask[i] != 0;
+  if (hit) {                                                                // environment.py:66-79
+    reset_kin(prm, k);
+#pragma unroll
+    for (int c = 0; c < 12; ++c) f64[c * n + i] = k[c];
+    const int b = i32[kPlaneBits * n + i];
+    i32[kPlaneBits * n + i] = make_bits(fc_mode(b), ft_mode(b), 1, flag);
+    i32[kPlaneCount * n + i] = 0;
+    f64[kPlaneRet * n + i] = 0.0;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 12; ++c) k[c] = f64[c * n + i];
+  }
+  write_obs(obs, obs64, i, k);
+}
+
+__global__ void init_kernel(const Params prm, int64_t n, double* f64, int32_t* i32) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+#pragma unroll
+  for (int c = 0; c < 12; ++c) f64[c * n + i] = prm.init_kin[c];           // environment.py:30-33
+  f64[12 * n + i] = prm.fuel_c0;                                            // :42-43
+  f64[13 * n + i] = prm.fuel_t0;
+  f64[14 * n + i] = INFINITY;                                               // :44
+  f64[kPlaneRet * n + i] = 0.0;
+  i32[kPlaneDz * n + i] = 0;                                                // :41
+  i32[kPlaneCount * n + i] = 0;
+  i32[kPlaneBits * n + i] = make_bits(prm.fuel_c0_mode, prm.fuel_t0_mode, 1, prm.flag);
+}
+
+__global__ void __launch_bounds__(256) danger_zone_kernel(int64_t n, const double* __restrict__ X,
+                                                          const double* __restrict__ fuel,
+                                                          const int32_t* __restrict__ mode, int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  satenv_params prm;
+  for (int c = 0; c < 3; ++c) { prm.R_cw[c] = 0.0; prm.V_cw[c] = 0.0; }   // states are already absolute
+  const double* x = X + i * 12;
+  int cnt = 0;
+  const int rc = danger_zone(prm, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], x[8], x[9], x[10], x[11],
+                             fuel[i], mode[i], cnt);
+  out[i] = rc ? rc : cnt;
+}
+
+__global__ void __launch_bounds__(256) solve_alpha_kernel(int64_t n, const double* __restrict__ in,
+                                                          double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* x = in + i * 6;   // Delta_Vm, theta, v_1x, v_1y, h, alpha_guess
+  const double u = 3.986e14, dvm = x[0], theta = x[1], v1x = x[2], v1y = x[3], h = x[4];
+  const double A = (2.0 * u * (1.0 - cos(theta))) / (h * v1y) - v1x * sin(theta) / v1y;
+  out[i] = hybrd1(A, sin(theta), dvm, x[5]);
+}
+
+}  // namespace
+
+struct satenv_env {
+  int64_t n = 0;
+  int device = 0;
+  satenv_params prm{};
+  double* f64 = nullptr;
+  int32_t* i32 = nullptr;
+  int32_t* err = nullptr;
+  int block = 64;
+};
+
+namespace {
+
+int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
+
+// env-step launch geometry: N = 16384 envs is only 256 waves, so 64-lane
+// workgroups spread them over all 256 CUs instead of packing 4 per CU.
+int pick_block(int64_t n) {
+  if (n <= 256 * 64) return 64;
+  if (n <= 256 * 128) return 128;
+  return 256;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* satenv_last_error(void) { return g_last_error.c_str(); }
+int satenv_abi_version(void) { return SATENV_ABI_VERSION; }
+
+int satenv_stm(double t, double* M) {
+  if (!M) return fail(SATENV_ERR_ARG, "satenv_stm: null output");
+  // satellite_function.py:753-781; r**3 as the correctly rounded python int -> float
+  const double R3 = (double)((__int128)42164000 * 42164000 * 42164000);
+  const double omega = std::sqrt(3.986e14 / R3);
+  const double tau = omega * t, s = std::sin(tau), c = std::cos(tau);
+  const double m[36] = {4 - 3 * c, 0, 0, s / omega, 2 * (1 - c) / omega, 0,
+                        6 * (s - tau), 1, 0, -2 * (1 - c) / omega, 4 * s / omega - 3 * tau, 0,
+                        0, 0, c, 0, 0, s / omega,
+                        3 * omega * s, 0, 0, c, 2 * s, 0,
+                        6 * omega * (c - 1), 0, 0, -2 * s, 4 * c - 3, 0,
+                        0, 0, -omega * s, 0, 0, c};
+  std::memcpy(M, m, sizeof(m));
+  return SATENV_OK;
+}
+
+int satenv_default_params(satenv_params* p) {
+  if (!p) return fail(SATENV_ERR_ARG, "satenv_default_params: null");
+  std::memset(p, 0, sizeof(*p));
+  p->d_capture = 100000;   // environment.py:28 ctor default (train_* overwrite it)
+  p->d_range = 100000;
+  p->win_reward = 100;
+  p->burn_reward = 0;
+  p->mu = 3.986e14;
+  p->R_cw[0] = 27098000; p->R_cw[1] = 32306000; p->R_cw[2] = 0;
+  p->V_cw[0] = -2350; p->V_cw[1] = 1970; p->V_cw[2] = 0;
+  satenv_stm(100.0, p->stm);
+  p->fuel_c0 = 320; p->fuel_t0 = 320;
+  p->fuel_c0_mode = SATENV_NUM_PYINT; p->fuel_t0_mode = SATENV_NUM_PYINT;
+  const double kin[12] = {2000, 2000, 1000, 1.71, 1.14, 1.3, 1000, 2000, 0, 1.71, 1.14, 1.3};   // :26-27
+  std::memcpy(p->init_kin, kin, sizeof(kin));
+  p->max_episode_steps = 1000;   // CPPO_main.py:28
+  p->flag = 0;
+  return SATENV_OK;
+}
+
+int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, int device) {
+  if (!out || !p || num_envs <= 0) return fail(SATENV_ERR_ARG, "satenv_create: bad arguments");
+  HIP_TRY(hipSetDevice(device));
+  satenv_env* h = new satenv_env();
+  h->n = num_envs;
+  h->device = device;
+  h->prm = *p;
+  h->block = pick_block(num_envs);
+  hipError_t e = hipMalloc(&h->f64, sizeof(double) * kF64Planes * num_envs);
+  if (e == hipSuccess) e = hipMalloc(&h->i32, sizeof(int32_t) * kI32Planes * num_envs);
+  if (e == hipSuccess) e = hipMalloc(&h->err, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemset(h->err, 0, sizeof(int32_t));
+  if (e != hipSuccess) {
+    satenv_destroy(h);
+    return fail(SATENV_ERR_HIP, std::string("satenv_create: ") + hipGetErrorString(e));
+  }
+  hipLaunchKernelGGL(init_kernel, dim3(grid_for(num_envs, 256)), dim3(256), 0, nullptr, h->prm, h->n, h->f64,
+                     h->i32);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    satenv_destroy(h);
+    return fail(SATENV_ERR_HIP, std::string("satenv_create init: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return SATENV_OK;
+}
+
+int satenv_destroy(satenv_env* h) {
+  if (!h) return SATENV_OK;
+  if (h->f64) (void)hipFree(h->f64);
+  if (h->i32) (void)hipFree(h->i32);
+  if (h->err) (void)hipFree(h->err);
+  delete h;
+  return SATENV_OK;
+}
+
+int satenv_num_envs(const satenv_env* h, int64_t* n) {
+  if (!h || !n) return fail(SATENV_ERR_ARG, "satenv_num_envs: null");
+  *n = h->n;
+  return SATENV_OK;
+}
+
+int satenv_set_params(satenv_env* h, const satenv_params* p) {
+  if (!h || !p) return fail(SATENV_ERR_ARG, "satenv_set_params: null");
+  h->prm = *p;
+  return SATENV_OK;
+}
+
+int satenv_reset(satenv_env* h, int32_t flag, const uint8_t* env_mask, float* obs_out, double* obs64_out,
+                 void* stream) {
+  if (!h) return fail(SATENV_ERR_ARG, "satenv_reset: null handle");
+  if (flag != 0 && flag != 1) return fail(SATENV_ERR_ARG, "satenv_reset: only Flag 0/1 are on the hot path");
+  h->prm.flag = flag;
+  hipLaunchKernelGGL(reset_kernel, dim3(grid_for(h->n, 256)), dim3(256), 0, (hipStream_t)stream, h->prm, h->n,
+                     h->f64, h->i32, flag, env_mask, obs_out, obs64_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_step(satenv_env* h, const float* pa, const float* ea, const int32_t* episode_count, float* obs_out,
+                double* obs64_out, double* reward_out, uint8_t* done_out, void* stream) {
+  if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step: null argument");
+  StepIO io{pa, ea, episode_count, obs_out, obs64_out, reward_out, nullptr, done_out, nullptr, h->err};
+  hipLaunchKernelGGL(step_kernel<false>, dim3(grid_for(h->n, h->block)), dim3(h->block), 0, (hipStream_t)stream,
+                     h->prm, h->n, h->f64, h->i32, io);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_step_autoreset(satenv_env* h, const float* pa, const float* ea, float* obs_out, float* reward_out,
+                          uint8_t* done_out, double* stats_out, void* stream) {
+  if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step_autoreset: null argument");
+  StepIO io{pa, ea, nullptr, obs_out, nullptr, nullptr, reward_out, done_out, stats_out, h->err};
+  hipLaunchKernelGGL(step_kernel<true>, dim3(grid_for(h->n, h->block)), dim3(h->block), 0, (hipStream_t)stream,
+                     h->prm, h->n, h->f64, h->i32, io);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_get_state(const satenv_env* h, double* f64_planes, int32_t* i32_planes, void* stream) {
+  if (!h) return fail(SATENV_ERR_ARG, "satenv_get_state: null handle");
+  if (f64_planes)
+    HIP_TRY(hipMemcpyAsync(f64_planes, h->f64, sizeof(double) * SATENV_F64_PLANES * h->n, hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+  if (i32_planes)
+    HIP_TRY(hipMemcpyAsync(i32_planes, h->i32, sizeof(int32_t) * SATENV_I32_PLANES * h->n,
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return SATENV_OK;
+}
+
+int satenv_set_state(satenv_env* h, const double* f64_planes, const int32_t* i32_planes, void* stream) {
+  if (!h) return fail(SATENV_ERR_ARG, "satenv_set_state: null handle");
+  if (f64_planes)
+    HIP_TRY(hipMemcpyAsync(h->f64, f64_planes, sizeof(double) * SATENV_F64_PLANES * h->n, hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+  if (i32_planes)
+    HIP_TRY(hipMemcpyAsync(h->i32, i32_planes, sizeof(int32_t) * SATENV_I32_PLANES * h->n,
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return SATENV_OK;
+}
+
+int satenv_danger_zone(int64_t n, const double* states, const double* fuel, const int32_t* fuel_mode,
+                       int32_t* count_out, void* stream) {
+  if (n <= 0 || !states || !fuel || !fuel_mode || !count_out) return fail(SATENV_ERR_ARG, "satenv_danger_zone: bad args");
+  hipLaunchKernelGGL(danger_zone_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, states, fuel,
+                     fuel_mode, count_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* stream) {
+  if (n <= 0 || !in || !alpha_out) return fail(SATENV_ERR_ARG, "satenv_solve_alpha: bad args");
+  hipLaunchKernelGGL(solve_alpha_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, in, alpha_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_check(satenv_env* h, int32_t* status) {
+  if (!h || !status) return fail(SATENV_ERR_ARG, "satenv_check: null");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(status, h->err, sizeof(int32_t), hipMemcpyDeviceToHost));
+  return SATENV_OK;
+}
+
+}  // extern "C"

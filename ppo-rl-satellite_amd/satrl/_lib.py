@@ -1,0 +1,131 @@
+"""ctypes binding of the product's C-ABI library ``libsatrl.so``.
+
+The library exports exactly the functions declared in ``include/satenv.h``
+and ``include/satrl_rollout.h`` (plain pointers, sizes and a ``void*``
+hipStream_t).  It is built in-tree by ``csrc/Makefile`` for gfx950.  There is
+no fallback: if the library is missing or cannot be loaded, every op raises.
+
+torch is imported first so that the process has a single HIP runtime
+(torch's bundled ``libamdhip64.so.7``; the library's NEEDED entry resolves to
+it by SONAME).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import torch  # noqa: F401  (must be loaded before libsatrl.so, see module doc)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libsatrl.so")
+
+SATENV_F64_PLANES = 15
+SATENV_I32_PLANES = 3
+OBS_DIM = 18
+ACT_DIM = 3
+
+
+class SatenvParams(C.Structure):
+    """Mirror of ``satenv_params`` (include/satenv.h)."""
+    _fields_ = [("d_capture", C.c_double), ("d_range", C.c_double), ("win_reward", C.c_double),
+                ("burn_reward", C.c_double), ("mu", C.c_double), ("R_cw", C.c_double * 3),
+                ("V_cw", C.c_double * 3), ("stm", C.c_double * 36), ("fuel_c0", C.c_double),
+                ("fuel_t0", C.c_double), ("init_kin", C.c_double * 12), ("max_episode_steps", C.c_int32),
+                ("flag", C.c_int32), ("fuel_c0_mode", C.c_int32), ("fuel_t0_mode", C.c_int32)]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def build(force: bool = False) -> str:
+    """Compile libsatrl.so for gfx950 with hipcc (csrc/Makefile)."""
+    args = ["make", "-s", "-C", CSRC_DIR, "-j4"]
+    if force:
+        subprocess.check_call(["make", "-s", "-C", CSRC_DIR, "clean"])
+    subprocess.check_call(args)
+    return LIB_PATH
+
+
+_lib = None
+
+_vp = C.c_void_p
+_i64 = C.c_int64
+_i32 = C.c_int32
+_SIGS = {
+    "satenv_default_params": ([C.POINTER(SatenvParams)], C.c_int),
+    "satenv_stm": ([C.c_double, C.POINTER(C.c_double)], C.c_int),
+    "satenv_last_error": ([], C.c_char_p),
+    "satenv_abi_version": ([], C.c_int),
+    "satenv_create": ([C.POINTER(_vp), _i64, C.POINTER(SatenvParams), C.c_int], C.c_int),
+    "satenv_destroy": ([_vp], C.c_int),
+    "satenv_num_envs": ([_vp, C.POINTER(_i64)], C.c_int),
+    "satenv_set_params": ([_vp, C.POINTER(SatenvParams)], C.c_int),
+    "satenv_reset": ([_vp, _i32, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_step": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_step_autoreset": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_get_state": ([_vp, _vp, _vp, _vp], C.c_int),
+    "satenv_set_state": ([_vp, _vp, _vp, _vp], C.c_int),
+    "satenv_check": ([_vp, C.POINTER(_i32)], C.c_int),
+    "satenv_danger_zone": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_solve_alpha": ([_i64, _vp, _vp, _vp], C.c_int),
+    "satrl_gae": ([_i64, _i64, _vp, _vp, _vp, C.c_float, C.c_float, _vp, _vp, _vp], C.c_int),
+    "satrl_gaussian_sample": ([_i64, _vp, _vp, C.c_float, C.c_uint64, C.c_uint32, _i64, C.c_uint64, _vp, _vp, _vp],
+                              C.c_int),
+    "satrl_moments": ([_i64, _vp, _vp, _vp], C.c_int),
+    "satrl_last_error": ([], C.c_char_p),
+}
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def lib():
+    """Load libsatrl.so (raises NativeError if it is absent/unloadable)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"{LIB_PATH} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        try:
+            L = C.CDLL(LIB_PATH)
+        except OSError as e:
+            raise NativeError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (argt, rest) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = rest
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().satenv_last_error().decode() if what.startswith("satenv") else lib().satrl_last_error().decode()
+        raise NativeError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = torch.cuda.current_stream() if stream is None else stream
+    return C.c_void_p(s.cuda_stream)
+
+
+def require_cuda(t, dtype, shape=None, name="tensor"):
+    if not t.is_cuda:
+        raise NativeError(f"{name} must be a device (cuda/HIP) tensor")
+    if t.dtype != dtype:
+        raise NativeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise NativeError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise NativeError(f"{name} shape {tuple(t.shape)} != {tuple(shape)}")
+    return t

@@ -1,0 +1,352 @@
+"""Environment front-ends over the HIP C-ABI (include/satenv.h).
+
+* ``VecSatellites`` -- N environments resident in HBM, torch device tensors in
+  and out; the engine's rollout path.
+* ``satellites``    -- drop-in for the reference class
+  (qiaobeibei/PPO-RL-Satellite environment.py:8-413): same constructor
+  keywords, ``reset(Flag)`` / ``step(pursuer_action, escaper_action,
+  epsiode_count)`` signatures, numpy outputs with the reference's dtypes and
+  the attributes its callers read (``observation_space``, ``action_space``,
+  ``d_capture`` ...).  It runs one env on the GPU kernel -- there is no CPU
+  implementation in the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ACT_DIM, OBS_DIM, SATENV_F64_PLANES, SATENV_I32_PLANES, check, ptr, require_cuda, stream_ptr
+
+PYINT, I64, F32, F64 = 0, 1, 2, 3
+STATE_F64 = ["Pp0", "Pp1", "Pp2", "Pv0", "Pv1", "Pv2", "Ep0", "Ep1", "Ep2", "Ev0", "Ev1", "Ev2",
+             "fuel_c", "fuel_t", "dis"]
+STATE_I32 = ["dz", "episode_count", "bits"]
+
+
+def default_params(**overrides) -> _lib.SatenvParams:
+    p = _lib.SatenvParams()
+    check(_lib.lib().satenv_default_params(C.byref(p)), "satenv_default_params")
+    for k, v in overrides.items():
+        if k in ("R_cw", "V_cw", "stm", "init_kin"):
+            getattr(p, k)[:] = [float(x) for x in np.asarray(v, dtype=np.float64).ravel()]
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def stm(t: float = 100.0) -> np.ndarray:
+    out = (C.c_double * 36)()
+    check(_lib.lib().satenv_stm(float(t), out), "satenv_stm")
+    return np.array(out[:]).reshape(6, 6)
+
+
+def _num_mode(v) -> int:
+    if isinstance(v, np.float32):
+        return F32
+    if isinstance(v, (np.floating, float)):
+        return F64
+    if isinstance(v, np.integer):
+        return I64
+    return PYINT
+
+
+class Box:
+    """Minimal stand-in for ``gym.spaces.Box`` (environment.py:57): shape/low/high/dtype."""
+
+    def __init__(self, low, high, shape, dtype=np.float32):
+        self.low, self.high, self.dtype = np.asarray(low), np.asarray(high), dtype
+        self.shape = tuple(shape)
+
+
+class Discrete:
+    def __init__(self, n):
+        self.n = n
+
+
+def _spaces():
+    # environment.py:51-62
+    position_low = np.array([-500000, -500000, -500000, -10000000, -10000000, -10000000, -10000000, -10000000,
+                             -10000000])
+    velocity_low = np.array([-10000, -10000, -10000, -50000, -50000, -50000, -50000, -50000, -50000])
+    low = np.concatenate((position_low, velocity_low))
+    obs = Box(low=low, high=-low, shape=(OBS_DIM,), dtype=np.float32)
+    act = np.array([[-1.6, 1.6], [-1.6, 1.6], [-1.6, 1.6]])
+    return obs, act, Discrete(5)
+
+
+class VecSatellites:
+    """``num_envs`` reference environments stepped by one HIP kernel launch.
+
+    Tensors are device tensors on ``device`` (actions f32 [N,3]); every call
+    is asynchronous on the current torch stream.
+    """
+
+    def __init__(self, num_envs: int, device=None, d_capture: float = 100000.0, d_range: float = 100000.0,
+                 max_episode_steps: int = 1000, Flag: int = 0, fuel_c=320, fuel_t=320, **params):
+        if not torch.cuda.is_available():
+            raise _lib.NativeError("VecSatellites needs a HIP device (MI355X); no CPU implementation exists")
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.num_envs = int(num_envs)
+        self._p = default_params(d_capture=float(d_capture), d_range=float(d_range),
+                                 max_episode_steps=int(max_episode_steps), flag=int(Flag), fuel_c0=float(fuel_c),
+                                 fuel_t0=float(fuel_t), fuel_c0_mode=_num_mode(fuel_c),
+                                 fuel_t0_mode=_num_mode(fuel_t), **params)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            check(_lib.lib().satenv_create(C.byref(h), self.num_envs, C.byref(self._p), self.device.index or 0),
+                  "satenv_create")
+        self._h = h
+        self.observation_space, self.action_space, self.action_space_beta = _spaces()
+        self.stats = torch.zeros(4, dtype=torch.float64, device=self.device)
+
+    # -- parameters -----------------------------------------------------------
+    def _push_params(self):
+        check(_lib.lib().satenv_set_params(self._h, C.byref(self._p)), "satenv_set_params")
+
+    @property
+    def d_capture(self):
+        return self._p.d_capture
+
+    @d_capture.setter
+    def d_capture(self, v):          # CPPO_main.py:98 "env.d_capture = d_capture"
+        self._p.d_capture = float(v)
+        self._push_params()
+
+    @property
+    def max_episode_steps(self):
+        return self._p.max_episode_steps
+
+    @max_episode_steps.setter
+    def max_episode_steps(self, v):
+        self._p.max_episode_steps = int(v)
+        self._push_params()
+
+    @property
+    def d_range(self):
+        return self._p.d_range
+
+    @d_range.setter
+    def d_range(self, v):
+        self._p.d_range = float(v)
+        self._push_params()
+
+    # -- API -----------------------------------------------------------------
+    def reset(self, Flag: int = 0, mask=None, obs_out=None, obs64_out=None):
+        """environment.py:66-79 for all envs (or those with mask != 0). Returns obs f32 [N,18]."""
+        n = self.num_envs
+        if obs_out is None and obs64_out is None:
+            obs_out = torch.empty((n, OBS_DIM), dtype=torch.float32, device=self.device)
+        if mask is not None:
+            require_cuda(mask, torch.uint8, (n,), "mask")
+        check(_lib.lib().satenv_reset(self._h, int(Flag), ptr(mask), ptr(obs_out), ptr(obs64_out), stream_ptr()),
+              "satenv_reset")
+        return obs_out if obs_out is not None else obs64_out
+
+    def step(self, pursuer_action, escaper_action, epsiode_count=None, obs_out=None, obs64_out=None,
+             reward_out=None, done_out=None):
+        """environment.py:81-255 for all envs, no automatic reset.
+
+        Returns (obs f32 [N,18] or obs64, reward f64 [N], done u8 [N])."""
+        n = self.num_envs
+        require_cuda(pursuer_action, torch.float32, (n, ACT_DIM), "pursuer_action")
+        require_cuda(escaper_action, torch.float32, (n, ACT_DIM), "escaper_action")
+        if epsiode_count is not None:
+            require_cuda(epsiode_count, torch.int32, (n,), "epsiode_count")
+        if obs_out is None and obs64_out is None:
+            obs_out = torch.empty((n, OBS_DIM), dtype=torch.float32, device=self.device)
+        if reward_out is None:
+            reward_out = torch.empty(n, dtype=torch.float64, device=self.device)
+        if done_out is None:
+            done_out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        check(_lib.lib().satenv_step(self._h, ptr(pursuer_action), ptr(escaper_action), ptr(epsiode_count),
+                                     ptr(obs_out), ptr(obs64_out), ptr(reward_out), ptr(done_out), stream_ptr()),
+              "satenv_step")
+        return (obs_out if obs_out is not None else obs64_out), reward_out, done_out
+
+    def step_autoreset(self, pursuer_action, escaper_action, obs_out=None, reward_out=None, done_out=None,
+                       stats=True):
+        """One step of the CPPO_main.py:119-153 loop for all envs: device episode
+        counters, done envs reset in-kernel (obs_out = post-reset obs).
+        Returns (obs f32 [N,18], reward f32 [N], done u8 [N])."""
+        n = self.num_envs
+        if obs_out is None:
+            obs_out = torch.empty((n, OBS_DIM), dtype=torch.float32, device=self.device)
+        if reward_out is None:
+            reward_out = torch.empty(n, dtype=torch.float32, device=self.device)
+        if done_out is None:
+            done_out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        check(_lib.lib().satenv_step_autoreset(self._h, ptr(pursuer_action), ptr(escaper_action), ptr(obs_out),
+                                               ptr(reward_out), ptr(done_out), ptr(self.stats) if stats else None,
+                                               stream_ptr()), "satenv_step_autoreset")
+        return obs_out, reward_out, done_out
+
+    def get_state(self):
+        n = self.num_envs
+        f = torch.empty((SATENV_F64_PLANES, n), dtype=torch.float64, device=self.device)
+        i = torch.empty((SATENV_I32_PLANES, n), dtype=torch.int32, device=self.device)
+        check(_lib.lib().satenv_get_state(self._h, ptr(f), ptr(i), stream_ptr()), "satenv_get_state")
+        return f, i
+
+    def set_state(self, f64_planes=None, i32_planes=None):
+        n = self.num_envs
+        if f64_planes is not None:
+            require_cuda(f64_planes, torch.float64, (SATENV_F64_PLANES, n), "f64_planes")
+        if i32_planes is not None:
+            require_cuda(i32_planes, torch.int32, (SATENV_I32_PLANES, n), "i32_planes")
+        check(_lib.lib().satenv_set_state(self._h, ptr(f64_planes), ptr(i32_planes), stream_ptr()),
+              "satenv_set_state")
+
+    def check_errors(self) -> int:
+        st = C.c_int32(0)
+        check(_lib.lib().satenv_check(self._h, C.byref(st)), "satenv_check")
+        return st.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().satenv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pack_bits(fuel_c_mode, fuel_t_mode, vel_int, flag):
+    return (int(fuel_c_mode) & 3) | ((int(fuel_t_mode) & 3) << 2) | ((int(vel_int) & 1) << 4) | ((int(flag) & 1) << 5)
+
+
+def unpack_bits(b):
+    b = int(b)
+    return dict(fuel_c_mode=b & 3, fuel_t_mode=(b >> 2) & 3, vel_int=(b >> 4) & 1, flag=(b >> 5) & 1)
+
+
+def _typed(v, mode):
+    return [int(v), np.int64(v), np.float32(v), np.float64(v)][mode]
+
+
+class satellites:  # noqa: N801  (reference class name)
+    """Drop-in for ``environment.satellites`` (environment.py:8), Flag 0/1.
+
+    Same keywords as environment.py:26-28; ``args.max_episode_steps`` is
+    required as in environment.py:46.  State lives on the GPU; the public
+    attributes are read back on access.
+    """
+
+    def __init__(self, Pursuer_position=np.array([2000, 2000, 1000]), Pursuer_vector=np.array([1.71, 1.14, 1.3]),
+                 Escaper_position=np.array([1000, 2000, 0]), Escaper_vector=np.array([1.71, 1.14, 1.3]),
+                 M=0.4, dis_safe=1000, d_capture=100000, Flag=0, fuel_c=320, fuel_t=320, d_range=100000,
+                 args=None, device=None):
+        max_ep = args.max_episode_steps          # AttributeError on args=None, as environment.py:46
+        kin = np.concatenate([np.asarray(Pursuer_position, np.float64), np.asarray(Pursuer_vector, np.float64),
+                              np.asarray(Escaper_position, np.float64), np.asarray(Escaper_vector, np.float64)])
+        self._v = VecSatellites(1, device=device, d_capture=d_capture, d_range=d_range, max_episode_steps=max_ep,
+                                Flag=Flag, fuel_c=fuel_c, fuel_t=fuel_t, init_kin=kin)
+        self.dis_dafe = dis_safe
+        self.M = M
+        self.burn_reward = 0
+        self.win_reward = 100
+        self.ellipse_params = []
+        self.observation_space, self.action_space, self.action_space_beta = _spaces()
+        dev = self._v.device
+        self._pa = torch.empty((1, ACT_DIM), dtype=torch.float32, device=dev)
+        self._ea = torch.empty((1, ACT_DIM), dtype=torch.float32, device=dev)
+        self._cnt = torch.empty(1, dtype=torch.int32, device=dev)
+        self._obs = torch.empty((1, OBS_DIM), dtype=torch.float64, device=dev)
+        self._r = torch.empty(1, dtype=torch.float64, device=dev)
+        self._d = torch.empty(1, dtype=torch.uint8, device=dev)
+
+    # reference attributes ------------------------------------------------------
+    d_capture = property(lambda s: s._v.d_capture, lambda s, v: setattr(s._v, "d_capture", v))
+    d_range = property(lambda s: s._v.d_range, lambda s, v: setattr(s._v, "d_range", v))
+    max_episode_steps = property(lambda s: s._v.max_episode_steps,
+                                 lambda s, v: setattr(s._v, "max_episode_steps", v))
+
+    def _state(self):
+        f, i = self._v.get_state()
+        return f[:, 0].cpu().numpy(), i[:, 0].cpu().numpy()
+
+    def _set(self, fi=None, ii=None):
+        f, i = self._v.get_state()
+        if fi:
+            for k, v in fi.items():
+                f[k, 0] = v
+        if ii:
+            for k, v in ii.items():
+                i[k, 0] = v
+        self._v.set_state(f, i)
+
+    def _kin(self, lo):
+        f, i = self._state()
+        vel_int = unpack_bits(i[2])["vel_int"]
+        arr = f[lo:lo + 3].copy()
+        return arr.astype(np.int64) if vel_int else arr
+
+    Pursuer_position = property(lambda s: s._kin(0))
+    Pursuer_vector = property(lambda s: s._kin(3))
+    Escaper_position = property(lambda s: s._kin(6))
+    Escaper_vector = property(lambda s: s._kin(9))
+
+    @property
+    def fuel_c(self):
+        f, i = self._state()
+        return _typed(f[12], unpack_bits(i[2])["fuel_c_mode"])
+
+    @fuel_c.setter
+    def fuel_c(self, v):
+        f, i = self._v.get_state()
+        b = unpack_bits(int(i[2, 0]))
+        f[12, 0] = float(v)
+        i[2, 0] = pack_bits(_num_mode(v), b["fuel_t_mode"], b["vel_int"], b["flag"])
+        self._v.set_state(f, i)
+
+    @property
+    def fuel_t(self):
+        f, i = self._state()
+        return _typed(f[13], unpack_bits(i[2])["fuel_t_mode"])
+
+    @property
+    def dis(self):
+        return float(self._state()[0][14])
+
+    @property
+    def dangerous_zone(self):
+        return int(self._state()[1][0])
+
+    @property
+    def Flag(self):
+        return unpack_bits(self._state()[1][2])["flag"]
+
+    # API ------------------------------------------------------------------------
+    def reset(self, Flag):
+        """environment.py:66-79: returns the int64 observation."""
+        if Flag not in (0, 1):
+            raise NotImplementedError("Flag 2 (reachable-domain training) is outside the accelerated path")
+        self._v.reset(Flag, obs64_out=self._obs)
+        return self._obs[0].cpu().numpy().astype(np.int64)
+
+    def step(self, pursuer_action, escaper_action, epsiode_count):
+        """environment.py:81-255.  Actions are taken as float32 (the dtype
+        PPO_continuous.choose_action returns)."""
+        self._pa.copy_(torch.as_tensor(np.asarray(pursuer_action, dtype=np.float32).reshape(1, ACT_DIM)))
+        self._ea.copy_(torch.as_tensor(np.asarray(escaper_action, dtype=np.float32).reshape(1, ACT_DIM)))
+        self._cnt.fill_(int(epsiode_count))
+        self._v.step(self._pa, self._ea, self._cnt, obs_out=None, obs64_out=self._obs, reward_out=self._r,
+                     done_out=self._d)
+        obs = self._obs[0].cpu().numpy()
+        r = float(self._r.item())
+        done = bool(self._d.item())
+        if done:
+            r = int(r)          # terminal rewards are python ints in the reference
+        return obs, r, done
+
+    @staticmethod
+    def relative_state_to_absolute_state(R0, V0):
+        """environment.py:334-343."""
+        assert isinstance(R0, np.ndarray) and isinstance(V0, np.ndarray)
+        return np.array([27098000, 32306000, 0]) + R0, np.array([-2350, 1970, 0]) + V0

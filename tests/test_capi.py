@@ -1,0 +1,53 @@
+"""CPU checks of the C-ABI boundary: the library loads and exports every
+symbol the public headers declare (no compute calls: no GPU here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(sat\w+)\s*\(", txt, re.M))
+
+
+def test_headers_declare_expected_entry_points():
+    env = _declared("satenv.h")
+    assert {"satenv_create", "satenv_reset", "satenv_step", "satenv_step_autoreset", "satenv_destroy",
+            "satenv_get_state", "satenv_set_state", "satenv_last_error"} <= env
+    assert {"satrl_gae", "satrl_gaussian_sample", "satrl_moments"} <= _declared("satrl_rollout.h")
+
+
+def test_library_exports_every_declared_symbol():
+    import satrl._lib as L
+    if not os.path.exists(L.LIB_PATH):
+        L.build()
+    lib = L.lib()          # loads with torch's HIP runtime; no device needed
+    declared = _declared("satenv.h") | _declared("satrl_rollout.h")
+    for name in sorted(declared):
+        assert hasattr(lib, name), name
+    assert set(L.exported_symbols()) == declared
+
+
+def test_host_helpers_without_gpu():
+    import numpy as np
+    import satrl._lib as L
+    from satrl import env as E
+    assert L.lib().satenv_abi_version() == 1
+    p = E.default_params()
+    assert p.max_episode_steps == 1000 and p.fuel_c0 == 320 and p.d_range == 100000
+    # host STM equals the oracle's / reference's matrix bit for bit
+    import oracle as O
+    assert np.array_equal(E.stm(100.0), O.stm(100.0))
+
+
+def test_product_has_no_cpu_fallback():
+    import torch
+    from satrl import env as E
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(Exception):
+        E.VecSatellites(4)
