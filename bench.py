@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Benchmark: one "step" = one PPO iteration of the hot path on N GPUs:
+a rollout of T=2048 env-steps for each of 16384 envs per GPU (actor forward
+x2 agents -> HIP Gaussian sampling -> HIP FP64 env step, hipGraph chunks),
+critic values, HIP GAE scan, global advantage normalisation, and the PPO
+update (K=10 epochs x minibatch 4096, hidden 256, Adam, grad clip).
+Workload = BASELINE.json configs[2]; scaling is weak (16384 envs per GPU).
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Rank 0 prints ONE JSON line.  value = all env-steps processed by all ranks
+(N_total * T * K) / max-over-ranks wall time of the K timed iterations.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
+
+METRIC = "env-steps/sec + PPO updates/sec at N_envs=16384, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: FP32 matrix 157.3 TF spec
+ENV_BYTES_PER_STEP = 381       # DESIGN.md "Roofline": state 16 f64 + 3 i32 planes r/w, actions, obs, reward, done
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--num-envs", type=int, default=16384, help="envs per GPU")
+    ap.add_argument("--horizon", type=int, default=2048)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--minibatch", type=int, default=4096)
+    ap.add_argument("--epochs", type=int, default=10)
+    ap.add_argument("--d-capture", type=float, default=15000.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--env-kernel-iters", type=int, default=200)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """Oracle (oracle/satenv_oracle.c, the CPU restatement) on host cores:
+    a bounded sample of the same env workload (Flag 0, reset state,
+    uniform f32 actions), OpenMP over envs."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = 4096
+    rng = np.random.default_rng(0)
+    # calibrate steps for ~`seconds` of work
+    steps = 4
+    pa = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
+    t0 = time.perf_counter()
+    O.rollout(n, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=threads)
+    dt = time.perf_counter() - t0
+    steps = int(max(4, min(400, steps * seconds / max(dt, 1e-3))))
+    pa = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
+    t0 = time.perf_counter()
+    O.rollout(n, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=threads)
+    dt = time.perf_counter() - t0
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle C restatement, {n} envs x {steps} steps from reset (Flag 0, U(-1.6,1.6) f32 actions, "
+                      f"d_capture 15000), OpenMP {threads} threads on '{model}' (os.cpu_count()={os.cpu_count()})",
+            "seconds": dt}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pg = dist.group.WORLD
+
+    from satrl.trainer import VecTrainer, args_param
+    args = args_param(batch_size=a.num_envs * a.horizon, mini_batch_size=a.minibatch, hidden_width=a.hidden,
+                      K_epochs=a.epochs, max_episode_steps=1000, num_envs=a.num_envs, horizon=a.horizon, seed=0,
+                      max_train_steps=int(3e6), chkpt_dir="/tmp")
+    tr = VecTrainer(args, flag=0, d_capture=a.d_capture, pg=pg, env_offset=rank * a.num_envs)
+
+    def barrier():
+        if pg is not None:
+            dist.barrier()
+
+    timers = {}
+    for _ in range(a.warmup):
+        tr.iteration()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        stats = tr.iteration(timers)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if pg is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    n_total = a.num_envs * world
+    env_steps = n_total * a.horizon * a.steps
+    value = env_steps / elapsed
+
+    # ---- env-kernel roofline: HIP events around eager launches on the kernel's stream
+    env = tr.env
+    pa = tr.buf.act[0].clone()
+    ea = torch.empty_like(pa).uniform_(-1.6, 1.6)
+    obs = torch.empty((a.num_envs, 18), dtype=torch.float32, device="cuda")
+    rew = torch.empty(a.num_envs, dtype=torch.float32, device="cuda")
+    dn = torch.empty(a.num_envs, dtype=torch.uint8, device="cuda")
+    for _ in range(10):
+        env.step_autoreset(pa, ea, obs, rew, dn)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.env_kernel_iters):
+        env.step_autoreset(pa, ea, obs, rew, dn)
+    e1.record()
+    torch.cuda.synchronize()
+    env_us = e0.elapsed_time(e1) * 1e3 / a.env_kernel_iters
+    achieved = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
+
+    rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
+    update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
+    gae_ms = sum(timers["gae_ms"]) / len(timers["gae_ms"])
+    H = a.hidden
+    flop_per_transition_epoch = 6 * (18 * H + H * H + 3 * H) + 6 * (18 * H + H * H + H)
+    upd_flops = a.num_envs * a.horizon * a.epochs * flop_per_transition_epoch
+    upd_tfs = upd_flops / (update_ms * 1e-3) / 1e12
+    n_minibatches = a.epochs * ((a.num_envs * a.horizon) // a.minibatch)
+
+    if rank == 0:
+        cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_baseline_seconds)
+        out = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64+f32",
+            "data": "synthetic: reference reset state, random-init (orthogonal, seed 0) policies",
+            "config": {"workload": "BASELINE.json configs[2]: num_envs=16384/GPU, hidden=256, horizon=2048, "
+                                   "GAE lambda=0.95, minibatch=4096, 10 PPO epochs",
+                       "num_envs_per_gpu": a.num_envs, "num_envs_total": n_total, "horizon": a.horizon,
+                       "hidden": a.hidden, "minibatch_per_gpu": a.minibatch, "epochs": a.epochs,
+                       "d_capture": a.d_capture, "parallelism": f"dp{world}"},
+            "ppo_updates_per_s": a.steps / elapsed,
+            "rollout_env_steps_per_s": n_total * a.horizon / (rollout_ms * 1e-3),
+            "rollout_ms": rollout_ms, "gae_ms": gae_ms, "update_ms": update_ms,
+            "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
+            "episodes_finished_total": float(stats[0]),
+            "roofline": {"kernel": "satenv step_kernel<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "avg_launch_us": env_us,
+                         "bytes_per_env_step": ENV_BYTES_PER_STEP,
+                         "note": "algorithmic bytes; the kernel is FP64-VALU/transcendental bound (DESIGN.md)"},
+            "roofline_update": {"bound": "mfma", "achieved": upd_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
+                                "flop_per_transition_epoch": flop_per_transition_epoch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -29,10 +29,13 @@ extern "C" {
 int satrl_gae(int64_t T, int64_t N, const float* r, const uint8_t* done, const float* v, float gamma, float lamda,
               float* adv_out, float* vtarget_out, void* stream);
 
-/* mean f32 [N][3], log_std f32 [3]; act/logp f32 [N][3].                     */
+/* mean f32 [N][3], log_std f32 [3]; act/logp f32 [N][3].  The Philox
+ * counter's step is `step` plus, if step_base (a device u64) is non-NULL,
+ * *step_base -- so a captured hipGraph replays with fresh noise once the
+ * caller advances *step_base.                                              */
 int satrl_gaussian_sample(int64_t N, const float* mean, const float* log_std, float max_action, uint64_t seed,
-                          uint32_t agent, int64_t env_offset, uint64_t step, float* act_out, float* logp_out,
-                          void* stream);
+                          uint32_t agent, int64_t env_offset, uint64_t step, const uint64_t* step_base,
+                          float* act_out, float* logp_out, void* stream);
 
 /* out f64[2] += (sum x, sum x^2) over x f32 [n]  (out must be zeroed first) */
 int satrl_moments(int64_t n, const float* x, double* out, void* stream);

@@ -73,11 +73,13 @@ __device__ __forceinline__ float u01(uint32_t x) {         // [0, 1)
 __global__ void __launch_bounds__(256) gaussian_kernel(int64_t N, const float* __restrict__ mean,
                                                        const float* __restrict__ log_std, float max_action,
                                                        uint32_t k0, uint32_t k1, int64_t env_offset,
-                                                       uint64_t step, float* __restrict__ act,
+                                                       uint64_t step, const uint64_t* __restrict__ step_base,
+                                                       float* __restrict__ act,
                                                        float* __restrict__ logp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const uint64_t gid = (uint64_t)(env_offset + i);
+  if (step_base) step += *step_base;
   uint32_t c[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
   philox(c, k0, k1);
   float z[4];
@@ -149,13 +151,13 @@ int satrl_gae(int64_t T, int64_t N, const float* r, const uint8_t* done, const f
 }
 
 int satrl_gaussian_sample(int64_t N, const float* mean, const float* log_std, float max_action, uint64_t seed,
-                          uint32_t agent, int64_t env_offset, uint64_t step, float* act_out, float* logp_out,
-                          void* stream) {
+                          uint32_t agent, int64_t env_offset, uint64_t step, const uint64_t* step_base,
+                          float* act_out, float* logp_out, void* stream) {
   if (N <= 0 || !mean || !log_std || !act_out || !logp_out) return -1;
   const uint32_t k0 = (uint32_t)seed ^ (agent * 0x85EBCA6Bu);
   const uint32_t k1 = (uint32_t)(seed >> 32) ^ (agent * 0xC2B2AE35u + 0x27D4EB2Fu);
   hipLaunchKernelGGL(gaussian_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, N, mean,
-                     log_std, max_action, k0, k1, env_offset, step, act_out, logp_out);
+                     log_std, max_action, k0, k1, env_offset, step, step_base, act_out, logp_out);
   HIP_CHECK_LAUNCH();
   return 0;
 }
