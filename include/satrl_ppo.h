@@ -1,0 +1,82 @@
+/*
+ * satrl_ppo.h -- C ABI of the fused PPO minibatch-step kernels (gfx950).
+ *
+ * Replaces the per-minibatch body of PPO_continuous.update
+ * (qiaobeibei/PPO-RL-Satellite ppo_continuous.py:213-239): actor
+ * clipped-surrogate + entropy loss and critic MSE loss, their backward
+ * passes, clip_grad_norm_(0.5) per net and Adam(eps) per net.  Actor and
+ * critic (same hidden width H, tanh) are stepped together on the same
+ * minibatch rows; the three H x H GEMMs per step are plain library GEMMs
+ * (hipBLASLt via torch.bmm, the two nets stacked as a batch of 2), every
+ * other op is one of the kernels below.
+ *
+ * Flat parameter / gradient / Adam-moment layout (f32, see satrl_ppo_layout):
+ *   W2   [2][H][H]     fc2.weight (actor, critic)
+ *   W1   [2][H][20]    [fc1.weight(18) | fc1.bias | 0]  (actor, critic)
+ *   b2   [2][H]        fc2.bias
+ *   W3a  [3][H]        actor mean_layer.weight
+ *   b3a  [4]           actor mean_layer.bias (3 used)
+ *   ls   [4]           actor log_std (3 used)
+ *   W3c  [H]           critic fc3.weight
+ *   b3c  [4]           critic fc3.bias (1 used)
+ * Gradients are produced as split-K partial slabs (dW2 from the GEMM split
+ * S ways, [dW1|db1] from satrl_ppo_dw1, the "tail" b2..b3c (6H+12 floats)
+ * from satrl_ppo_head) and summed by satrl_ppo_reduce in a fixed order, so
+ * a step is bitwise deterministic.  Packed transition rows (src) are [B][32] f32:
+ * s(18) a(3) logp(3) adv(1) v_target(1) pad(6).
+ */
+#ifndef SATRL_PPO_H
+#define SATRL_PPO_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SATRL_PPO_OFF_W2 = 0, SATRL_PPO_OFF_W1, SATRL_PPO_OFF_B2, SATRL_PPO_OFF_W3A, SATRL_PPO_OFF_B3A,
+       SATRL_PPO_OFF_LS, SATRL_PPO_OFF_W3C, SATRL_PPO_OFF_B3C, SATRL_PPO_TOTAL, SATRL_PPO_NOFF };
+
+/* host helper: element offsets of the flat layout for hidden width H (64, 128 or 256) */
+int satrl_ppo_layout(int H, int64_t* offsets /* [SATRL_PPO_NOFF] */);
+/* number of head workgroups (= partial slabs) and F4 blocks for a minibatch of mb rows */
+int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
+
+/* gather mb rows of src by idx, fc1 + tanh for both nets:
+ * H1 [2][mb][H], saug [mb][20] = [s | 1 | 0], aux [mb][8] = a logp_old adv v_target */
+int satrl_ppo_fwd1(int H, int mb, const float* src, const int64_t* idx, const float* P, float* H1, float* saug,
+                   float* aux, void* stream);
+
+/* fc2 bias + tanh, output layers, both losses and their gradients down to
+ * dZ2 [2][mb][H]; tail partials [n_head_wg][6H+12]; optional per-row
+ * losses [mb][2] (nullable).  hyper = {epsilon, entropy_coef, max_action}. */
+int satrl_ppo_head(int H, int mb, const float* Z2, const float* P, const float* aux, float epsilon,
+                   float entropy_coef, float max_action, float* dZ2, float* partials, float* row_loss, void* stream);
+
+/* dZ1 = dH1 * (1 - H1^2), n elements (in place allowed) */
+int satrl_ppo_tanh_bwd(int64_t n, const float* dH1, const float* H1, float* dZ1, void* stream);
+
+/* [dW1 | db1] split-K partials: dZ1 = dH1 * (1 - H1^2) formed on the fly,
+ * part [satrl_ppo_w1_chunks(mb)][2][H][20]                                */
+int satrl_ppo_w1_chunks(int mb);
+int satrl_ppo_dw1(int H, int mb, const float* dH1, const float* H1, const float* saug, float* part, void* stream);
+
+/* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
+ * satrl_ppo_dw1 slabs, pt: satrl_ppo_head tail slabs); mode 2: per-block
+ * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and
+ * advance steps [2] (f64); mode 3: both.  (mode 1 | all-reduce(G) | mode 2
+ * under data parallelism.)  Every sum has a fixed order.                  */
+int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const float* p1, const float* pt, float* G,
+                     double* nsq, double* steps, void* stream);
+
+/* clip_grad_norm_(max_norm) per net (use_clip) + torch Adam (lerp form) per
+ * net: lr [2] f32 device, betas/eps host scalars. */
+int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const float* lr, float beta1, float beta2,
+                   float eps, float max_norm, int use_clip, const float* G, float* P, float* M, float* V,
+                   void* stream);
+
+const char* satrl_ppo_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

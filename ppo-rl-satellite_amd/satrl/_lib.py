@@ -77,6 +77,18 @@ _SIGS = {
                               C.c_int),
     "satrl_moments": ([_i64, _vp, _vp, _vp], C.c_int),
     "satrl_last_error": ([], C.c_char_p),
+    "satrl_ppo_layout": ([C.c_int, C.POINTER(_i64)], C.c_int),
+    "satrl_ppo_sizes": ([C.c_int, C.c_int, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
+    "satrl_ppo_fwd1": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_head": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp, _vp, _vp],
+                       C.c_int),
+    "satrl_ppo_tanh_bwd": ([_i64, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_w1_chunks": ([C.c_int], C.c_int),
+    "satrl_ppo_dw1": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_adam": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, _vp,
+                        _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_last_error": ([], C.c_char_p),
 }
 
 
@@ -104,7 +116,9 @@ def lib():
 
 def check(rc: int, what: str):
     if rc != 0:
-        msg = lib().satenv_last_error().decode() if what.startswith("satenv") else lib().satrl_last_error().decode()
+        L = lib()
+        msg = (L.satenv_last_error() if what.startswith("satenv") else
+               L.satrl_ppo_last_error() if what.startswith("satrl_ppo") else L.satrl_last_error()).decode()
         raise NativeError(f"{what} failed ({rc}): {msg}")
 
 

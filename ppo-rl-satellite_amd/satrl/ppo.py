@@ -15,6 +15,7 @@ The ``Actor_Beta`` policy (ppo_continuous.py:14-59) is outside the hot path
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
 
@@ -65,7 +66,7 @@ class Actor_Gaussian(nn.Module):  # noqa: N801
         return torch.distributions.Normal(mean, std, validate_args=False)
 
     def save_checkpoint(self):
-        torch.save(self.state_dict(), self.chkpt_file)
+        torch.save({k: v.detach().cpu().clone() for k, v in self.state_dict().items()}, self.chkpt_file)
 
     def load_checkpoint(self):
         self.load_state_dict(torch.load(self.chkpt_file, weights_only=True, map_location="cpu"))
@@ -93,7 +94,7 @@ class Critic(nn.Module):
         return self.fc3(s)
 
     def save_checkpoint(self):
-        torch.save(self.state_dict(), self.chkpt_file)
+        torch.save({k: v.detach().cpu().clone() for k, v in self.state_dict().items()}, self.chkpt_file)
 
     def load_checkpoint(self):
         self.load_state_dict(torch.load(self.chkpt_file, weights_only=True, map_location="cpu"))
@@ -141,143 +142,134 @@ def moments(x, out=None):
 
 
 # ---------------------------------------------------------------------------
-# minibatch step (ppo_continuous.py:213-239)
+# fused minibatch step (ppo_continuous.py:213-239), include/satrl_ppo.h
 # ---------------------------------------------------------------------------
-class MinibatchStepper:
-    """Actor + critic clipped-surrogate / MSE step on index batches.
+OFF_NAMES = ["W2", "W1", "b2", "W3a", "b3a", "ls", "W3c", "b3c", "total"]
 
-    The step for a fixed minibatch size is captured once into a hipGraph
-    holding ``group`` consecutive minibatches; each replay consumes one
-    [group, mb] block of a device permutation.  ``src`` is the packed
-    transition table [B, 32] f32: s(18) a(3) logp(3) adv(1) v_target(1) pad.
-    With a process group, gradients of both nets are averaged with one
-    bucketed all-reduce per minibatch (eager, between two captured halves).
-    """
 
-    S, A, LP, ADV, VT = slice(0, 18), slice(18, 21), slice(21, 24), slice(24, 25), slice(25, 26)
+def ppo_layout(H):
+    off = (C.c_int64 * 9)()
+    check(_lib.lib().satrl_ppo_layout(int(H), off), "satrl_ppo_layout")
+    return dict(zip(OFF_NAMES, [int(v) for v in off]))
 
-    def __init__(self, learner, mb, group, pg=None, use_graph=True):
+
+class FusedMinibatch:
+    """One PPO minibatch step for actor + critic on shared rows:
+    5 HIP kernels + 3 hipBLASLt GEMMs (torch.bmm over the stacked nets; the
+    K = mb weight-gradient GEMM split S ways into partial slabs).
+    Captured into hipGraphs of ``group`` consecutive minibatches, replayed
+    over [group, mb] blocks of a device permutation."""
+
+    def __init__(self, learner, mb, group, use_graph=True, splitk=4):
         self.L = learner
-        self.mb = mb
-        self.group = group
-        self.pg = pg
-        self.use_graph = use_graph and torch.cuda.is_available()
-        dev = learner.device
-        self.idx = torch.zeros((group, mb), dtype=torch.int64, device=dev)
+        self.mb = int(mb)
+        self.group = int(group)
+        self.use_graph = use_graph
+        self.S = splitk if self.mb % splitk == 0 else 1
+        H, dev = learner.H, learner.device
+        nwg, nblk = C.c_int64(), C.c_int64()
+        check(_lib.lib().satrl_ppo_sizes(H, self.mb, C.byref(nwg), C.byref(nblk)), "satrl_ppo_sizes")
+        self.nwg, self.nblk = nwg.value, nblk.value
+        self.nw1 = _lib.lib().satrl_ppo_w1_chunks(self.mb)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.H1 = torch.empty(2 * self.mb * H, **f32)
+        self.Z2 = torch.empty(2 * self.mb * H, **f32)       # also dH1
+        self.dZ2 = torch.empty(2 * self.mb * H, **f32)
+        self.saug = torch.empty(self.mb * 20, **f32)
+        self.aux = torch.empty(self.mb * 8, **f32)
+        self.partials = torch.empty(self.nwg * (6 * H + 12), **f32)
+        self.p1 = torch.empty(self.nw1 * 2 * H * 20, **f32)
+        self.p2 = torch.empty(2 * self.S * H * H, **f32)
+        self.nsq = torch.zeros(2 * self.nblk, dtype=torch.float64, device=dev)
+        self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         self.graph = None
-        self.graph_b = None
         self._src_ptr = None
 
-    # one minibatch: ppo_continuous.py:216-239, actor first then critic
-    def _actor_loss(self, rows):
+    def step(self, src, idx, mb=None):
         L = self.L
-        s, a, lp_old, adv = rows[:, self.S], rows[:, self.A], rows[:, self.LP], rows[:, self.ADV]
-        mean = L.actor(s)
-        log_std = L.actor.log_std.expand_as(mean)
-        std = torch.exp(log_std)
-        var = std ** 2
-        log_scale = std.log()
-        logp = -((a - mean) ** 2) / (2 * var) - log_scale - LOG_SQRT_2PI        # Normal.log_prob
-        ent = (ENT_CONST + torch.log(std)).sum(1, keepdim=True)                 # Normal.entropy().sum(1)
-        ratios = torch.exp(logp.sum(1, keepdim=True) - lp_old.sum(1, keepdim=True))
-        surr1 = ratios * adv
-        surr2 = torch.clamp(ratios, 1 - L.epsilon, 1 + L.epsilon) * adv
-        return (-torch.min(surr1, surr2) - L.entropy_coef * ent).mean()
-
-    def _critic_loss(self, rows):
-        return F.mse_loss(rows[:, self.VT], self.L.critic(rows[:, self.S]))
-
-    def _fwd_bwd(self, src, idx):
-        L = self.L
-        rows = src.index_select(0, idx)
-        L.opt_a.zero_grad(set_to_none=False)
-        self._actor_loss(rows).backward()
-        L.opt_c.zero_grad(set_to_none=False)
-        self._critic_loss(rows).backward()
-
-    def _apply(self):
-        L = self.L
-        if L.use_grad_clip:
-            torch.nn.utils.clip_grad_norm_(L.actor_params, 0.5)
-        L.opt_a.step()
-        if L.use_grad_clip:
-            torch.nn.utils.clip_grad_norm_(L.critic_params, 0.5)
-        L.opt_c.step()
-
-    def _allreduce(self):
-        import torch.distributed as dist
-        L = self.L
-        grads = [p.grad for p in L.actor_params + L.critic_params]
-        flat = torch._utils._flatten_dense_tensors(grads)
-        dist.all_reduce(flat, group=self.pg)
-        flat.div_(dist.get_world_size(self.pg))
-        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-            g.copy_(f)
-
-    def _eager_group(self, src, ng):
-        for k in range(ng):
-            self._fwd_bwd(src, self.idx[k])
-            if self.pg is not None:
-                self._allreduce()
-            self._apply()
+        H = L.H
+        mb = self.mb if mb is None else int(mb)
+        S = self.S if mb % self.S == 0 else 1
+        lib, sp = _lib.lib(), stream_ptr()
+        n = 2 * mb * H
+        H1, Z2, dZ2 = self.H1[:n], self.Z2[:n], self.dZ2[:n]
+        check(lib.satrl_ppo_fwd1(H, mb, ptr(src), ptr(idx), ptr(L.P), ptr(H1), ptr(self.saug), ptr(self.aux), sp),
+              "satrl_ppo_fwd1")
+        H1v, Z2v, dZ2v = H1.view(2, mb, H), Z2.view(2, mb, H), dZ2.view(2, mb, H)
+        torch.bmm(H1v, L.W2v.transpose(1, 2), out=Z2v)                       # fc2 (both nets)
+        check(lib.satrl_ppo_head(H, mb, ptr(Z2), ptr(L.P), ptr(self.aux), float(L.epsilon), float(L.entropy_coef),
+                                 float(L.max_action), ptr(dZ2), ptr(self.partials), None, sp), "satrl_ppo_head")
+        torch.bmm(dZ2v, L.W2v, out=Z2v)                                       # dH1 (reuses Z2)
+        # dW2 split-K S ways: [2S, mb/S, H]^T @ [2S, mb/S, H] -> slabs [2][S][H][H]
+        p2v = self.p2[:2 * S * H * H].view(2 * S, H, H)
+        torch.bmm(dZ2.view(2 * S, mb // S, H).transpose(1, 2), H1.view(2 * S, mb // S, H), out=p2v)
+        check(lib.satrl_ppo_dw1(H, mb, ptr(Z2), ptr(H1), ptr(self.saug), ptr(self.p1), sp), "satrl_ppo_dw1")
+        if L.pg is None:
+            check(lib.satrl_ppo_reduce(H, mb, S, 3, ptr(self.p2), ptr(self.p1), ptr(self.partials), ptr(L.G),
+                                       ptr(self.nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
+        else:
+            import torch.distributed as dist
+            check(lib.satrl_ppo_reduce(H, mb, S, 1, ptr(self.p2), ptr(self.p1), ptr(self.partials), ptr(L.G), None,
+                                       None, sp), "satrl_ppo_reduce")
+            dist.all_reduce(L.G, group=L.pg)                                  # one bucket, both nets
+            L.G.div_(dist.get_world_size(L.pg))
+            check(lib.satrl_ppo_reduce(H, mb, S, 2, None, None, None, ptr(L.G), ptr(self.nsq), ptr(L.steps), sp),
+                  "satrl_ppo_reduce")
+        check(lib.satrl_ppo_adam(H, mb, ptr(self.nsq), ptr(L.steps), ptr(L.lr), float(L.beta1), float(L.beta2),
+                                 float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)), ptr(L.G), ptr(L.P), ptr(L.M),
+                                 ptr(L.V), sp), "satrl_ppo_adam")
 
     def _capture(self, src):
-        # warm up on a side stream (allocates grads / optimizer state), then capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                self._fwd_bwd(src, self.idx[0])
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             for k in range(self.group):
-                self._fwd_bwd(src, self.idx[k])
-                self._apply()
+                self.step(src, self.idx[k])
         self._src_ptr = src.data_ptr()
 
     def run(self, src, perm):
-        """Run all minibatches of one epoch; perm int64 [B] on device."""
+        """All minibatches of one epoch (BatchSampler drop_last=False order)."""
         B = perm.numel()
         mb, G = self.mb, self.group
         nfull = B // mb
+        graphable = self.use_graph and self.L.pg is None and torch.cuda.is_available()
         k = 0
-        graphable = self.use_graph and self.pg is None
-        if graphable and (self.graph is None or self._src_ptr != src.data_ptr()):
-            # optimizer state must exist before capture: one eager warm step on a
-            # zero-lr copy is not needed -- Adam(capturable) allocates lazily, so
-            # the first group runs eagerly.
-            if not self.L._opt_ready:
-                ng = min(G, nfull)
-                self.idx[:ng].copy_(perm[: ng * mb].view(ng, mb))
-                self._eager_group(src, ng)
-                self.L._opt_ready = True
-                k = ng
-            if nfull - k >= G:
-                self._capture(src)
         while k < nfull:
             ng = min(G, nfull - k)
             self.idx[:ng].copy_(perm[k * mb:(k + ng) * mb].view(ng, mb))
-            if graphable and ng == G and self.graph is not None:
+            if graphable and ng == G:
+                if self.graph is None or self._src_ptr != src.data_ptr():
+                    self._capture(src)
                 self.graph.replay()
             else:
-                self._eager_group(src, ng)
+                for j in range(ng):
+                    self.step(src, self.idx[j])
             k += ng
-        if B % mb:                                     # drop_last=False tail
-            tail = perm[nfull * mb:]
-            self._fwd_bwd(src, tail)
-            if self.pg is not None:
-                self._allreduce()
-            self._apply()
+        if B % mb:
+            tail = perm[nfull * mb:].contiguous()
+            self.step(src, tail, mb=tail.numel())
+
+
+def _bind(module, name, view):
+    """Make module.<name> a Parameter that aliases ``view`` (flat storage)."""
+    module._parameters[name] = nn.Parameter(view, requires_grad=False)
 
 
 class PPOLearner:
-    """Actor/critic pair + optimizers + batched update (device resident)."""
+    """Actor/critic pair whose parameters, gradients and Adam moments live in
+    flat device buffers (include/satrl_ppo.h layout); the nn.Module
+    parameters are views into ``P`` so every forward pass (rollout, values,
+    evaluate) reads the weights the fused update writes."""
 
     def __init__(self, args, agent_idx, device=None, pg=None, graph_group=16, use_graph=True):
         self.device = torch.device("cuda") if device is None else torch.device(device)
         self.args = args
-        self.max_action = args.max_action
+        self.H = int(args.hidden_width)
+        if not args.use_tanh:
+            raise NotImplementedError("the fused update implements the tanh networks (use_tanh=True, CPPO_main.py:38)")
+        self.max_action = float(args.max_action)
         self.batch_size = args.batch_size
         self.mini_batch_size = args.mini_batch_size
         self.max_train_steps = args.max_train_steps
@@ -289,22 +281,46 @@ class PPOLearner:
         self.use_grad_clip = args.use_grad_clip
         self.use_lr_decay = args.use_lr_decay
         self.use_adv_norm = args.use_adv_norm
-        # CPU init with the reference's RNG consumption order (actor, then critic)
-        actor = Actor_Gaussian(args, agent_idx)
-        critic = Critic(args, agent_idx)
-        self.actor = actor.to(self.device)
-        self.critic = critic.to(self.device)
-        self.actor_params = list(self.actor.parameters())
-        self.critic_params = list(self.critic.parameters())
-        eps = 1e-5 if args.set_adam_eps else 1e-8
-        self._lr_a_t = torch.tensor(float(self.lr_a), device=self.device)
-        self._lr_c_t = torch.tensor(float(self.lr_c), device=self.device)
-        self.opt_a = torch.optim.Adam(self.actor_params, lr=self._lr_a_t, eps=eps, capturable=True, foreach=True)
-        self.opt_c = torch.optim.Adam(self.critic_params, lr=self._lr_c_t, eps=eps, capturable=True, foreach=True)
-        self._opt_ready = False
+        self.beta1, self.beta2 = 0.9, 0.999                  # torch.optim.Adam defaults
+        self.adam_eps = 1e-5 if args.set_adam_eps else 1e-8  # ppo_continuous.py:161-166
         self.pg = pg
         self.graph_group = graph_group
         self.use_graph = use_graph
+        # CPU init with the reference's RNG consumption order (actor, then critic)
+        actor = Actor_Gaussian(args, agent_idx)
+        critic = Critic(args, agent_idx)
+        self.off = ppo_layout(self.H)
+        H, o = self.H, self.off
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.P = torch.zeros(o["total"], **f32)
+        self.G = torch.zeros(o["total"], **f32)
+        self.M = torch.zeros(o["total"], **f32)
+        self.V = torch.zeros(o["total"], **f32)
+        self.steps = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.lr = torch.tensor([float(self.lr_a), float(self.lr_c)], **f32)
+        self.actor = actor.to(self.device)
+        self.critic = critic.to(self.device)
+        P = self.P
+        self.W2v = P[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
+        self.GW2v = self.G[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
+        W1 = P[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
+        self.GW1v = self.G[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
+        b2 = P[o["b2"]:o["b2"] + 2 * H].view(2, H)
+        views = {
+            (self.actor.fc1, "weight"): W1[0, :, :18], (self.actor.fc1, "bias"): W1[0, :, 18],
+            (self.critic.fc1, "weight"): W1[1, :, :18], (self.critic.fc1, "bias"): W1[1, :, 18],
+            (self.actor.fc2, "weight"): self.W2v[0], (self.actor.fc2, "bias"): b2[0],
+            (self.critic.fc2, "weight"): self.W2v[1], (self.critic.fc2, "bias"): b2[1],
+            (self.actor.mean_layer, "weight"): P[o["W3a"]:o["W3a"] + 3 * H].view(3, H),
+            (self.actor.mean_layer, "bias"): P[o["b3a"]:o["b3a"] + 3],
+            (self.actor, "log_std"): P[o["ls"]:o["ls"] + 3].view(1, 3),
+            (self.critic.fc3, "weight"): P[o["W3c"]:o["W3c"] + H].view(1, H),
+            (self.critic.fc3, "bias"): P[o["b3c"]:o["b3c"] + 1],
+        }
+        with torch.no_grad():
+            for (mod, name), view in views.items():
+                view.copy_(getattr(mod, name).detach())
+                _bind(mod, name, view)
         self._steppers = {}
 
     # -- lr ---------------------------------------------------------------------
@@ -312,33 +328,48 @@ class PPOLearner:
         """ppo_continuous.py:244-250."""
         lr_a_now = self.lr_a * (1 - total_steps / self.max_train_steps)
         lr_c_now = self.lr_c * (1 - total_steps / self.max_train_steps)
-        self._lr_a_t.fill_(lr_a_now)
-        self._lr_c_t.fill_(lr_c_now)
-        for p in self.opt_a.param_groups:
-            p["lr"] = self._lr_a_t
-        for p in self.opt_c.param_groups:
-            p["lr"] = self._lr_c_t
+        self.lr.copy_(torch.tensor([lr_a_now, lr_c_now], dtype=torch.float32))
 
     @property
     def lr_now(self):
-        return float(self._lr_a_t.item()), float(self._lr_c_t.item())
+        v = self.lr.cpu().tolist()
+        return v[0], v[1]
+
+    def param_groups(self):
+        """(actor params, critic params) as tensors, reference order."""
+        return list(self.actor.parameters()), list(self.critic.parameters())
+
+    def flat_views(self, buf):
+        """{"actor.fc1.weight": view, ...} of a flat buffer (P, G, M or V)."""
+        H, o = self.H, self.off
+        W1 = buf[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
+        W2 = buf[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
+        b2 = buf[o["b2"]:o["b2"] + 2 * H].view(2, H)
+        return {"actor.fc1.weight": W1[0, :, :18], "actor.fc1.bias": W1[0, :, 18],
+                "actor.fc2.weight": W2[0], "actor.fc2.bias": b2[0],
+                "actor.mean_layer.weight": buf[o["W3a"]:o["W3a"] + 3 * H].view(3, H),
+                "actor.mean_layer.bias": buf[o["b3a"]:o["b3a"] + 3],
+                "actor.log_std": buf[o["ls"]:o["ls"] + 3].view(1, 3),
+                "critic.fc1.weight": W1[1, :, :18], "critic.fc1.bias": W1[1, :, 18],
+                "critic.fc2.weight": W2[1], "critic.fc2.bias": b2[1],
+                "critic.fc3.weight": buf[o["W3c"]:o["W3c"] + H].view(1, H),
+                "critic.fc3.bias": buf[o["b3c"]:o["b3c"] + 1]}
 
     # -- update -----------------------------------------------------------------
     def stepper(self, mb):
         if mb not in self._steppers:
-            self._steppers[mb] = MinibatchStepper(self, mb, self.graph_group, pg=self.pg, use_graph=self.use_graph)
+            self._steppers[mb] = FusedMinibatch(self, mb, self.graph_group, use_graph=self.use_graph)
         return self._steppers[mb]
 
     def normalize_adv(self, adv):
         """ppo_continuous.py:209-210 (unbiased std); global over the process group."""
         if not self.use_adv_norm:
             return adv
-        n_local = adv.numel()
         if self.pg is None:
             return (adv - adv.mean()) / (adv.std() + 1e-5)
         import torch.distributed as dist
         m = moments(adv)
-        cnt = torch.tensor([float(n_local)], dtype=torch.float64, device=adv.device)
+        cnt = torch.tensor([float(adv.numel())], dtype=torch.float64, device=adv.device)
         buf = torch.cat([m, cnt])
         dist.all_reduce(buf, group=self.pg)
         s, s2, n = buf[0], buf[1], buf[2]
@@ -350,12 +381,9 @@ class PPOLearner:
         """K epochs of minibatch steps over the packed table src [B, 32]
         (adv already normalised), then lr decay (ppo_continuous.py:212-242)."""
         B = src.shape[0]
-        st = self.stepper(self.mini_batch_size)
+        st = self.stepper(min(self.mini_batch_size, B))
         for ep in range(self.K_epochs):
-            if perms is not None:
-                perm = perms[ep]
-            else:
-                perm = torch.randperm(B, device=self.device, generator=generator)
+            perm = perms[ep] if perms is not None else torch.randperm(B, device=self.device, generator=generator)
             st.run(src, perm)
         if self.use_lr_decay:
             self.lr_decay(total_steps)
@@ -394,14 +422,6 @@ class PPO_continuous:  # noqa: N801
         self.mini_batch_size = args.mini_batch_size
         self.K_epochs = args.K_epochs
         self.gamma, self.lamda = args.gamma, args.lamda
-
-    @property
-    def optimizer_actor(self):
-        return self.L.opt_a
-
-    @property
-    def optimizer_critic(self):
-        return self.L.opt_c
 
     def _obs(self, s):
         return torch.as_tensor(np.asarray(s), dtype=torch.float32).reshape(1, -1).to(self.L.device)

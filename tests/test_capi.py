@@ -19,6 +19,7 @@ def test_headers_declare_expected_entry_points():
     assert {"satenv_create", "satenv_reset", "satenv_step", "satenv_step_autoreset", "satenv_destroy",
             "satenv_get_state", "satenv_set_state", "satenv_last_error"} <= env
     assert {"satrl_gae", "satrl_gaussian_sample", "satrl_moments"} <= _declared("satrl_rollout.h")
+    assert {"satrl_ppo_fwd1", "satrl_ppo_head", "satrl_ppo_reduce", "satrl_ppo_adam"} <= _declared("satrl_ppo.h")
 
 
 def test_library_exports_every_declared_symbol():
@@ -26,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     if not os.path.exists(L.LIB_PATH):
         L.build()
     lib = L.lib()          # loads with torch's HIP runtime; no device needed
-    declared = _declared("satenv.h") | _declared("satrl_rollout.h")
+    declared = _declared("satenv.h") | _declared("satrl_rollout.h") | _declared("satrl_ppo.h")
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(L.exported_symbols()) == declared
