@@ -52,7 +52,7 @@ def cpu_baseline(seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
-    n = 4096
+    n = 16384
     rng = np.random.default_rng(0)
     # calibrate steps for ~`seconds` of work
     steps = 4
@@ -61,7 +61,7 @@ def cpu_baseline(seconds):
     t0 = time.perf_counter()
     O.rollout(n, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=threads)
     dt = time.perf_counter() - t0
-    steps = int(max(4, min(400, steps * seconds / max(dt, 1e-3))))
+    steps = int(max(4, min(4096, steps * seconds / max(dt, 1e-3))))
     pa = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
     ea = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
     t0 = time.perf_counter()

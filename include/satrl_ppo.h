@@ -69,10 +69,12 @@ int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const floa
                      double* nsq, double* steps, void* stream);
 
 /* clip_grad_norm_(max_norm) per net (use_clip) + torch Adam (lerp form) per
- * net: lr [2] f32 device, betas/eps host scalars. */
-int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const float* lr, float beta1, float beta2,
-                   float eps, float max_norm, int use_clip, const float* G, float* P, float* M, float* V,
-                   void* stream);
+ * net: lr [2] f32 device; bct f64 [bct_len][2] = {1 - beta1**k, sqrt(1 -
+ * beta2**k)} for step k computed on the host with python-float math (as
+ * torch.optim.Adam does), 1.0 past the table.                             */
+int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const double* bct, int bct_len,
+                   const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
+                   float* P, float* M, float* V, void* stream);
 
 const char* satrl_ppo_last_error(void);
 

@@ -22,6 +22,7 @@ namespace {
 thread_local std::string g_err;
 
 constexpr int kRows = 16;          // minibatch rows per fwd1/head workgroup
+constexpr int kF1Rows = 8;         // rows per fwd1 workgroup
 constexpr int kW1Rows = 32;        // rows per dw1 workgroup (split-K chunk of [dW1 | db1])
 constexpr float kLogSqrt2Pi = 0.9189385332046727f;   // math.log(math.sqrt(2*math.pi))
 
@@ -60,8 +61,8 @@ __global__ void __launch_bounds__(H) fwd1_kernel(int mb, const float* __restrict
                                                  const float* __restrict__ P, float* __restrict__ H1,
                                                  float* __restrict__ saug, float* __restrict__ aux) {
   const Layout L = layout(H);
-  __shared__ float s[kRows][20];
-  const int r0 = blockIdx.x * kRows;
+  __shared__ float s[kF1Rows][20];
+  const int r0 = blockIdx.x * kF1Rows;
   const int t = threadIdx.x;
   // W1 rows of this thread's hidden unit for both nets: 2 x 5 float4 loads
   const float4* wa4 = reinterpret_cast<const float4*>(P + L.W1 + (int64_t)t * 20);
@@ -69,7 +70,7 @@ __global__ void __launch_bounds__(H) fwd1_kernel(int mb, const float* __restrict
   float4 qa[5], qc[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) { qa[k] = wa4[k]; qc[k] = wc4[k]; }
-  for (int q = t; q < kRows * 26; q += H) {
+  for (int q = t; q < kF1Rows * 26; q += H) {
     const int r = q / 26, c = q % 26, row = r0 + r;
     float v = 0.0f;
     if (row < mb) v = src[idx[row] * 32 + c];
@@ -77,7 +78,7 @@ __global__ void __launch_bounds__(H) fwd1_kernel(int mb, const float* __restrict
     else if (row < mb) aux[(int64_t)row * 8 + (c - 18)] = v;
   }
   __syncthreads();
-  for (int q = t; q < kRows * 20; q += H) {
+  for (int q = t; q < kF1Rows * 20; q += H) {
     const int r = q / 20, c = q % 20, row = r0 + r;
     if (row < mb) saug[(int64_t)row * 20 + c] = c < 18 ? s[r][c] : (c == 18 ? 1.0f : 0.0f);
   }
@@ -86,7 +87,7 @@ __global__ void __launch_bounds__(H) fwd1_kernel(int mb, const float* __restrict
   const float wc[20] = {qc[0].x, qc[0].y, qc[0].z, qc[0].w, qc[1].x, qc[1].y, qc[1].z, qc[1].w, qc[2].x, qc[2].y,
                         qc[2].z, qc[2].w, qc[3].x, qc[3].y, qc[3].z, qc[3].w, qc[4].x, qc[4].y, qc[4].z, qc[4].w};
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {
+  for (int r = 0; r < kF1Rows; ++r) {
     const int row = r0 + r;
     float za = 0.0f, zc = 0.0f;
 #pragma unroll
@@ -109,62 +110,48 @@ __global__ void __launch_bounds__(H) fwd1_kernel(int mb, const float* __restrict
 template <int H>
 __global__ void __launch_bounds__(H) dw1_kernel(int mb, const float* __restrict__ dH1, const float* __restrict__ H1,
                                                 const float* __restrict__ saug, float* __restrict__ part) {
-  __shared__ float s[kW1Rows][20];
+  __shared__ __attribute__((aligned(16))) float s[kW1Rows][20];
   const int r0 = blockIdx.x * kW1Rows;
+  const int net = blockIdx.y;                                      // 0 actor, 1 critic
   const int t = threadIdx.x;
   for (int q = t; q < kW1Rows * 20; q += H) {
     const int r = q / 20, c = q % 20, row = r0 + r;
     s[r][c] = row < mb ? saug[(int64_t)row * 20 + c] : 0.0f;
   }
-  float za[kW1Rows], zc[kW1Rows];
+  float g[kW1Rows], y[kW1Rows];
+  const int64_t base = (int64_t)net * mb;
 #pragma unroll
-  for (int r = 0; r < kW1Rows; ++r) {
+  for (int r = 0; r < kW1Rows; ++r) {                              // all loads in flight together
     const int row = min(r0 + r, mb - 1);
-    const float ga = dH1[(int64_t)row * H + t], ya = H1[(int64_t)row * H + t];
-    const float gc = dH1[((int64_t)mb + row) * H + t], yc = H1[((int64_t)mb + row) * H + t];
-    const bool ok = r0 + r < mb;
-    za[r] = ok ? ga * (1.0f - ya * ya) : 0.0f;                     // tanh backward
-    zc[r] = ok ? gc * (1.0f - yc * yc) : 0.0f;
+    g[r] = dH1[(base + row) * H + t];
+    y[r] = H1[(base + row) * H + t];
   }
   __syncthreads();
-  float aa[20], ac[20];
+  float acc[20];
 #pragma unroll
-  for (int k = 0; k < 20; ++k) { aa[k] = 0.0f; ac[k] = 0.0f; }
+  for (int k = 0; k < 20; ++k) acc[k] = 0.0f;
 #pragma unroll
   for (int r = 0; r < kW1Rows; ++r) {
+    const float dz = (r0 + r < mb) ? g[r] * (1.0f - y[r] * y[r]) : 0.0f;   // tanh backward
 #pragma unroll
-    for (int k = 0; k < 20; ++k) {
-      aa[k] = fmaf(za[r], s[r][k], aa[k]);
-      ac[k] = fmaf(zc[r], s[r][k], ac[k]);
+    for (int k4 = 0; k4 < 5; ++k4) {
+      const float4 sv = *reinterpret_cast<const float4*>(&s[r][4 * k4]);
+      acc[4 * k4 + 0] = fmaf(dz, sv.x, acc[4 * k4 + 0]);
+      acc[4 * k4 + 1] = fmaf(dz, sv.y, acc[4 * k4 + 1]);
+      acc[4 * k4 + 2] = fmaf(dz, sv.z, acc[4 * k4 + 2]);
+      acc[4 * k4 + 3] = fmaf(dz, sv.w, acc[4 * k4 + 3]);
     }
   }
-  float4* pa = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * H * 20 + (int64_t)t * 20);
-  float4* pc = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * H * 20 + (int64_t)(H + t) * 20);
+  float4* pp = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * H * 20 + (int64_t)(net * H + t) * 20);
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    pa[k] = make_float4(aa[4 * k], aa[4 * k + 1], aa[4 * k + 2], aa[4 * k + 3]);
-    pc[k] = make_float4(ac[4 * k], ac[4 * k + 1], ac[4 * k + 2], ac[4 * k + 3]);
-  }
-}
-
-// reduce-scatter of 64 per-lane values across a wave: lane l ends with sum of value l
-__device__ __forceinline__ float wave_reduce_scatter64(float (&v)[64]) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) {
-    const bool upper = (lane & s) != 0;
-#pragma unroll
-    for (int i = 0; i < s; ++i) {
-      const float send = upper ? v[i] : v[i + s];
-      const float keep = upper ? v[i + s] : v[i];
-      v[i] = keep + __shfl_xor(send, s, 64);
-    }
-  }
-  return v[0];
+  for (int k = 0; k < 5; ++k) pp[k] = make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
 }
 
 // ---------------------------------------------------------------------------
-// head: ppo_continuous.py:216-239 per row, both nets.
+// head: ppo_continuous.py:216-239 per row, both nets.  Thread j = hidden unit.
+// The output layers (3 actor dots + 1 critic dot per row over H) go through
+// an LDS transpose: [2][kRows][H] activations, then 4 threads per (row,
+// output) each sum H/4 products and finish with two xor-shuffles.
 // ---------------------------------------------------------------------------
 template <int H>
 __global__ void __launch_bounds__(H) head_kernel(int mb, const float* __restrict__ Z2, const float* __restrict__ P,
@@ -172,21 +159,21 @@ __global__ void __launch_bounds__(H) head_kernel(int mb, const float* __restrict
                                                  float max_action, float* __restrict__ dZ2,
                                                  float* __restrict__ partials, float* __restrict__ row_loss) {
   const Layout L = layout(H);
-  constexpr int NW = H / 64;
-  __shared__ float red[NW][64];
+  static_assert(H >= 64 && H % 64 == 0, "H");
+  __shared__ __attribute__((aligned(16))) float hs[2][kRows][H];   // tanh(fc2) activations
+  __shared__ __attribute__((aligned(16))) float w3s[4][H];          // W3a rows 0..2, W3c
+  __shared__ float sums[kRows][4];
   __shared__ float dz3s[kRows][4];
   __shared__ float lsp[kRows][4];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x;
   const int r0 = blockIdx.x * kRows;
   const float b2a = P[L.b2 + t], b2c = P[L.b2 + H + t];
   const float w30 = P[L.W3a + t], w31 = P[L.W3a + H + t], w32 = P[L.W3a + 2 * H + t];
   const float w3c = P[L.W3c + t];
+  w3s[0][t] = w30; w3s[1][t] = w31; w3s[2][t] = w32; w3s[3][t] = w3c;
   float ha[kRows], hc[kRows];
-  float v[64];
-  // issue every Z2 load of the workgroup's rows before the first use (one
-  // wave per SIMD: the loads must be in flight together, not one per tanh)
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {
+  for (int r = 0; r < kRows; ++r) {                                  // all loads in flight together
     const int row = min(r0 + r, mb - 1);
     ha[r] = Z2[(int64_t)row * H + t];
     hc[r] = Z2[((int64_t)mb + row) * H + t];
@@ -194,35 +181,43 @@ __global__ void __launch_bounds__(H) head_kernel(int mb, const float* __restrict
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const bool ok = r0 + r < mb;
-    const float a = ok ? tanhf(ha[r] + b2a) : 0.0f;               // actor fc2 + tanh
-    const float c = ok ? tanhf(hc[r] + b2c) : 0.0f;               // critic fc2 + tanh
-    ha[r] = a;
-    hc[r] = c;
-    v[4 * r + 0] = a * w30;
-    v[4 * r + 1] = a * w31;
-    v[4 * r + 2] = a * w32;
-    v[4 * r + 3] = c * w3c;
+    ha[r] = ok ? tanhf(ha[r] + b2a) : 0.0f;                        // actor fc2 + tanh
+    hc[r] = ok ? tanhf(hc[r] + b2c) : 0.0f;                        // critic fc2 + tanh
+    hs[0][r][t] = ha[r];
+    hs[1][r][t] = hc[r];
   }
-  red[w][lane] = wave_reduce_scatter64(v);
+  __syncthreads();
+  // 64 (row, output) dots x 4 partial threads; H threads cover 64*4/H rounds
+  for (int o4 = t; o4 < kRows * 4 * 4; o4 += H) {
+    const int o = o4 >> 2, part = o4 & 3;
+    const int r = o >> 2, q = o & 3;
+    const float* hrow = &hs[q == 3 ? 1 : 0][r][part * (H / 4)];
+    const float* wrow = &w3s[q][part * (H / 4)];
+    float acc = 0.0f;
+#pragma unroll 8
+    for (int k = 0; k < H / 4; k += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(hrow + k);
+      const float4 y = *reinterpret_cast<const float4*>(wrow + k);
+      acc = fmaf(x.x, y.x, acc);
+      acc = fmaf(x.y, y.y, acc);
+      acc = fmaf(x.z, y.z, acc);
+      acc = fmaf(x.w, y.w, acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (part == 0) sums[r][q] = acc;
+  }
   __syncthreads();
   if (t < kRows) {
     const int r = t, row = r0 + r;
     float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
     if (row < mb) {
-      float sums[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float s = 0.0f;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) s += red[k][4 * r + q];
-        sums[q] = s;
-      }
       const float* ax = aux + (int64_t)row * 8;
       const float inv = 1.0f / (float)mb;
       float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
-        th[d] = tanhf(sums[d] + P[L.b3a + d]);
+        th[d] = tanhf(sums[r][d] + P[L.b3a + d]);
         mu[d] = max_action * th[d];                                  // 1.6 * tanh(mean_layer)
         const float sd = expf(P[L.ls + d]);
         var[d] = sd * sd;
@@ -249,7 +244,7 @@ __global__ void __launch_bounds__(H) head_kernel(int mb, const float* __restrict
         dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
         dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
       }
-      const float vc = sums[3] + P[L.b3c];
+      const float vc = sums[r][3] + P[L.b3c];
       const float vt = ax[7];
       dz[3] = 2.0f * inv * (vc - vt);                                // d mse / d v
       if (row_loss) {
@@ -329,6 +324,9 @@ __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
     a = 0.0; c = 0.0;
     for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) { sh[0] = a; sh[1] = c; }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -345,8 +343,10 @@ __device__ __forceinline__ float chunk_sum(const float* __restrict__ part, int64
                                            bool valid, float (*sh)[CH + 1]) {
   const int t = threadIdx.x, e = t % E, c = t / E;
   float s = 0.0f;
-  if (valid)
+  if (valid) {
+#pragma unroll 8
     for (int w = c; w < nparts; w += CH) s += part[(int64_t)w * stride + el];
+  }
   sh[e][c] = s;
   __syncthreads();
   float tot = 0.0f;
@@ -429,8 +429,9 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
 // adam: torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (_single_tensor_adam)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double* __restrict__ nsq,
-                                                   const double* __restrict__ steps, const float* __restrict__ lr,
-                                                   float beta1, float beta2, float eps, float max_norm, int use_clip,
+                                                   const double* __restrict__ steps, const double* __restrict__ bct,
+                                                   int bct_len, const float* __restrict__ lr, float beta1,
+                                                   float beta2, float eps, float max_norm, int use_clip,
                                                    const float* __restrict__ G, float* __restrict__ P,
                                                    float* __restrict__ M, float* __restrict__ V) {
   const Layout L = layout(H);
@@ -439,15 +440,18 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   double a = 0.0, c = 0.0;
   for (int k = threadIdx.x; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
   block_sum2(a, c, sh);
-  if (threadIdx.x == 0) {
-    const float nrm[2] = {(float)sqrt(a), (float)sqrt(c)};
-    for (int n = 0; n < 2; ++n) {
-      cst[n][0] = use_clip ? fminf(max_norm / (nrm[n] + 1e-6f), 1.0f) : 1.0f;
-      const double bc1 = 1.0 - pow((double)beta1, steps[n]);
-      const double bc2 = 1.0 - pow((double)beta2, steps[n]);
-      cst[n][1] = (float)((double)lr[n] / bc1);
-      cst[n][2] = (float)sqrt(bc2);
-    }
+  if (threadIdx.x < 2) {
+    const int n = threadIdx.x;
+    const double nn = n == 0 ? sh[0] : sh[1];
+    const float nrm = (float)sqrt(nn);
+    cst[n][0] = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
+    // bct[2*step] = 1 - beta1**step, bct[2*step+1] = sqrt(1 - beta2**step) (python float
+    // math, as torch.optim.Adam computes them); constant 1.0 past the table
+    const int st = (int)steps[n];
+    const double bc1 = st < bct_len ? bct[2 * st] : 1.0;
+    const double bc2s = st < bct_len ? bct[2 * st + 1] : 1.0;
+    cst[n][1] = (float)((double)lr[n] / bc1);
+    cst[n][2] = (float)bc2s;
   }
   __syncthreads();
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
@@ -520,7 +524,7 @@ int satrl_ppo_w1_chunks(int mb) { return mb > 0 ? n_w1_wg(mb) : -1; }
 
 int satrl_ppo_dw1(int H, int mb, const float* dH1, const float* H1, const float* saug, float* part, void* stream) {
   if (!valid_h(H) || mb <= 0 || !dH1 || !H1 || !saug || !part) return -1;
-  dim3 gr(n_w1_wg(mb));
+  dim3 gr(n_w1_wg(mb), 2);
   hipStream_t s = (hipStream_t)stream;
   if (H == 64) hipLaunchKernelGGL(dw1_kernel<64>, gr, dim3(64), 0, s, mb, dH1, H1, saug, part);
   else if (H == 128) hipLaunchKernelGGL(dw1_kernel<128>, gr, dim3(128), 0, s, mb, dH1, H1, saug, part);
@@ -532,7 +536,7 @@ int satrl_ppo_dw1(int H, int mb, const float* dH1, const float* H1, const float*
 int satrl_ppo_fwd1(int H, int mb, const float* src, const int64_t* idx, const float* P, float* H1, float* saug,
                    float* aux, void* stream) {
   if (!valid_h(H) || mb <= 0 || !src || !idx || !P || !H1 || !saug || !aux) return -1;
-  dim3 g(n_head_wg(mb));
+  dim3 g((mb + kF1Rows - 1) / kF1Rows);
   hipStream_t s = (hipStream_t)stream;
   if (H == 64) hipLaunchKernelGGL(fwd1_kernel<64>, g, dim3(64), 0, s, mb, src, idx, P, H1, saug, aux);
   else if (H == 128) hipLaunchKernelGGL(fwd1_kernel<128>, g, dim3(128), 0, s, mb, src, idx, P, H1, saug, aux);
@@ -582,15 +586,15 @@ int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const floa
   return 0;
 }
 
-int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const float* lr, float beta1, float beta2,
-                   float eps, float max_norm, int use_clip, const float* G, float* P, float* M, float* V,
-                   void* stream) {
-  if (!valid_h(H) || mb <= 0 || !nsq || !steps || !lr || !G || !P || !M || !V) return -1;
+int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const double* bct, int bct_len,
+                   const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
+                   float* P, float* M, float* V, void* stream) {
+  if (!valid_h(H) || mb <= 0 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P || !M || !V) return -1;
   const Layout L = layout(H);
   const int nblk = n_blocks(geom(H, mb, 1));
   const int blocks = (int)((L.total + 1023) / 1024);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps, lr, beta1,
-                     beta2, eps, max_norm, use_clip, G, P, M, V);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps, bct, bct_len,
+                     lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V);
   LAUNCH_CHECK();
   return 0;
 }

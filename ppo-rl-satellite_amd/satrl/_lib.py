@@ -86,8 +86,8 @@ _SIGS = {
     "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_w1_chunks": ([C.c_int], C.c_int),
     "satrl_ppo_dw1": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_adam": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, _vp,
-                        _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_adam": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float, C.c_float,
+                        C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_last_error": ([], C.c_char_p),
 }
 

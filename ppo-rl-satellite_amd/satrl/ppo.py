@@ -215,9 +215,9 @@ class FusedMinibatch:
             L.G.div_(dist.get_world_size(L.pg))
             check(lib.satrl_ppo_reduce(H, mb, S, 2, None, None, None, ptr(L.G), ptr(self.nsq), ptr(L.steps), sp),
                   "satrl_ppo_reduce")
-        check(lib.satrl_ppo_adam(H, mb, ptr(self.nsq), ptr(L.steps), ptr(L.lr), float(L.beta1), float(L.beta2),
-                                 float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)), ptr(L.G), ptr(L.P), ptr(L.M),
-                                 ptr(L.V), sp), "satrl_ppo_adam")
+        check(lib.satrl_ppo_adam(H, mb, ptr(self.nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
+                                 float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
+                                 ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), sp), "satrl_ppo_adam")
 
     def _capture(self, src):
         s = torch.cuda.Stream()
@@ -250,6 +250,22 @@ class FusedMinibatch:
         if B % mb:
             tail = perm[nfull * mb:].contiguous()
             self.step(src, tail, mb=tail.numel())
+
+
+def adam_bias_table(beta1=0.9, beta2=0.999):
+    """{1 - beta1**k, sqrt(1 - beta2**k)} in python-float math, as
+    torch.optim.Adam._single_tensor_adam computes them per step; rows up to
+    the step where both are exactly 1.0."""
+    rows = [(0.0, 0.0)]
+    k = 1
+    while True:
+        b1 = 1 - beta1 ** k
+        b2 = math.sqrt(1 - beta2 ** k)
+        rows.append((b1, b2))
+        if b1 == 1.0 and b2 == 1.0:
+            break
+        k += 1
+    return torch.tensor(rows, dtype=torch.float64)
 
 
 def _bind(module, name, view):
@@ -297,6 +313,7 @@ class PPOLearner:
         self.M = torch.zeros(o["total"], **f32)
         self.V = torch.zeros(o["total"], **f32)
         self.steps = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.bct = adam_bias_table(self.beta1, self.beta2).to(self.device)
         self.lr = torch.tensor([float(self.lr_a), float(self.lr_c)], **f32)
         self.actor = actor.to(self.device)
         self.critic = critic.to(self.device)
