@@ -6,9 +6,10 @@
  * clipped-surrogate + entropy loss and critic MSE loss, their backward
  * passes, clip_grad_norm_(0.5) per net and Adam(eps) per net.  Actor and
  * critic (same hidden width H, tanh) are stepped together on the same
- * minibatch rows; the three H x H GEMMs per step are plain library GEMMs
- * (hipBLASLt via torch.bmm, the two nets stacked as a batch of 2), every
- * other op is one of the kernels below.
+ * minibatch rows.  Per minibatch: satrl_ppo_rowpass (everything that is
+ * row-parallel, incl. the two H x H products on f32 MFMA), the dW2 weight
+ * gradient as a plain library GEMM (hipBLASLt via torch.bmm, split-K),
+ * satrl_ppo_reduce and satrl_ppo_adam.
  *
  * Flat parameter / gradient / Adam-moment layout (f32, see satrl_ppo_layout):
  *   W2   [2][H][H]     fc2.weight (actor, critic)
@@ -20,9 +21,9 @@
  *   W3c  [H]           critic fc3.weight
  *   b3c  [4]           critic fc3.bias (1 used)
  * Gradients are produced as split-K partial slabs (dW2 from the GEMM split
- * S ways, [dW1|db1] from satrl_ppo_dw1, the "tail" b2..b3c (6H+12 floats)
- * from satrl_ppo_head) and summed by satrl_ppo_reduce in a fixed order, so
- * a step is bitwise deterministic.  Packed transition rows (src) are [B][32] f32:
+ * S ways, [dW1|db1] and the "tail" b2..b3c (6H+12 floats) from
+ * satrl_ppo_rowpass) and summed by satrl_ppo_reduce in a fixed order, so a
+ * step is bitwise deterministic.  Packed transition rows (src) are [B][32] f32:
  * s(18) a(3) logp(3) adv(1) v_target(1) pad(6).
  */
 #ifndef SATRL_PPO_H
@@ -41,27 +42,8 @@ int satrl_ppo_layout(int H, int64_t* offsets /* [SATRL_PPO_NOFF] */);
 /* number of head workgroups (= partial slabs) and F4 blocks for a minibatch of mb rows */
 int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
 
-/* gather mb rows of src by idx, fc1 + tanh for both nets:
- * H1 [2][mb][H], saug [mb][20] = [s | 1 | 0], aux [mb][8] = a logp_old adv v_target */
-int satrl_ppo_fwd1(int H, int mb, const float* src, const int64_t* idx, const float* P, float* H1, float* saug,
-                   float* aux, void* stream);
-
-/* fc2 bias + tanh, output layers, both losses and their gradients down to
- * dZ2 [2][mb][H]; tail partials [n_head_wg][6H+12]; optional per-row
- * losses [mb][2] (nullable).  hyper = {epsilon, entropy_coef, max_action}. */
-int satrl_ppo_head(int H, int mb, const float* Z2, const float* P, const float* aux, float epsilon,
-                   float entropy_coef, float max_action, float* dZ2, float* partials, float* row_loss, void* stream);
-
-/* dZ1 = dH1 * (1 - H1^2), n elements (in place allowed) */
-int satrl_ppo_tanh_bwd(int64_t n, const float* dH1, const float* H1, float* dZ1, void* stream);
-
-/* [dW1 | db1] split-K partials: dZ1 = dH1 * (1 - H1^2) formed on the fly,
- * part [satrl_ppo_w1_chunks(mb)][2][H][20]                                */
-int satrl_ppo_w1_chunks(int mb);
-int satrl_ppo_dw1(int H, int mb, const float* dH1, const float* H1, const float* saug, float* part, void* stream);
-
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
- * satrl_ppo_dw1 slabs, pt: satrl_ppo_head tail slabs); mode 2: per-block
+ * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
  * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and
  * advance steps [2] (f64); mode 3: both.  (mode 1 | all-reduce(G) | mode 2
  * under data parallelism.)  Every sum has a fixed order.                  */
@@ -74,7 +56,19 @@ int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const floa
  * torch.optim.Adam does), 1.0 past the table.                             */
 int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
-                   float* P, float* M, float* V, void* stream);
+                   float* P, float* M, float* V, float* W2T /* nullable: also write fc2.weight^T */,
+                   void* stream);
+
+/* The row-parallel part of one minibatch step in ONE launch (16 rows per
+ * workgroup): gather + fc1 + tanh, fc2 (f32 MFMA), output layers, both
+ * losses and their gradients, backprop through fc2 (f32 MFMA on W2T =
+ * fc2.weight^T per net, [2][H][H]) and tanh(fc1).  Writes H1 and dZ2
+ * [2][mb][H] (inputs of the dW2 GEMM), the tail partial slabs
+ * [ceil(mb/16)][6H+12] and the [dW1 | db1] partial slabs
+ * [ceil(mb/16)][2][H][20].                                                */
+int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const float* P, const float* W2T,
+                      float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
+                      float* pw1, void* stream);
 
 const char* satrl_ppo_last_error(void);
 

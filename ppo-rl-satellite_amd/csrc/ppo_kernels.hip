@@ -1,14 +1,13 @@
 // ppo_kernels.hip -- fused PPO minibatch-step kernels for gfx950 (include/satrl_ppo.h).
 //
-// Per minibatch (actor + critic together, same rows):
-//   fwd1   gather rows (packed [B][32]) + fc1 + tanh           -> H1, saug, aux
-//   [bmm]  Z2  = H1 @ W2^T                                      (hipBLASLt, batch 2)
-//   head   fc2 bias+tanh, output layers, losses, d/dZ2, tail partial slabs
-//   [bmm]  dH1 = dZ2 @ W2 ; G.W2 = dZ2^T @ H1
-//   tanh_bwd dZ1 = dH1 * (1 - H1^2)
-//   [bmm]  G.W1 = dZ1^T @ saug      ([dW1 | db1] in one GEMM via the ones column)
-//   reduce tail partials -> G, per-block squared norms per net
-//   adam   clip coefficient per net + Adam (torch single-tensor formula)
+// Per minibatch (actor + critic together, same rows), four launches:
+//   rowpass  gather, fc1, fc2 (f32 MFMA), output layers, losses, backprop to
+//            dZ2 and through fc2 (f32 MFMA) and fc1's tanh; writes H1, dZ2
+//            and partial slabs of every small gradient
+//   [bmm]    dW2 = dZ2^T @ H1 split-K S ways (hipBLASLt, batch 2S)
+//   reduce   partial slabs -> G (fixed order), per-block squared norms per net
+//   adam     clip coefficient per net + Adam (torch single-tensor formula),
+//            also refreshes fc2.weight^T used by the next rowpass
 // Every reduction has a fixed order, so a step is bitwise reproducible.
 #include <hip/hip_runtime.h>
 
@@ -21,9 +20,8 @@ namespace {
 
 thread_local std::string g_err;
 
-constexpr int kRows = 16;          // minibatch rows per fwd1/head workgroup
-constexpr int kF1Rows = 8;         // rows per fwd1 workgroup
-constexpr int kW1Rows = 32;        // rows per dw1 workgroup (split-K chunk of [dW1 | db1])
+constexpr int kRows = 16;          // minibatch rows per rowpass workgroup
+
 constexpr float kLogSqrt2Pi = 0.9189385332046727f;   // math.log(math.sqrt(2*math.pi))
 
 struct Layout {
@@ -54,185 +52,221 @@ __device__ __forceinline__ int net_of(const Layout& L, int64_t e, int H) {
 }
 
 // ---------------------------------------------------------------------------
-// fwd1: gather + fc1 + tanh.  One workgroup = kRows rows, thread j = hidden unit.
+// rowpass: the whole row-parallel part of a minibatch step in one launch.
+// One workgroup = 16 minibatch rows, 4 waves; wave w owns net w>>1 and the
+// column half (w&1) of the hidden layer: T = H/32 MFMA tiles of 16x16.
+//   A  gather rows -> S (LDS); Z1 = [S|1] W1aug^T       f32 MFMA 16x16x4
+//   B  Z2 = tanh(Z1) W2^T                               f32 MFMA, W2 from L2
+//   C  tanh(fc2), output layers, both losses, dZ2 -> LDS/HBM, tail partials
+//   D  dH1 = dZ2 W2 (rows of W2T = fc2.weight^T)        f32 MFMA
+//   E  dZ1 = dH1 (1 - H1^2); [dW1|db1] = dZ1^T [S|1]    f32 MFMA, dZ1's
+//      accumulator layout is already the A operand
+// Accumulator layout of a 16x16x4 tile: acc[t][j] = D[row 4*lg + j][col li].
+// Inside a 32-wide k chunk lane group g takes k = 32c + 8g + kk (kk < 8), so
+// every B fetch is a 32-B run of a 128-B line and A comes as 2 ds_read_b128
+// from rows padded by 16 B.
 // ---------------------------------------------------------------------------
-template <int H>
-__global__ void __launch_bounds__(H) fwd1_kernel(int mb, const float* __restrict__ src, const int64_t* __restrict__ idx,
-                                                 const float* __restrict__ P, float* __restrict__ H1,
-                                                 float* __restrict__ saug, float* __restrict__ aux) {
-  const Layout L = layout(H);
-  __shared__ float s[kF1Rows][20];
-  const int r0 = blockIdx.x * kF1Rows;
-  const int t = threadIdx.x;
-  // W1 rows of this thread's hidden unit for both nets: 2 x 5 float4 loads
-  const float4* wa4 = reinterpret_cast<const float4*>(P + L.W1 + (int64_t)t * 20);
-  const float4* wc4 = reinterpret_cast<const float4*>(P + L.W1 + (int64_t)(H + t) * 20);
-  float4 qa[5], qc[5];
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[t] (t < T) += A[16][K] (LDS, row stride LDA) x B^T with B[n][k] row-major
+// (ld LDB) for columns n0 + 16t; tiles are processed 4 at a time, 32-k chunks,
+// next chunk's B prefetched into registers during the current chunk's MFMAs.
+template <int K, int LDA, int LDB, int T>
+__device__ __forceinline__ void mfma_rows16(const float* __restrict__ A, const float* __restrict__ B, int n0,
+                                            f4 (&acc)[T]) {
+  constexpr int TG = T < 4 ? T : 4;
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
 #pragma unroll
-  for (int k = 0; k < 5; ++k) { qa[k] = wa4[k]; qc[k] = wc4[k]; }
-  for (int q = t; q < kF1Rows * 26; q += H) {
+  for (int t0 = 0; t0 < T; t0 += TG) {
+    float4 b0[TG], b1[TG], n0v[TG], n1v[TG];
+#pragma unroll
+    for (int t = 0; t < TG; ++t) {
+      const float* bp = B + (int64_t)(n0 + 16 * (t0 + t) + i) * LDB + 8 * g;
+      b0[t] = *reinterpret_cast<const float4*>(bp);
+      b1[t] = *reinterpret_cast<const float4*>(bp + 4);
+    }
+#pragma unroll 1
+    for (int c = 0; c < K / 32; ++c) {
+      if (c + 1 < K / 32) {
+#pragma unroll
+        for (int t = 0; t < TG; ++t) {
+          const float* bp = B + (int64_t)(n0 + 16 * (t0 + t) + i) * LDB + 32 * (c + 1) + 8 * g;
+          n0v[t] = *reinterpret_cast<const float4*>(bp);
+          n1v[t] = *reinterpret_cast<const float4*>(bp + 4);
+        }
+      }
+      const float4 a0 = *reinterpret_cast<const float4*>(A + i * LDA + 32 * c + 8 * g);
+      const float4 a1 = *reinterpret_cast<const float4*>(A + i * LDA + 32 * c + 8 * g + 4);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.x, b0[t].x, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.y, b0[t].y, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.z, b0[t].z, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.w, b0[t].w, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.x, b1[t].x, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.y, b1[t].y, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.z, b1[t].z, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.w, b1[t].w, acc[t0 + t]);
+#pragma unroll
+      for (int t = 0; t < TG; ++t) { b0[t] = n0v[t]; b1[t] = n1v[t]; }
+    }
+  }
+}
+
+template <int H, int NW>
+__global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* __restrict__ src,
+                                                      const int64_t* __restrict__ idx, const float* __restrict__ P,
+                                                      const float* __restrict__ W2T, float epsilon, float ent_coef,
+                                                      float max_action, float* __restrict__ H1g,
+                                                      float* __restrict__ dZ2g, float* __restrict__ ptail,
+                                                      float* __restrict__ pw1) {
+  // NW waves: the first NW/2 own the actor, the rest the critic; each wave a
+  // slice of H/(NW/2) hidden columns = T tiles of 16
+  constexpr int R = 16, LDA = H + 4, HW = NW / 2, T = H / 16 / HW, LDS_S = 36, NT = NW * 64;
+  static_assert(T >= 1 && H % (16 * HW) == 0, "tile split");
+  const Layout L = layout(H);
+  __shared__ __attribute__((aligned(16))) float h1s[2][R][LDA];     // tanh(fc1)
+  __shared__ __attribute__((aligned(16))) float dzs[2][R][LDA];     // dZ2
+  __shared__ __attribute__((aligned(16))) float S[R][LDS_S];        // [s(18) | 1 | 0...] per row
+  __shared__ float ax[R][8];
+  __shared__ float osum[NW][R][3];
+  __shared__ float dz3s[R][4];
+  __shared__ float lsp[R][4];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
+  const int net = w / HW, n0 = (w % HW) * (H / HW);
+  const int r0 = blockIdx.x * R;
+
+  // ---- A: gather, fc1 on MFMA ------------------------------------------------
+  for (int q = tid; q < R * 26; q += NT) {
     const int r = q / 26, c = q % 26, row = r0 + r;
-    float v = 0.0f;
-    if (row < mb) v = src[idx[row] * 32 + c];
-    if (c < 18) s[r][c] = v;
-    else if (row < mb) aux[(int64_t)row * 8 + (c - 18)] = v;
+    const float v = row < mb ? src[idx[row] * 32 + c] : 0.0f;
+    if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;             // s | a, logp_old, adv, v_target
+  }
+  for (int q = tid; q < R * (LDS_S - 18); q += NT) {
+    const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
+    S[r][c] = (c == 18 && r0 + r < mb) ? 1.0f : 0.0f;             // bias column of W1aug, zero pad
   }
   __syncthreads();
-  for (int q = t; q < kF1Rows * 20; q += H) {
-    const int r = q / 20, c = q % 20, row = r0 + r;
-    if (row < mb) saug[(int64_t)row * 20 + c] = c < 18 ? s[r][c] : (c == 18 ? 1.0f : 0.0f);
-  }
-  const float wa[20] = {qa[0].x, qa[0].y, qa[0].z, qa[0].w, qa[1].x, qa[1].y, qa[1].z, qa[1].w, qa[2].x, qa[2].y,
-                        qa[2].z, qa[2].w, qa[3].x, qa[3].y, qa[3].z, qa[3].w, qa[4].x, qa[4].y, qa[4].z, qa[4].w};
-  const float wc[20] = {qc[0].x, qc[0].y, qc[0].z, qc[0].w, qc[1].x, qc[1].y, qc[1].z, qc[1].w, qc[2].x, qc[2].y,
-                        qc[2].z, qc[2].w, qc[3].x, qc[3].y, qc[3].z, qc[3].w, qc[4].x, qc[4].y, qc[4].z, qc[4].w};
+  f4 acc[T];
+  f4 h1[T];
 #pragma unroll
-  for (int r = 0; r < kF1Rows; ++r) {
-    const int row = r0 + r;
-    float za = 0.0f, zc = 0.0f;
+  for (int t = 0; t < T; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  {
+    // W1aug rows [n][20] (k 0..19) padded to 32 with zeros: lane group g takes k = 8g .. 8g+7
+    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
+    const float4 a0 = *reinterpret_cast<const float4*>(&S[li][8 * lg]);
+    const float4 a1 = *reinterpret_cast<const float4*>(&S[li][8 * lg + 4]);
 #pragma unroll
-    for (int k = 0; k < 18; ++k) {
-      za = fmaf(s[r][k], wa[k], za);
-      zc = fmaf(s[r][k], wc[k], zc);
-    }
-    if (row < mb) {
-      H1[(int64_t)row * H + t] = tanhf(za + wa[18]);               // actor fc1 + tanh
-      H1[((int64_t)mb + row) * H + t] = tanhf(zc + wc[18]);        // critic fc1 + tanh
+    for (int t = 0; t < T; ++t) {
+      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
+      float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lg < 2) { b0 = *reinterpret_cast<const float4*>(bp + 8 * lg); b1 = *reinterpret_cast<const float4*>(bp + 8 * lg + 4); }
+      else if (lg == 2) b0 = *reinterpret_cast<const float4*>(bp + 16);
+      acc[t] = mfma4(a0.x, b0.x, acc[t]); acc[t] = mfma4(a0.y, b0.y, acc[t]);
+      acc[t] = mfma4(a0.z, b0.z, acc[t]); acc[t] = mfma4(a0.w, b0.w, acc[t]);
+      acc[t] = mfma4(a1.x, b1.x, acc[t]); acc[t] = mfma4(a1.y, b1.y, acc[t]);
+      acc[t] = mfma4(a1.z, b1.z, acc[t]); acc[t] = mfma4(a1.w, b1.w, acc[t]);
     }
   }
-}
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int n = n0 + 16 * t + li;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * lg + j;
+      const float h = tanhf(acc[t][j]);                              // fc1 + tanh
+      h1[t][j] = h;
+      h1s[net][r][n] = h;
+      if (r0 + r < mb) H1g[((int64_t)net * mb + r0 + r) * H + n] = h;
+    }
+    acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
 
-// ---------------------------------------------------------------------------
-// dw1: [dW1 | db1] partials.  dZ1 = dH1 * (1 - H1^2) is formed on the fly
-// (layer 1 needs no further backprop), so neither dZ1 nor a K=mb GEMM with
-// N=20 is materialised.  One workgroup = kW1Rows rows, thread = hidden unit.
-// ---------------------------------------------------------------------------
-template <int H>
-__global__ void __launch_bounds__(H) dw1_kernel(int mb, const float* __restrict__ dH1, const float* __restrict__ H1,
-                                                const float* __restrict__ saug, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float s[kW1Rows][20];
-  const int r0 = blockIdx.x * kW1Rows;
-  const int net = blockIdx.y;                                      // 0 actor, 1 critic
-  const int t = threadIdx.x;
-  for (int q = t; q < kW1Rows * 20; q += H) {
-    const int r = q / 20, c = q % 20, row = r0 + r;
-    s[r][c] = row < mb ? saug[(int64_t)row * 20 + c] : 0.0f;
-  }
-  float g[kW1Rows], y[kW1Rows];
-  const int64_t base = (int64_t)net * mb;
-#pragma unroll
-  for (int r = 0; r < kW1Rows; ++r) {                              // all loads in flight together
-    const int row = min(r0 + r, mb - 1);
-    g[r] = dH1[(base + row) * H + t];
-    y[r] = H1[(base + row) * H + t];
-  }
-  __syncthreads();
-  float acc[20];
-#pragma unroll
-  for (int k = 0; k < 20; ++k) acc[k] = 0.0f;
-#pragma unroll
-  for (int r = 0; r < kW1Rows; ++r) {
-    const float dz = (r0 + r < mb) ? g[r] * (1.0f - y[r] * y[r]) : 0.0f;   // tanh backward
-#pragma unroll
-    for (int k4 = 0; k4 < 5; ++k4) {
-      const float4 sv = *reinterpret_cast<const float4*>(&s[r][4 * k4]);
-      acc[4 * k4 + 0] = fmaf(dz, sv.x, acc[4 * k4 + 0]);
-      acc[4 * k4 + 1] = fmaf(dz, sv.y, acc[4 * k4 + 1]);
-      acc[4 * k4 + 2] = fmaf(dz, sv.z, acc[4 * k4 + 2]);
-      acc[4 * k4 + 3] = fmaf(dz, sv.w, acc[4 * k4 + 3]);
-    }
-  }
-  float4* pp = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * H * 20 + (int64_t)(net * H + t) * 20);
-#pragma unroll
-  for (int k = 0; k < 5; ++k) pp[k] = make_float4(acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]);
-}
+  // ---- B: Z2 = H1 W2^T -------------------------------------------------------
+  mfma_rows16<H, LDA, H, T>(&h1s[net][0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
 
-// ---------------------------------------------------------------------------
-// head: ppo_continuous.py:216-239 per row, both nets.  Thread j = hidden unit.
-// The output layers (3 actor dots + 1 critic dot per row over H) go through
-// an LDS transpose: [2][kRows][H] activations, then 4 threads per (row,
-// output) each sum H/4 products and finish with two xor-shuffles.
-// ---------------------------------------------------------------------------
-template <int H>
-__global__ void __launch_bounds__(H) head_kernel(int mb, const float* __restrict__ Z2, const float* __restrict__ P,
-                                                 const float* __restrict__ aux, float epsilon, float ent_coef,
-                                                 float max_action, float* __restrict__ dZ2,
-                                                 float* __restrict__ partials, float* __restrict__ row_loss) {
-  const Layout L = layout(H);
-  static_assert(H >= 64 && H % 64 == 0, "H");
-  __shared__ __attribute__((aligned(16))) float hs[2][kRows][H];   // tanh(fc2) activations
-  __shared__ __attribute__((aligned(16))) float w3s[4][H];          // W3a rows 0..2, W3c
-  __shared__ float sums[kRows][4];
-  __shared__ float dz3s[kRows][4];
-  __shared__ float lsp[kRows][4];
-  const int t = threadIdx.x;
-  const int r0 = blockIdx.x * kRows;
-  const float b2a = P[L.b2 + t], b2c = P[L.b2 + H + t];
-  const float w30 = P[L.W3a + t], w31 = P[L.W3a + H + t], w32 = P[L.W3a + 2 * H + t];
-  const float w3c = P[L.W3c + t];
-  w3s[0][t] = w30; w3s[1][t] = w31; w3s[2][t] = w32; w3s[3][t] = w3c;
-  float ha[kRows], hc[kRows];
+  // ---- C: fc2 tanh, output layers, losses, dZ2 --------------------------------
+  float w3[T][3];
+  float b2v[T];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {                                  // all loads in flight together
-    const int row = min(r0 + r, mb - 1);
-    ha[r] = Z2[(int64_t)row * H + t];
-    hc[r] = Z2[((int64_t)mb + row) * H + t];
-  }
-#pragma unroll
-  for (int r = 0; r < kRows; ++r) {
-    const bool ok = r0 + r < mb;
-    ha[r] = ok ? tanhf(ha[r] + b2a) : 0.0f;                        // actor fc2 + tanh
-    hc[r] = ok ? tanhf(hc[r] + b2c) : 0.0f;                        // critic fc2 + tanh
-    hs[0][r][t] = ha[r];
-    hs[1][r][t] = hc[r];
-  }
-  __syncthreads();
-  // 64 (row, output) dots x 4 partial threads; H threads cover 64*4/H rounds
-  for (int o4 = t; o4 < kRows * 4 * 4; o4 += H) {
-    const int o = o4 >> 2, part = o4 & 3;
-    const int r = o >> 2, q = o & 3;
-    const float* hrow = &hs[q == 3 ? 1 : 0][r][part * (H / 4)];
-    const float* wrow = &w3s[q][part * (H / 4)];
-    float acc = 0.0f;
-#pragma unroll 8
-    for (int k = 0; k < H / 4; k += 4) {
-      const float4 x = *reinterpret_cast<const float4*>(hrow + k);
-      const float4 y = *reinterpret_cast<const float4*>(wrow + k);
-      acc = fmaf(x.x, y.x, acc);
-      acc = fmaf(x.y, y.y, acc);
-      acc = fmaf(x.z, y.z, acc);
-      acc = fmaf(x.w, y.w, acc);
+  for (int t = 0; t < T; ++t) {
+    const int n = n0 + 16 * t + li;
+    b2v[t] = P[L.b2 + net * H + n];
+    if (net == 0) {
+      w3[t][0] = P[L.W3a + n]; w3[t][1] = P[L.W3a + H + n]; w3[t][2] = P[L.W3a + 2 * H + n];
+    } else {
+      w3[t][0] = P[L.W3c + n]; w3[t][1] = 0.0f; w3[t][2] = 0.0f;
     }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    if (part == 0) sums[r][q] = acc;
+  }
+  float p[3][4];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[q][j] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float h = tanhf(acc[t][j] + b2v[t]);                    // fc2 + tanh
+      acc[t][j] = h;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) p[q][j] = fmaf(h, w3[t][q], p[q][j]);
+    }
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = p[q][j];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      p[q][j] = v;
+    }
+  if (li == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) osum[w][4 * lg + j][q] = p[q][j];
   }
   __syncthreads();
-  if (t < kRows) {
-    const int r = t, row = r0 + r;
+  if (tid < R) {
+    const int r = tid, row = r0 + r;
     float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
     if (row < mb) {
-      const float* ax = aux + (int64_t)row * 8;
       const float inv = 1.0f / (float)mb;
       float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
       for (int d = 0; d < 3; ++d) {
-        th[d] = tanhf(sums[r][d] + P[L.b3a + d]);
+        float od = 0.0f;
+#pragma unroll
+        for (int k = 0; k < HW; ++k) od += osum[k][r][d];
+        th[d] = tanhf(od + P[L.b3a + d]);
         mu[d] = max_action * th[d];                                  // 1.6 * tanh(mean_layer)
         const float sd = expf(P[L.ls + d]);
         var[d] = sd * sd;
-        dv[d] = ax[d] - mu[d];
+        dv[d] = ax[r][d] - mu[d];
         logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - logf(sd)) - kLogSqrt2Pi;
       }
       const float lsum = (logp[0] + logp[1]) + logp[2];
-      const float lold = (ax[3] + ax[4]) + ax[5];
+      const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
       const float ratio = expf(lsum - lold);
-      const float adv = ax[6];
+      const float adv = ax[r][6];
       const float s1 = ratio * adv;
       const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
       const float s2 = cr * adv;
-      // torch.min backward splits ties; clamp backward passes inside [lo, hi]
-      const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+      const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);   // torch.min tie split
       const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
       const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
       const float dmin = -inv;
@@ -244,69 +278,85 @@ __global__ void __launch_bounds__(H) head_kernel(int mb, const float* __restrict
         dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
         dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
       }
-      const float vc = sums[r][3] + P[L.b3c];
-      const float vt = ax[7];
-      dz[3] = 2.0f * inv * (vc - vt);                                // d mse / d v
-      if (row_loss) {
-        float ent = 0.0f;
+      float oc = 0.0f;
 #pragma unroll
-        for (int d = 0; d < 3; ++d) ent += 0.5f + 0.5f * 1.8378770664093453f + logf(expf(P[L.ls + d]));
-        row_loss[(int64_t)row * 2 + 0] = -fminf(s1, s2) - ent_coef * ent;
-        row_loss[(int64_t)row * 2 + 1] = (vt - vc) * (vt - vc);
-      }
+      for (int k = 0; k < HW; ++k) oc += osum[HW + k][r][0];
+      const float vc = oc + P[L.b3c];
+      dz[3] = 2.0f * inv * (vc - ax[r][7]);                          // d mse / d v
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      dz3s[r][q] = dz[q];
-      lsp[r][q] = dls[q];
-    }
+    for (int q = 0; q < 4; ++q) { dz3s[r][q] = dz[q]; lsp[r][q] = dls[q]; }
   }
   __syncthreads();
-  float db2a = 0.f, db2c = 0.f, g30 = 0.f, g31 = 0.f, g32 = 0.f, g3c = 0.f;
+  float* tp = ptail + (int64_t)blockIdx.x * L.tail;                  // tail-relative slab
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) {
-    const int row = r0 + r;
-    const float d0 = dz3s[r][0], d1 = dz3s[r][1], d2 = dz3s[r][2], dc = dz3s[r][3];   // 0 past mb
-    const float dha = (d0 * w30 + d1 * w31) + d2 * w32;            // dZ3 @ W3
-    const float dza = dha * (1.0f - ha[r] * ha[r]);                // tanh backward
-    const float dzc = (dc * w3c) * (1.0f - hc[r] * hc[r]);
-    if (row < mb) {
-      dZ2[(int64_t)row * H + t] = dza;
-      dZ2[((int64_t)mb + row) * H + t] = dzc;
+  for (int t = 0; t < T; ++t) {
+    const int n = n0 + 16 * t + li;
+    float cb2 = 0.f, cw[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * lg + j;
+      const float h = acc[t][j];
+      float dh;
+      if (net == 0) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
+      else dh = dz3s[r][3] * w3[t][0];
+      const float d2 = dh * (1.0f - h * h);                         // tanh backward
+      dzs[net][r][n] = d2;
+      if (r0 + r < mb) dZ2g[((int64_t)net * mb + r0 + r) * H + n] = d2;
+      cb2 += d2;
+      if (net == 0) {
+        cw[0] = fmaf(dz3s[r][0], h, cw[0]); cw[1] = fmaf(dz3s[r][1], h, cw[1]); cw[2] = fmaf(dz3s[r][2], h, cw[2]);
+      } else {
+        cw[0] = fmaf(dz3s[r][3], h, cw[0]);
+      }
     }
-    db2a += dza;
-    db2c += dzc;
-    g30 += d0 * ha[r];
-    g31 += d1 * ha[r];
-    g32 += d2 * ha[r];
-    g3c += dc * hc[r];
+    cb2 += __shfl_xor(cb2, 16, 64); cb2 += __shfl_xor(cb2, 32, 64);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) { cw[q] += __shfl_xor(cw[q], 16, 64); cw[q] += __shfl_xor(cw[q], 32, 64); }
+    if (lg == 0) {
+      tp[net * H + n] = cb2;                                         // db2
+      if (net == 0) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
+      else tp[5 * H + 8 + n] = cw[0];                                // dW3c
+    }
   }
-  float* part = partials + (int64_t)blockIdx.x * L.tail;           // tail-relative layout
-  part[t] = db2a;
-  part[H + t] = db2c;
-  part[2 * H + t] = g30;
-  part[3 * H + t] = g31;
-  part[4 * H + t] = g32;
-  part[5 * H + 8 + t] = g3c;
-  if (t < 4) {
+  if (tid < 4) {
     float sb = 0.f, sl = 0.f, sc = 0.f;
-    for (int r = 0; r < kRows; ++r) {
-      sb += t < 3 ? dz3s[r][t] : 0.0f;
-      sl += t < 3 ? lsp[r][t] : 0.0f;
-      sc += t == 0 ? dz3s[r][3] : 0.0f;
+    for (int r = 0; r < R; ++r) {
+      sb += tid < 3 ? dz3s[r][tid] : 0.0f;
+      sl += tid < 3 ? lsp[r][tid] : 0.0f;
+      sc += tid == 0 ? dz3s[r][3] : 0.0f;
     }
-    part[5 * H + t] = sb;            // b3a
-    part[5 * H + 4 + t] = sl;        // log_std
-    part[6 * H + 8 + t] = sc;        // b3c
+    tp[5 * H + tid] = sb;            // b3a
+    tp[5 * H + 4 + tid] = sl;        // log_std
+    tp[6 * H + 8 + tid] = sc;        // b3c
   }
-}
+  __syncthreads();
 
-__global__ void __launch_bounds__(256) tanh_bwd_kernel(int64_t n4, const float4* __restrict__ dh,
-                                                       const float4* __restrict__ h, float4* __restrict__ dz) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 g = dh[i], y = h[i];
-    dz[i] = make_float4(g.x * (1.0f - y.x * y.x), g.y * (1.0f - y.y * y.y), g.z * (1.0f - y.z * y.z),
-                        g.w * (1.0f - y.w * y.w));
+  // ---- D: dH1 = dZ2 W2 -------------------------------------------------------
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  mfma_rows16<H, LDA, H, T>(&dzs[net][0][0], W2T + (int64_t)net * H * H, n0, acc);
+
+  // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
+  // acc[t][j] = dZ1[row 4lg+j][n0+16t+li] is the A operand A[n][r] of the
+  // product (k = row, kk = j); B[r][k'] = S[4lg+kk][16h + li] from LDS.
+  float* pw = pw1 + (int64_t)blockIdx.x * 2 * H * 20 + (int64_t)net * H * 20;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[t][j] = acc[t][j] * (1.0f - h1[t][j] * h1[t][j]);   // tanh backward
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      f4 d = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[t][kk], S[4 * lg + kk][16 * hb + li], d);
+      // d[j] = dW1aug[n = n0 + 16t + 4lg + j][k' = 16hb + li]
+      const int kp = 16 * hb + li;
+      if (kp < 20) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pw[(int64_t)(n0 + 16 * t + 4 * lg + j) * 20 + kp] = d[j];
+      }
+    }
   }
 }
 
@@ -433,7 +483,8 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
                                                    int bct_len, const float* __restrict__ lr, float beta1,
                                                    float beta2, float eps, float max_norm, int use_clip,
                                                    const float* __restrict__ G, float* __restrict__ P,
-                                                   float* __restrict__ M, float* __restrict__ V) {
+                                                   float* __restrict__ M, float* __restrict__ V,
+                                                   float* __restrict__ W2T) {
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float cst[2][3];                                      // coef, step_size, bc2_sqrt per net
@@ -465,14 +516,19 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
     float v = V[e];
     v = v * beta2 + w2 * (g * g);                                  // mul_(beta2).addcmul_(g, g, 1 - beta2)
     const float denom = sqrtf(v) / cst[net][2] + eps;
-    P[e] = P[e] + (-cst[net][1]) * (m / denom);                    // addcdiv_(m, denom, -step_size)
+    const float pn = P[e] + (-cst[net][1]) * (m / denom);          // addcdiv_(m, denom, -step_size)
+    P[e] = pn;
     M[e] = m;
     V[e] = v;
+    if (W2T != nullptr && e < L.W1) {                              // keep fc2.weight^T for the dH1 MFMA
+      const int64_t HH = (int64_t)H * H, k = e % HH;
+      W2T[(e / HH) * HH + (k % H) * H + k / H] = pn;
+    }
   }
 }
 
 int n_head_wg(int mb) { return (mb + kRows - 1) / kRows; }
-int n_w1_wg(int mb) { return (mb + kW1Rows - 1) / kW1Rows; }
+int n_w1_wg(int mb) { return n_head_wg(mb); }
 RedGeom geom(int H, int mb, int S) {
   const Layout L = layout(H);
   RedGeom g;
@@ -520,59 +576,31 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
   return 0;
 }
 
-int satrl_ppo_w1_chunks(int mb) { return mb > 0 ? n_w1_wg(mb) : -1; }
-
-int satrl_ppo_dw1(int H, int mb, const float* dH1, const float* H1, const float* saug, float* part, void* stream) {
-  if (!valid_h(H) || mb <= 0 || !dH1 || !H1 || !saug || !part) return -1;
-  dim3 gr(n_w1_wg(mb), 2);
-  hipStream_t s = (hipStream_t)stream;
-  if (H == 64) hipLaunchKernelGGL(dw1_kernel<64>, gr, dim3(64), 0, s, mb, dH1, H1, saug, part);
-  else if (H == 128) hipLaunchKernelGGL(dw1_kernel<128>, gr, dim3(128), 0, s, mb, dH1, H1, saug, part);
-  else hipLaunchKernelGGL(dw1_kernel<256>, gr, dim3(256), 0, s, mb, dH1, H1, saug, part);
-  LAUNCH_CHECK();
-  return 0;
-}
-
-int satrl_ppo_fwd1(int H, int mb, const float* src, const int64_t* idx, const float* P, float* H1, float* saug,
-                   float* aux, void* stream) {
-  if (!valid_h(H) || mb <= 0 || !src || !idx || !P || !H1 || !saug || !aux) return -1;
-  dim3 g((mb + kF1Rows - 1) / kF1Rows);
-  hipStream_t s = (hipStream_t)stream;
-  if (H == 64) hipLaunchKernelGGL(fwd1_kernel<64>, g, dim3(64), 0, s, mb, src, idx, P, H1, saug, aux);
-  else if (H == 128) hipLaunchKernelGGL(fwd1_kernel<128>, g, dim3(128), 0, s, mb, src, idx, P, H1, saug, aux);
-  else hipLaunchKernelGGL(fwd1_kernel<256>, g, dim3(256), 0, s, mb, src, idx, P, H1, saug, aux);
-  LAUNCH_CHECK();
-  return 0;
-}
-
-int satrl_ppo_head(int H, int mb, const float* Z2, const float* P, const float* aux, float epsilon, float ent_coef,
-                   float max_action, float* dZ2, float* partials, float* row_loss, void* stream) {
-  if (!valid_h(H) || mb <= 0 || !Z2 || !P || !aux || !dZ2 || !partials) return -1;
+int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const float* P, const float* W2T,
+                      float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
+                      float* pw1, void* stream) {
+  if (!valid_h(H) || mb <= 0 || !src || !idx || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1) return -1;
   dim3 g(n_head_wg(mb));
   hipStream_t s = (hipStream_t)stream;
+  // waves per workgroup: two tiles of 16 hidden columns per wave, so a CU
+  // keeps 16 waves' worth of W2 fetches in flight (the GEMM phases are
+  // L2-latency bound at one wave per SIMD)
   if (H == 64)
-    hipLaunchKernelGGL(head_kernel<64>, g, dim3(64), 0, s, mb, Z2, P, aux, epsilon, ent_coef, max_action, dZ2,
-                       partials, row_loss);
+    hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
+                       max_action, H1, dZ2, ptail, pw1);
   else if (H == 128)
-    hipLaunchKernelGGL(head_kernel<128>, g, dim3(128), 0, s, mb, Z2, P, aux, epsilon, ent_coef, max_action, dZ2,
-                       partials, row_loss);
+    hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
+                       max_action, H1, dZ2, ptail, pw1);
   else
-    hipLaunchKernelGGL(head_kernel<256>, g, dim3(256), 0, s, mb, Z2, P, aux, epsilon, ent_coef, max_action, dZ2,
-                       partials, row_loss);
+    hipLaunchKernelGGL((rowpass_kernel<256, 16>), g, dim3(1024), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
+                       max_action, H1, dZ2, ptail, pw1);
   LAUNCH_CHECK();
   return 0;
 }
 
-int satrl_ppo_tanh_bwd(int64_t n, const float* dH1, const float* H1, float* dZ1, void* stream) {
-  if (n <= 0 || (n & 3) || !dH1 || !H1 || !dZ1) return -1;
-  const int64_t n4 = n / 4;
-  int64_t blocks = (n4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(tanh_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n4,
-                     (const float4*)dH1, (const float4*)H1, (float4*)dZ1);
-  LAUNCH_CHECK();
-  return 0;
-}
+
+
+
 
 int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const float* p1, const float* pt, float* G,
                      double* nsq, double* steps, void* stream) {
@@ -588,13 +616,13 @@ int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const floa
 
 int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
-                   float* P, float* M, float* V, void* stream) {
+                   float* P, float* M, float* V, float* W2T, void* stream) {
   if (!valid_h(H) || mb <= 0 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P || !M || !V) return -1;
   const Layout L = layout(H);
   const int nblk = n_blocks(geom(H, mb, 1));
   const int blocks = (int)((L.total + 1023) / 1024);
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps, bct, bct_len,
-                     lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V);
+                     lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T);
   LAUNCH_CHECK();
   return 0;
 }

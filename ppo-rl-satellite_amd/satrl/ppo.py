@@ -154,11 +154,12 @@ def ppo_layout(H):
 
 
 class FusedMinibatch:
-    """One PPO minibatch step for actor + critic on shared rows:
-    5 HIP kernels + 3 hipBLASLt GEMMs (torch.bmm over the stacked nets; the
-    K = mb weight-gradient GEMM split S ways into partial slabs).
-    Captured into hipGraphs of ``group`` consecutive minibatches, replayed
-    over [group, mb] blocks of a device permutation."""
+    """One PPO minibatch step for actor + critic on shared rows, 4 launches:
+    satrl_ppo_rowpass (gather, both MLPs forward/backward on f32 MFMA, losses),
+    the dW2 weight-gradient GEMM (hipBLASLt via torch.bmm, split-K S ways),
+    satrl_ppo_reduce and satrl_ppo_adam.  Captured into hipGraphs of
+    ``group`` consecutive minibatches, replayed over [group, mb] blocks of a
+    device permutation."""
 
     def __init__(self, learner, mb, group, use_graph=True, splitk=4):
         self.L = learner
@@ -170,15 +171,11 @@ class FusedMinibatch:
         nwg, nblk = C.c_int64(), C.c_int64()
         check(_lib.lib().satrl_ppo_sizes(H, self.mb, C.byref(nwg), C.byref(nblk)), "satrl_ppo_sizes")
         self.nwg, self.nblk = nwg.value, nblk.value
-        self.nw1 = _lib.lib().satrl_ppo_w1_chunks(self.mb)
         f32 = dict(dtype=torch.float32, device=dev)
         self.H1 = torch.empty(2 * self.mb * H, **f32)
-        self.Z2 = torch.empty(2 * self.mb * H, **f32)       # also dH1
         self.dZ2 = torch.empty(2 * self.mb * H, **f32)
-        self.saug = torch.empty(self.mb * 20, **f32)
-        self.aux = torch.empty(self.mb * 8, **f32)
-        self.partials = torch.empty(self.nwg * (6 * H + 12), **f32)
-        self.p1 = torch.empty(self.nw1 * 2 * H * 20, **f32)
+        self.ptail = torch.empty(self.nwg * (6 * H + 12), **f32)
+        self.pw1 = torch.empty(self.nwg * 2 * H * 20, **f32)
         self.p2 = torch.empty(2 * self.S * H * H, **f32)
         self.nsq = torch.zeros(2 * self.nblk, dtype=torch.float64, device=dev)
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
@@ -192,24 +189,19 @@ class FusedMinibatch:
         S = self.S if mb % self.S == 0 else 1
         lib, sp = _lib.lib(), stream_ptr()
         n = 2 * mb * H
-        H1, Z2, dZ2 = self.H1[:n], self.Z2[:n], self.dZ2[:n]
-        check(lib.satrl_ppo_fwd1(H, mb, ptr(src), ptr(idx), ptr(L.P), ptr(H1), ptr(self.saug), ptr(self.aux), sp),
-              "satrl_ppo_fwd1")
-        H1v, Z2v, dZ2v = H1.view(2, mb, H), Z2.view(2, mb, H), dZ2.view(2, mb, H)
-        torch.bmm(H1v, L.W2v.transpose(1, 2), out=Z2v)                       # fc2 (both nets)
-        check(lib.satrl_ppo_head(H, mb, ptr(Z2), ptr(L.P), ptr(self.aux), float(L.epsilon), float(L.entropy_coef),
-                                 float(L.max_action), ptr(dZ2), ptr(self.partials), None, sp), "satrl_ppo_head")
-        torch.bmm(dZ2v, L.W2v, out=Z2v)                                       # dH1 (reuses Z2)
-        # dW2 split-K S ways: [2S, mb/S, H]^T @ [2S, mb/S, H] -> slabs [2][S][H][H]
+        H1, dZ2 = self.H1[:n], self.dZ2[:n]
+        check(lib.satrl_ppo_rowpass(H, mb, ptr(src), ptr(idx), ptr(L.P), ptr(L.W2T), float(L.epsilon),
+                                    float(L.entropy_coef), float(L.max_action), ptr(H1), ptr(dZ2), ptr(self.ptail),
+                                    ptr(self.pw1), sp), "satrl_ppo_rowpass")
+        # dW2 = dZ2^T @ H1 per net, split-K S ways -> slabs [2][S][H][H]
         p2v = self.p2[:2 * S * H * H].view(2 * S, H, H)
         torch.bmm(dZ2.view(2 * S, mb // S, H).transpose(1, 2), H1.view(2 * S, mb // S, H), out=p2v)
-        check(lib.satrl_ppo_dw1(H, mb, ptr(Z2), ptr(H1), ptr(self.saug), ptr(self.p1), sp), "satrl_ppo_dw1")
         if L.pg is None:
-            check(lib.satrl_ppo_reduce(H, mb, S, 3, ptr(self.p2), ptr(self.p1), ptr(self.partials), ptr(L.G),
+            check(lib.satrl_ppo_reduce(H, mb, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        ptr(self.nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
             import torch.distributed as dist
-            check(lib.satrl_ppo_reduce(H, mb, S, 1, ptr(self.p2), ptr(self.p1), ptr(self.partials), ptr(L.G), None,
+            check(lib.satrl_ppo_reduce(H, mb, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G), None,
                                        None, sp), "satrl_ppo_reduce")
             dist.all_reduce(L.G, group=L.pg)                                  # one bucket, both nets
             L.G.div_(dist.get_world_size(L.pg))
@@ -217,7 +209,7 @@ class FusedMinibatch:
                   "satrl_ppo_reduce")
         check(lib.satrl_ppo_adam(H, mb, ptr(self.nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
                                  float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
-                                 ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), sp), "satrl_ppo_adam")
+                                 ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
 
     def _capture(self, src):
         s = torch.cuda.Stream()
@@ -319,6 +311,7 @@ class PPOLearner:
         self.critic = critic.to(self.device)
         P = self.P
         self.W2v = P[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
+        self.W2T = torch.zeros(2 * H * H, **f32)                 # fc2.weight^T per net (rowpass backprop)
         self.GW2v = self.G[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
         W1 = P[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
         self.GW1v = self.G[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
@@ -373,6 +366,12 @@ class PPOLearner:
                 "critic.fc3.bias": buf[o["b3c"]:o["b3c"] + 1]}
 
     # -- update -----------------------------------------------------------------
+    def sync_w2t(self):
+        """Refresh fc2.weight^T from P (Adam keeps it current during an update;
+        this covers loads / external writes between updates)."""
+        H = self.H
+        self.W2T.view(2, H, H).copy_(self.W2v.transpose(1, 2))
+
     def stepper(self, mb):
         if mb not in self._steppers:
             self._steppers[mb] = FusedMinibatch(self, mb, self.graph_group, use_graph=self.use_graph)
@@ -398,6 +397,7 @@ class PPOLearner:
         """K epochs of minibatch steps over the packed table src [B, 32]
         (adv already normalised), then lr decay (ppo_continuous.py:212-242)."""
         B = src.shape[0]
+        self.sync_w2t()
         st = self.stepper(min(self.mini_batch_size, B))
         for ep in range(self.K_epochs):
             perm = perms[ep] if perms is not None else torch.randperm(B, device=self.device, generator=generator)

@@ -19,7 +19,7 @@ def test_headers_declare_expected_entry_points():
     assert {"satenv_create", "satenv_reset", "satenv_step", "satenv_step_autoreset", "satenv_destroy",
             "satenv_get_state", "satenv_set_state", "satenv_last_error"} <= env
     assert {"satrl_gae", "satrl_gaussian_sample", "satrl_moments"} <= _declared("satrl_rollout.h")
-    assert {"satrl_ppo_fwd1", "satrl_ppo_head", "satrl_ppo_reduce", "satrl_ppo_adam"} <= _declared("satrl_ppo.h")
+    assert {"satrl_ppo_rowpass", "satrl_ppo_reduce", "satrl_ppo_adam", "satrl_ppo_layout"} <= _declared("satrl_ppo.h")
 
 
 def test_library_exports_every_declared_symbol():

@@ -142,7 +142,7 @@ def test_update_matches_reference():
 
 @pytest.mark.parametrize("H", [64, 256])
 def test_fused_step_vs_torch_autograd(H):
-    """satrl_ppo_* kernels + hipBLASLt GEMMs vs plain torch fp32 autograd +
+    """satrl_ppo_rowpass (f32 MFMA) + hipBLASLt dW2 + reduce + Adam vs plain torch fp32 autograd +
     clip_grad_norm_ + torch.optim.Adam on the same minibatch."""
     from satrl.ppo import PPOLearner
     from torch_reference import reference_step
@@ -162,6 +162,7 @@ def test_fused_step_vs_torch_autograd(H):
     src[:, 25] = torch.randn(B, device="cuda", generator=g) * 5
     idx = torch.randperm(B, device="cuda", generator=g)[:mb]
     grads, params = reference_step(L.actor, L.critic, src[idx], lr=args.lr_a)
+    L.sync_w2t()
     st = L.stepper(mb)
     st.step(src, idx)
     torch.cuda.synchronize()
