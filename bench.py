@@ -40,33 +40,30 @@ def parse():
     ap.add_argument("--d-capture", type=float, default=15000.0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--env-kernel-iters", type=int, default=200)
+    ap.add_argument("--kernel-iters", type=int, default=200)
     return ap.parse_args()
 
 
 def cpu_baseline(seconds):
     """Oracle (oracle/satenv_oracle.c, the CPU restatement) on host cores:
-    a bounded sample of the same env workload (Flag 0, reset state,
-    uniform f32 actions), OpenMP over envs."""
+    a bounded sample of the same env workload -- 16384 envs stepped from the
+    reference reset state with autoreset (Flag 0, uniform f32 actions), in
+    chunks of 256 steps until about `seconds` of CPU time, OpenMP over envs."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
-    n = 16384
+    n, chunk = 16384, 256
     rng = np.random.default_rng(0)
-    # calibrate steps for ~`seconds` of work
-    steps = 4
-    pa = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
-    ea = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
-    t0 = time.perf_counter()
-    O.rollout(n, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=threads)
-    dt = time.perf_counter() - t0
-    steps = int(max(4, min(4096, steps * seconds / max(dt, 1e-3))))
-    pa = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
-    ea = rng.uniform(-1.6, 1.6, (steps, n, 3)).astype(np.float32)
-    t0 = time.perf_counter()
-    O.rollout(n, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=threads)
-    dt = time.perf_counter() - t0
+    pa = rng.uniform(-1.6, 1.6, (chunk, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (chunk, n, 3)).astype(np.float32)
+    ro = O.Rollout(n, d_capture=15000.0, max_episode_steps=1000)
+    steps, dt = 0, 0.0
+    while dt < seconds and steps < 64 * chunk:
+        t0 = time.perf_counter()
+        ro.run(pa, ea, nthreads=threads)
+        dt += time.perf_counter() - t0
+        steps += chunk
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -76,8 +73,9 @@ def cpu_baseline(seconds):
     except OSError:
         pass
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle C restatement, {n} envs x {steps} steps from reset (Flag 0, U(-1.6,1.6) f32 actions, "
-                      f"d_capture 15000), OpenMP {threads} threads on '{model}' (os.cpu_count()={os.cpu_count()})",
+            "sample": f"oracle C restatement, {n} envs x {steps} consecutive steps from reset with autoreset "
+                      f"(Flag 0, U(-1.6,1.6) f32 actions, d_capture 15000, max_episode_steps 1000), OpenMP {threads} "
+                      f"threads on '{model}' (os.cpu_count()={os.cpu_count()})",
             "seconds": dt}
 
 
@@ -128,7 +126,34 @@ def main():
     env_steps = n_total * a.horizon * a.steps
     value = env_steps / elapsed
 
-    # ---- env-kernel roofline: HIP events around eager launches on the kernel's stream
+    # ---- roofline of the dominant kernel (satrl_ppo_rowpass, ~60% of the update):
+    # HIP events around back-to-back launches on the stream it is launched on
+    # (torch's current stream, see satrl._lib.stream_ptr), same inputs as the update.
+    L = tr.learner
+    st = L.stepper(a.minibatch)
+    src = tr.buf.packed
+    g = torch.Generator(device="cuda").manual_seed(1)
+    idx = torch.randperm(src.shape[0], device="cuda", generator=g)[:a.minibatch].contiguous()
+    for _ in range(10):
+        st.rowpass(src, idx)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.kernel_iters):
+        st.rowpass(src, idx)
+    e1.record()
+    torch.cuda.synchronize()
+    rowpass_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+    rowpass_flop = st.rowpass_flops(a.hidden, a.minibatch)
+    rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
+    traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", "r1_rowpass_pmc.json")
+    if os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            pmc = json.load(f)
+        if pmc.get("hidden") == a.hidden and pmc.get("minibatch") == a.minibatch:
+            traffic = pmc["hbm_bytes_per_launch"]
+
+    # ---- env kernel (FP64 step, autoreset): HIP events around eager launches on its stream
     env = tr.env
     pa = tr.buf.act[0].clone()
     ea = torch.empty_like(pa).uniform_(-1.6, 1.6)
@@ -137,14 +162,13 @@ def main():
     dn = torch.empty(a.num_envs, dtype=torch.uint8, device="cuda")
     for _ in range(10):
         env.step_autoreset(pa, ea, obs, rew, dn)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(a.env_kernel_iters):
+    for _ in range(a.kernel_iters):
         env.step_autoreset(pa, ea, obs, rew, dn)
     e1.record()
     torch.cuda.synchronize()
-    env_us = e0.elapsed_time(e1) * 1e3 / a.env_kernel_iters
-    achieved = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
+    env_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+    env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
 
     rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
     update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
@@ -172,11 +196,16 @@ def main():
             "rollout_ms": rollout_ms, "gae_ms": gae_ms, "update_ms": update_ms,
             "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
             "episodes_finished_total": float(stats[0]),
-            "roofline": {"kernel": "satenv step_kernel<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "avg_launch_us": env_us,
-                         "bytes_per_env_step": ENV_BYTES_PER_STEP,
-                         "note": "algorithmic bytes; the kernel is FP64-VALU/transcendental bound (DESIGN.md)"},
+            "roofline": {"kernel": "satrl_ppo_rowpass<256,16> (hand-written HIP, f32 MFMA 16x16x4)", "bound": "mfma",
+                         "achieved": rowpass_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": rowpass_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
+                         "avg_launch_us": rowpass_us, "flop_per_launch": rowpass_flop,
+                         "traffic_source": "profiles/r1_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)",
+                         "note": "f32 MFMA; every CU re-reads both fc2 weights from L2 per 16 rows (DESIGN.md)"},
+            "roofline_env": {"kernel": "satenv step_kernel<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
+                             "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
+                             "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
+                             "note": "algorithmic bytes; the kernel is FP64 latency bound (DESIGN.md)"},
             "roofline_update": {"bound": "mfma", "achieved": upd_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                                 "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
                                 "flop_per_transition_epoch": flop_per_transition_epoch},

@@ -173,6 +173,34 @@ def rollout(n_envs, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nt
     return rew, done
 
 
+class Rollout:
+    """Like rollout() but the envs persist across run() calls (autoreset at
+    done), so a long CPU sample can be fed in bounded action chunks."""
+
+    def __init__(self, n_envs, d_capture=15000.0, max_episode_steps=1000, flag=0):
+        self.n = int(n_envs)
+        self.p = params(d_capture, max_episode_steps)
+        self.envs = (OrcEnv * self.n)()
+        for i in range(self.n):
+            lib().orc_env_init(C.byref(self.envs[i]))
+            lib().orc_reset(C.byref(self.envs[i]), flag, None)
+        self.cnt = np.zeros(self.n, dtype=np.int32)
+
+    def run(self, pa, ea, nthreads=1):
+        steps = pa.shape[0]
+        rew = np.zeros((steps, self.n))
+        done = np.zeros((steps, self.n), dtype=np.int32)
+        pa = np.ascontiguousarray(pa, dtype=np.float32)
+        ea = np.ascontiguousarray(ea, dtype=np.float32)
+        rc = lib().orc_rollout(C.byref(self.p), self.envs, self.n, steps, pa.ctypes.data_as(C.POINTER(C.c_float)),
+                               ea.ctypes.data_as(C.POINTER(C.c_float)),
+                               self.cnt.ctypes.data_as(C.POINTER(C.c_int32)), _dp(rew),
+                               done.ctypes.data_as(C.POINTER(C.c_int32)), int(nthreads))
+        if rc != 0:
+            raise RuntimeError("oracle rollout error")
+        return rew, done
+
+
 # --------------------------------------------------------------------------
 # Learning-side restatements (ppo_continuous.py)
 # --------------------------------------------------------------------------

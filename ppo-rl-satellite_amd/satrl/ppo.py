@@ -182,17 +182,35 @@ class FusedMinibatch:
         self.graph = None
         self._src_ptr = None
 
+    def rowpass(self, src, idx, mb=None):
+        """satrl_ppo_rowpass alone (a pure function of src, idx and the
+        parameters: bench.py times it on its own for the roofline)."""
+        L = self.L
+        H = L.H
+        mb = self.mb if mb is None else int(mb)
+        n = 2 * mb * H
+        H1, dZ2 = self.H1[:n], self.dZ2[:n]
+        check(_lib.lib().satrl_ppo_rowpass(H, mb, ptr(src), ptr(idx), ptr(L.P), ptr(L.W2T), float(L.epsilon),
+                                           float(L.entropy_coef), float(L.max_action), ptr(H1), ptr(dZ2),
+                                           ptr(self.ptail), ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass")
+        return H1, dZ2
+
+    @staticmethod
+    def rowpass_flops(H, mb):
+        """Algorithmic FLOPs of one rowpass launch (DESIGN.md "Roofline"):
+        per row and net fc1 forward + [dW1|db1] (2*18*H + H each), fc2 forward
+        and dH1 (2*H*H each); output layers forward/backward (actor 3 outputs
+        x 3 products, critic 1 x 3)."""
+        per_row = 2 * (2 * (2 * 18 * H + H) + 2 * (2 * H * H)) + 2 * 3 * 3 * H + 2 * 1 * 3 * H
+        return per_row * mb
+
     def step(self, src, idx, mb=None):
         L = self.L
         H = L.H
         mb = self.mb if mb is None else int(mb)
         S = self.S if mb % self.S == 0 else 1
         lib, sp = _lib.lib(), stream_ptr()
-        n = 2 * mb * H
-        H1, dZ2 = self.H1[:n], self.dZ2[:n]
-        check(lib.satrl_ppo_rowpass(H, mb, ptr(src), ptr(idx), ptr(L.P), ptr(L.W2T), float(L.epsilon),
-                                    float(L.entropy_coef), float(L.max_action), ptr(H1), ptr(dZ2), ptr(self.ptail),
-                                    ptr(self.pw1), sp), "satrl_ppo_rowpass")
+        H1, dZ2 = self.rowpass(src, idx, mb)
         # dW2 = dZ2^T @ H1 per net, split-K S ways -> slabs [2][S][H][H]
         p2v = self.p2[:2 * S * H * H].view(2 * S, H, H)
         torch.bmm(dZ2.view(2 * S, mb // S, H).transpose(1, 2), H1.view(2 * S, mb // S, H), out=p2v)

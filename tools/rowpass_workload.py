@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Workload for the PMC passes of tools/profile_round.sh: satrl_ppo_rowpass
+launched back to back at the bench configuration (hidden 256, minibatch
+4096 rows gathered by a random permutation from a packed buffer of
+16384 x 2048 transitions, as in one PPO epoch of bench.py)."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
+
+from satrl.ppo import PPOLearner  # noqa: E402
+from satrl.trainer import args_param  # noqa: E402
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    H, mb, rows = 256, 4096, 16384 * 2048
+    a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=rows, chkpt_dir="/tmp")
+    L = PPOLearner(a, "pursuer", use_graph=False)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    src = torch.randn((rows, 32), device="cuda", generator=g)
+    perm = torch.randperm(rows, device="cuda", generator=g)
+    st = L.stepper(mb)
+    for k in range(iters):
+        st.rowpass(src, perm[k * mb:(k + 1) * mb])
+    torch.cuda.synchronize()
+    print("ok")
+
+
+if __name__ == "__main__":
+    main()

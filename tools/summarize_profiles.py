@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Turns rocprofv3 CSV output (tools/profile_round.sh) into the committed
+summaries under profiles/: the kernel-stats table of the bench command and
+the per-launch HBM traffic of satrl_ppo_rowpass from the FETCH_SIZE /
+WRITE_SIZE passes (MI355X_MICROARCH.md "HBM": FETCH_SIZE reports half the
+bytes of 16-B-per-lane reads on gfx950 -> x2; WRITE_SIZE exact; both in KB)."""
+import csv
+import json
+import os
+import sys
+
+
+def kernel_stats(path, out):
+    rows = list(csv.DictReader(open(path)))
+    with open(out, "w") as f:
+        f.write("name,calls,total_ns,avg_ns,min_ns,max_ns,percent\n")
+        for r in rows:
+            name = r["Name"].replace(",", ";")
+            f.write(f'"{name}",{r["Calls"]},{r["TotalDurationNs"]},{r["AverageNs"]},{r["MinNs"]},{r["MaxNs"]},'
+                    f'{r["Percentage"]}\n')
+    return rows
+
+
+def pmc_per_dispatch(path, kernel_sub, counter):
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    vals = sorted(per.values())
+    return vals[len(vals) // 2] if vals else None, len(vals)
+
+
+def main():
+    d = sys.argv[1]          # gpurun_out/<run>
+    tag = sys.argv[2]        # e.g. r1
+    prof = sys.argv[3] if len(sys.argv) > 3 else os.path.join(d, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    ks = os.path.join(d, "bench", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        kernel_stats(ks, os.path.join(prof, f"{tag}_bench_kernel_stats.csv"))
+    fetch = os.path.join(d, "pmc_fetch", "run_counter_collection.csv")
+    write = os.path.join(d, "pmc_write", "run_counter_collection.csv")
+    if os.path.exists(fetch) and os.path.exists(write):
+        f_kb, nf = pmc_per_dispatch(fetch, "rowpass_kernel", "FETCH_SIZE")
+        w_kb, nw = pmc_per_dispatch(write, "rowpass_kernel", "WRITE_SIZE")
+        res = {"kernel": "rowpass_kernel<256, 16>", "hidden": 256, "minibatch": 4096,
+               "dispatches": [nf, nw], "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
+               "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
+               "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
+               "workload": "tools/rowpass_workload.py"}
+        with open(os.path.join(prof, f"{tag}_rowpass_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
