@@ -52,3 +52,27 @@ def test_product_has_no_cpu_fallback():
         pytest.skip("GPU present")
     with pytest.raises(Exception):
         E.VecSatellites(4)
+
+
+def test_reference_module_name_shims():
+    """`from environment import satellites` etc. (CPPO_main.py:5-7) resolve to the engine."""
+    import importlib
+    import sys
+    from conftest import PKG_DIR
+    sys.path.insert(0, str(PKG_DIR))
+    try:
+        env = importlib.import_module("environment")
+        ppo = importlib.import_module("ppo_continuous")
+        rb = importlib.import_module("replaybuffer")
+        main = importlib.import_module("CPPO_main")
+    finally:
+        sys.path.remove(str(PKG_DIR))
+    import satrl.buffer
+    import satrl.env
+    import satrl.ppo
+    import satrl.trainer
+    assert env.satellites is satrl.env.satellites
+    assert ppo.PPO_continuous is satrl.ppo.PPO_continuous
+    assert rb.ReplayBuffer is satrl.buffer.ReplayBuffer
+    assert main.args_param is satrl.trainer.args_param
+    assert main.train_pursuer_network is satrl.trainer.train_pursuer_network
