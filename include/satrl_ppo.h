@@ -39,7 +39,7 @@ enum { SATRL_PPO_OFF_W2 = 0, SATRL_PPO_OFF_W1, SATRL_PPO_OFF_B2, SATRL_PPO_OFF_W
 
 /* host helper: element offsets of the flat layout for hidden width H (64, 128 or 256) */
 int satrl_ppo_layout(int H, int64_t* offsets /* [SATRL_PPO_NOFF] */);
-/* number of head workgroups (= partial slabs) and F4 blocks for a minibatch of mb rows */
+/* number of partial slabs (32-row blocks) and of norm blocks for a minibatch of mb rows */
 int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
 
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
@@ -59,13 +59,14 @@ int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const 
                    float* P, float* M, float* V, float* W2T /* nullable: also write fc2.weight^T */,
                    void* stream);
 
-/* The row-parallel part of one minibatch step in ONE launch (16 rows per
- * workgroup): gather + fc1 + tanh, fc2 (f32 MFMA), output layers, both
- * losses and their gradients, backprop through fc2 (f32 MFMA on W2T =
- * fc2.weight^T per net, [2][H][H]) and tanh(fc1).  Writes H1 and dZ2
- * [2][mb][H] (inputs of the dW2 GEMM), the tail partial slabs
- * [ceil(mb/16)][6H+12] and the [dW1 | db1] partial slabs
- * [ceil(mb/16)][2][H][20].                                                */
+/* The row-parallel part of one minibatch step in ONE launch (a workgroup
+ * per net and 32-row block): gather + fc1 + tanh, fc2 (f32 MFMA), output
+ * layer, the net's loss and gradients, backprop through fc2 (f32 MFMA on
+ * W2T = fc2.weight^T per net, [2][H][H]) and tanh(fc1).  Rows are
+ * src[idx[r]] (idx nullable: rows 0..mb-1 of src, contiguous).  Writes H1
+ * and dZ2 [2][mb][H] (inputs of the dW2 GEMM), the tail partial slabs
+ * [n_head_wg][6H+12] and the [dW1 | db1] partial slabs [n_head_wg][2][H][20]
+ * (n_head_wg = ceil(mb/32), satrl_ppo_sizes).                             */
 int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const float* P, const float* W2T,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream);

@@ -20,7 +20,23 @@ namespace {
 
 thread_local std::string g_err;
 
-constexpr int kRows = 16;          // minibatch rows per rowpass workgroup
+#ifdef SATRL_PHASE_PROBE
+// development-only phase stamps (tools/_probe/phase_probe.py), never in the
+// shipped build: [workgroup][stamp][wave 0 | wave NW/2][s_memrealtime, s_memtime]
+__device__ unsigned long long g_probe[4096][8][2][2];
+#define PHASE_PROBE(k)                                                        \
+  do {                                                                        \
+    if (threadIdx.x == 0 || threadIdx.x == blockDim.x / 2) {                  \
+      const int pw_ = threadIdx.x == 0 ? 0 : 1;                               \
+      g_probe[blockIdx.x][k][pw_][0] = wall_clock64();                        \
+      g_probe[blockIdx.x][k][pw_][1] = clock64();                             \
+    }                                                                         \
+  } while (0)
+#else
+#define PHASE_PROBE(k) do {} while (0)
+#endif
+
+constexpr int kRows = 32;          // minibatch rows per rowpass workgroup (and per partial slab)
 
 constexpr float kLogSqrt2Pi = 0.9189385332046727f;   // math.log(math.sqrt(2*math.pi))
 
@@ -53,18 +69,25 @@ __device__ __forceinline__ int net_of(const Layout& L, int64_t e, int H) {
 
 // ---------------------------------------------------------------------------
 // rowpass: the whole row-parallel part of a minibatch step in one launch.
-// One workgroup = 16 minibatch rows, 4 waves; wave w owns net w>>1 and the
-// column half (w&1) of the hidden layer: T = H/32 MFMA tiles of 16x16.
+// The actor and critic losses are independent given (adv, v_target), so a
+// workgroup owns ONE net (blockIdx & 1; with round-robin dispatch the actor
+// lands on the even XCDs, the critic on the odd ones) and 32 minibatch rows
+// (blockIdx >> 1).  Its NW waves split the hidden columns: wave w owns
+// CT = H/16/NW tiles of 16 columns for both 16-row tiles.  Every CU thus
+// streams one net's fc2 weights per phase (256 KB at H=256) for 32 rows:
+// the two MFMA phases are L2->CU ingest bound.
 //   A  gather rows -> S (LDS); Z1 = [S|1] W1aug^T       f32 MFMA 16x16x4
 //   B  Z2 = tanh(Z1) W2^T                               f32 MFMA, W2 from L2
-//   C  tanh(fc2), output layers, both losses, dZ2 -> LDS/HBM, tail partials
+//   C  tanh(fc2), output layer(s), the net's loss, dZ2 -> LDS/HBM, tail partials
 //   D  dH1 = dZ2 W2 (rows of W2T = fc2.weight^T)        f32 MFMA
 //   E  dZ1 = dH1 (1 - H1^2); [dW1|db1] = dZ1^T [S|1]    f32 MFMA, dZ1's
 //      accumulator layout is already the A operand
-// Accumulator layout of a 16x16x4 tile: acc[t][j] = D[row 4*lg + j][col li].
-// Inside a 32-wide k chunk lane group g takes k = 32c + 8g + kk (kk < 8), so
-// every B fetch is a 32-B run of a 128-B line and A comes as 2 ds_read_b128
-// from rows padded by 16 B.
+// Accumulator layout of a 16x16x4 tile: acc[rt][ct][j] = D[row 16rt + 4lg + j]
+// [col n0 + 16ct + li].  Inside a 32-wide k chunk lane group g takes
+// k = 32c + 8g + kk (kk < 8): every B fetch is a 32-B run of a 128-B line and
+// A comes as 2 ds_read_b128 per row tile from rows padded by 16 B.
+// Partial slabs are per 32-row block: the actor and critic workgroups of a
+// block write disjoint parts of the same slab.
 // ---------------------------------------------------------------------------
 using f4 = __attribute__((ext_vector_type(4))) float;
 
@@ -72,55 +95,77 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// acc[t] (t < T) += A[16][K] (LDS, row stride LDA) x B^T with B[n][k] row-major
-// (ld LDB) for columns n0 + 16t; tiles are processed 4 at a time, 32-k chunks,
-// next chunk's B prefetched into registers during the current chunk's MFMAs.
-template <int K, int LDA, int LDB, int T>
-__device__ __forceinline__ void mfma_rows16(const float* __restrict__ A, const float* __restrict__ B, int n0,
-                                            f4 (&acc)[T]) {
-  constexpr int TG = T < 4 ? T : 4;
-  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+// sum over the 16 lanes of a DPP row (lanes 16k .. 16k+15), result in every
+// lane of the row: xor-1 and xor-2 quad permutes, then half-row and row
+// mirrors -- VALU DPP, no LDS traffic (ds_bpermute chains were the slowest
+// part of the output-layer dot products).  Fixed order, so deterministic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror
+  return v;
+}
+
+template <int CT>
+__device__ __forceinline__ void b_chunk(const float* __restrict__ bp, int LDB, float4 (&b)[CT][2]) {
 #pragma unroll
-  for (int t0 = 0; t0 < T; t0 += TG) {
-    float4 b0[TG], b1[TG], n0v[TG], n1v[TG];
+  for (int t = 0; t < CT; ++t) {
+    b[t][0] = *reinterpret_cast<const float4*>(bp + 16 * t * LDB);
+    b[t][1] = *reinterpret_cast<const float4*>(bp + 16 * t * LDB + 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);   // keep the prefetch where it is issued
+}
+
+template <int LDA, int RT, int CT>
+__device__ __forceinline__ void mfma_chunk(const float* __restrict__ ap, const float4 (&b)[CT][2],
+                                           f4 (&acc)[RT][CT]) {
+  float4 a[RT][2];
 #pragma unroll
-    for (int t = 0; t < TG; ++t) {
-      const float* bp = B + (int64_t)(n0 + 16 * (t0 + t) + i) * LDB + 8 * g;
-      b0[t] = *reinterpret_cast<const float4*>(bp);
-      b1[t] = *reinterpret_cast<const float4*>(bp + 4);
-    }
-#pragma unroll 1
-    for (int c = 0; c < K / 32; ++c) {
-      if (c + 1 < K / 32) {
+  for (int rt = 0; rt < RT; ++rt) {
+    a[rt][0] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA);
+    a[rt][1] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA + 4);
+  }
 #pragma unroll
-        for (int t = 0; t < TG; ++t) {
-          const float* bp = B + (int64_t)(n0 + 16 * (t0 + t) + i) * LDB + 32 * (c + 1) + 8 * g;
-          n0v[t] = *reinterpret_cast<const float4*>(bp);
-          n1v[t] = *reinterpret_cast<const float4*>(bp + 4);
-        }
-      }
-      const float4 a0 = *reinterpret_cast<const float4*>(A + i * LDA + 32 * c + 8 * g);
-      const float4 a1 = *reinterpret_cast<const float4*>(A + i * LDA + 32 * c + 8 * g + 4);
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.x, b0[t].x, acc[t0 + t]);
+    for (int e = 0; e < 4; ++e) {
 #pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.y, b0[t].y, acc[t0 + t]);
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.z, b0[t].z, acc[t0 + t]);
-#pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a0.w, b0[t].w, acc[t0 + t]);
-#pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.x, b1[t].x, acc[t0 + t]);
-#pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.y, b1[t].y, acc[t0 + t]);
-#pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.z, b1[t].z, acc[t0 + t]);
-#pragma unroll
-      for (int t = 0; t < TG; ++t) acc[t0 + t] = mfma4(a1.w, b1[t].w, acc[t0 + t]);
-#pragma unroll
-      for (int t = 0; t < TG; ++t) { b0[t] = n0v[t]; b1[t] = n1v[t]; }
+        for (int t = 0; t < CT; ++t) acc[rt][t] = mfma4(a[rt][h][e], b[t][h][e], acc[rt][t]);
     }
   }
+}
+
+// acc[rt][t] += A[16rt.. +16][K] (LDS, row stride LDA) x B^T with B[n][k]
+// row-major (ld LDB) for columns n0 + 16t, in 32-wide k chunks.  Chunk pairs
+// with two register buffers in a rolled loop (prefetch distance one chunk);
+// loads unconditional and the last pair peeled, so every vmcnt wait is exact.
+template <int K, int LDA, int LDB, int RT, int CT>
+__device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
+                                          f4 (&acc)[RT][CT]) {
+  constexpr int NC = K / 32;
+  static_assert(NC % 2 == 0, "chunk pairs");
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const float* ap = A + i * LDA + 8 * g;
+  const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
+  float4 x[CT][2], y[CT][2];
+  b_chunk<CT>(bp, LDB, x);
+#pragma unroll 1
+  for (int c = 0; c < NC - 2; c += 2) {
+    b_chunk<CT>(bp + 32 * (c + 1), LDB, y);
+    mfma_chunk<LDA, RT, CT>(ap + 32 * c, x, acc);
+    b_chunk<CT>(bp + 32 * (c + 2), LDB, x);
+    mfma_chunk<LDA, RT, CT>(ap + 32 * (c + 1), y, acc);
+  }
+  b_chunk<CT>(bp + 32 * (NC - 1), LDB, y);
+  mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 2), x, acc);
+  mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 1), y, acc);
 }
 
 template <int H, int NW>
@@ -130,77 +175,35 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1) {
-  // NW waves: the first NW/2 own the actor, the rest the critic; each wave a
-  // slice of H/(NW/2) hidden columns = T tiles of 16
-  constexpr int R = 16, LDA = H + 4, HW = NW / 2, T = H / 16 / HW, LDS_S = 36, NT = NW * 64;
-  static_assert(T >= 1 && H % (16 * HW) == 0, "tile split");
+  constexpr int R = kRows, RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
+  static_assert(CT >= 1 && H % (16 * NW) == 0, "tile split");
   const Layout L = layout(H);
-  __shared__ __attribute__((aligned(16))) float h1s[2][R][LDA];     // tanh(fc1)
-  __shared__ __attribute__((aligned(16))) float dzs[2][R][LDA];     // dZ2
-  __shared__ __attribute__((aligned(16))) float S[R][LDS_S];        // [s(18) | 1 | 0...] per row
+  __shared__ __attribute__((aligned(16))) float h1s[R][LDA];     // tanh(fc1)
+  __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
+  __shared__ __attribute__((aligned(16))) float S[R][LDS_S];     // [s(18) | 1 | 0...] per row
   __shared__ float ax[R][8];
   __shared__ float osum[NW][R][3];
   __shared__ float dz3s[R][4];
   __shared__ float lsp[R][4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
-  const int net = w / HW, n0 = (w % HW) * (H / HW);
-  const int r0 = blockIdx.x * R;
+  const int net = blockIdx.x & 1, rb = blockIdx.x >> 1, n0 = w * (H / NW);
+  const int r0 = rb * R;
+  PHASE_PROBE(0);
 
   // ---- A: gather, fc1 on MFMA ------------------------------------------------
   for (int q = tid; q < R * 26; q += NT) {
     const int r = q / 26, c = q % 26, row = r0 + r;
-    const float v = row < mb ? src[idx[row] * 32 + c] : 0.0f;
+    const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
     if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;             // s | a, logp_old, adv, v_target
   }
   for (int q = tid; q < R * (LDS_S - 18); q += NT) {
     const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
     S[r][c] = (c == 18 && r0 + r < mb) ? 1.0f : 0.0f;             // bias column of W1aug, zero pad
   }
-  __syncthreads();
-  f4 acc[T];
-  f4 h1[T];
+  // fc2 bias and output-layer weights of this wave's columns (used in C)
+  float w3[CT][3], b2v[CT];
 #pragma unroll
-  for (int t = 0; t < T; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  {
-    // W1aug rows [n][20] (k 0..19) padded to 32 with zeros: lane group g takes k = 8g .. 8g+7
-    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
-    const float4 a0 = *reinterpret_cast<const float4*>(&S[li][8 * lg]);
-    const float4 a1 = *reinterpret_cast<const float4*>(&S[li][8 * lg + 4]);
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
-      float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lg < 2) { b0 = *reinterpret_cast<const float4*>(bp + 8 * lg); b1 = *reinterpret_cast<const float4*>(bp + 8 * lg + 4); }
-      else if (lg == 2) b0 = *reinterpret_cast<const float4*>(bp + 16);
-      acc[t] = mfma4(a0.x, b0.x, acc[t]); acc[t] = mfma4(a0.y, b0.y, acc[t]);
-      acc[t] = mfma4(a0.z, b0.z, acc[t]); acc[t] = mfma4(a0.w, b0.w, acc[t]);
-      acc[t] = mfma4(a1.x, b1.x, acc[t]); acc[t] = mfma4(a1.y, b1.y, acc[t]);
-      acc[t] = mfma4(a1.z, b1.z, acc[t]); acc[t] = mfma4(a1.w, b1.w, acc[t]);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int n = n0 + 16 * t + li;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = 4 * lg + j;
-      const float h = tanhf(acc[t][j]);                              // fc1 + tanh
-      h1[t][j] = h;
-      h1s[net][r][n] = h;
-      if (r0 + r < mb) H1g[((int64_t)net * mb + r0 + r) * H + n] = h;
-    }
-    acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  }
-  __syncthreads();
-
-  // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  mfma_rows16<H, LDA, H, T>(&h1s[net][0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
-
-  // ---- C: fc2 tanh, output layers, losses, dZ2 --------------------------------
-  float w3[T][3];
-  float b2v[T];
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < CT; ++t) {
     const int n = n0 + 16 * t + li;
     b2v[t] = P[L.b2 + net * H + n];
     if (net == 0) {
@@ -209,114 +212,164 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       w3[t][0] = P[L.W3c + n]; w3[t][1] = 0.0f; w3[t][2] = 0.0f;
     }
   }
-  float p[3][4];
+  __syncthreads();
+  f4 acc[RT][CT];
+  float h1[RT][CT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
+  {
+    // W1aug rows [n][20] (k 0..19) padded to 32 with zeros: lane group g takes k = 8g .. 8g+7
+    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
+    float4 b[CT][2];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
+      b[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      b[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lg < 2) { b[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg); b[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4); }
+      else if (lg == 2) b[t][0] = *reinterpret_cast<const float4*>(bp + 16);
+    }
+    mfma_chunk<LDS_S, RT, CT>(&S[li][8 * lg], b, acc);
+  }
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int n = n0 + 16 * t + li;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * rt + 4 * lg + j;
+        const float h = tanhf(acc[rt][t][j]);                      // fc1 + tanh
+        h1[rt][t][j] = h;
+        h1s[r][n] = h;
+        if (r0 + r < mb) H1g[((int64_t)net * mb + r0 + r) * H + n] = h;
+      }
+      acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  __syncthreads();
+  PHASE_PROBE(1);
+
+  // ---- B: Z2 = H1 W2^T -------------------------------------------------------
+  mfma_rows<H, LDA, H, RT, CT>(&h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  PHASE_PROBE(2);
+
+  // ---- C: fc2 tanh, output layer(s), loss, dZ2 --------------------------------
+  const int NQ = net == 0 ? 3 : 1;                                  // output columns of this net
+  float p[3][RT][4];
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) p[q][j] = 0.0f;
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-  for (int t = 0; t < T; ++t)
+      for (int j = 0; j < 4; ++j) p[q][rt][j] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float h = tanhf(acc[t][j] + b2v[t]);                    // fc2 + tanh
-      acc[t][j] = h;
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) p[q][j] = fmaf(h, w3[t][q], p[q][j]);
-    }
+    for (int t = 0; t < CT; ++t)
 #pragma unroll
-  for (int q = 0; q < 3; ++q)
+      for (int j = 0; j < 4; ++j) {
+        const float h = tanhf(acc[rt][t][j] + b2v[t]);              // fc2 + tanh
+        acc[rt][t][j] = h;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = p[q][j];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      p[q][j] = v;
-    }
-  if (li == 0) {
+        for (int q = 0; q < 3; ++q) p[q][rt][j] = fmaf(h, w3[t][q], p[q][rt][j]);
+      }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+  for (int q = 0; q < 3; ++q) {
+    if (q >= NQ) break;                                            // uniform per workgroup
 #pragma unroll
-      for (int q = 0; q < 3; ++q) osum[w][4 * lg + j][q] = p[q][j];
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = row16_sum(p[q][rt][j]);
+        if (li == 0) osum[w][16 * rt + 4 * lg + j][q] = v;
+      }
   }
   __syncthreads();
+  PHASE_PROBE(3);
   if (tid < R) {
     const int r = tid, row = r0 + r;
     float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
     if (row < mb) {
       const float inv = 1.0f / (float)mb;
-      float th[3], mu[3], dv[3], var[3], logp[3];
+      if (net == 0) {                                              // actor: clipped surrogate + entropy
+        float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        float od = 0.0f;
+        for (int d = 0; d < 3; ++d) {
+          float od = 0.0f;
 #pragma unroll
-        for (int k = 0; k < HW; ++k) od += osum[k][r][d];
-        th[d] = tanhf(od + P[L.b3a + d]);
-        mu[d] = max_action * th[d];                                  // 1.6 * tanh(mean_layer)
-        const float sd = expf(P[L.ls + d]);
-        var[d] = sd * sd;
-        dv[d] = ax[r][d] - mu[d];
-        logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - logf(sd)) - kLogSqrt2Pi;
+          for (int k = 0; k < NW; ++k) od += osum[k][r][d];
+          th[d] = tanhf(od + P[L.b3a + d]);
+          mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
+          const float sd = expf(P[L.ls + d]);
+          var[d] = sd * sd;
+          dv[d] = ax[r][d] - mu[d];
+          logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - logf(sd)) - kLogSqrt2Pi;
+        }
+        const float lsum = (logp[0] + logp[1]) + logp[2];
+        const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
+        const float ratio = expf(lsum - lold);
+        const float adv = ax[r][6];
+        const float s1 = ratio * adv;
+        const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
+        const float s2 = cr * adv;
+        const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);   // torch.min tie split
+        const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+        const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
+        const float dmin = -inv;
+        const float dratio = dmin * g1 * adv + dmin * g2 * adv * inside;
+        const float dlsum = dratio * ratio;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const float dmu = dlsum * (dv[d] / var[d]);
+          dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
+          dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
+        }
+      } else {                                                     // critic: MSE
+        float oc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) oc += osum[k][r][0];
+        const float vc = oc + P[L.b3c];
+        dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
-      const float lsum = (logp[0] + logp[1]) + logp[2];
-      const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
-      const float ratio = expf(lsum - lold);
-      const float adv = ax[r][6];
-      const float s1 = ratio * adv;
-      const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
-      const float s2 = cr * adv;
-      const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);   // torch.min tie split
-      const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-      const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
-      const float dmin = -inv;
-      const float dratio = dmin * g1 * adv + dmin * g2 * adv * inside;
-      const float dlsum = dratio * ratio;
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const float dmu = dlsum * (dv[d] / var[d]);
-        dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
-        dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
-      }
-      float oc = 0.0f;
-#pragma unroll
-      for (int k = 0; k < HW; ++k) oc += osum[HW + k][r][0];
-      const float vc = oc + P[L.b3c];
-      dz[3] = 2.0f * inv * (vc - ax[r][7]);                          // d mse / d v
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) { dz3s[r][q] = dz[q]; lsp[r][q] = dls[q]; }
   }
   __syncthreads();
-  float* tp = ptail + (int64_t)blockIdx.x * L.tail;                  // tail-relative slab
+  PHASE_PROBE(4);
+  float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < CT; ++t) {
     const int n = n0 + 16 * t + li;
     float cb2 = 0.f, cw[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = 4 * lg + j;
-      const float h = acc[t][j];
-      float dh;
-      if (net == 0) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
-      else dh = dz3s[r][3] * w3[t][0];
-      const float d2 = dh * (1.0f - h * h);                         // tanh backward
-      dzs[net][r][n] = d2;
-      if (r0 + r < mb) dZ2g[((int64_t)net * mb + r0 + r) * H + n] = d2;
-      cb2 += d2;
-      if (net == 0) {
-        cw[0] = fmaf(dz3s[r][0], h, cw[0]); cw[1] = fmaf(dz3s[r][1], h, cw[1]); cw[2] = fmaf(dz3s[r][2], h, cw[2]);
-      } else {
-        cw[0] = fmaf(dz3s[r][3], h, cw[0]);
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * rt + 4 * lg + j;
+        const float h = acc[rt][t][j];
+        float dh;
+        if (net == 0) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
+        else dh = dz3s[r][3] * w3[t][0];
+        const float d2 = dh * (1.0f - h * h);                       // tanh backward
+        dzs[r][n] = d2;
+        if (r0 + r < mb) dZ2g[((int64_t)net * mb + r0 + r) * H + n] = d2;
+        cb2 += d2;
+        if (net == 0) {
+          cw[0] = fmaf(dz3s[r][0], h, cw[0]); cw[1] = fmaf(dz3s[r][1], h, cw[1]); cw[2] = fmaf(dz3s[r][2], h, cw[2]);
+        } else {
+          cw[0] = fmaf(dz3s[r][3], h, cw[0]);
+        }
       }
-    }
     cb2 += __shfl_xor(cb2, 16, 64); cb2 += __shfl_xor(cb2, 32, 64);
 #pragma unroll
     for (int q = 0; q < 3; ++q) { cw[q] += __shfl_xor(cw[q], 16, 64); cw[q] += __shfl_xor(cw[q], 32, 64); }
     if (lg == 0) {
-      tp[net * H + n] = cb2;                                         // db2
+      tp[net * H + n] = cb2;                                       // db2
       if (net == 0) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
-      else tp[5 * H + 8 + n] = cw[0];                                // dW3c
+      else tp[5 * H + 8 + n] = cw[0];                              // dW3c
     }
   }
   if (tid < 4) {
@@ -326,30 +379,41 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       sl += tid < 3 ? lsp[r][tid] : 0.0f;
       sc += tid == 0 ? dz3s[r][3] : 0.0f;
     }
-    tp[5 * H + tid] = sb;            // b3a
-    tp[5 * H + 4 + tid] = sl;        // log_std
-    tp[6 * H + 8 + tid] = sc;        // b3c
+    if (net == 0) {
+      tp[5 * H + tid] = sb;          // b3a
+      tp[5 * H + 4 + tid] = sl;      // log_std
+    } else {
+      tp[6 * H + 8 + tid] = sc;      // b3c
+    }
   }
   __syncthreads();
+  PHASE_PROBE(5);
 
   // ---- D: dH1 = dZ2 W2 -------------------------------------------------------
 #pragma unroll
-  for (int t = 0; t < T; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows16<H, LDA, H, T>(&dzs[net][0][0], W2T + (int64_t)net * H * H, n0, acc);
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
+  mfma_rows<H, LDA, H, RT, CT>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc);
+  PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
-  // acc[t][j] = dZ1[row 4lg+j][n0+16t+li] is the A operand A[n][r] of the
-  // product (k = row, kk = j); B[r][k'] = S[4lg+kk][16h + li] from LDS.
-  float* pw = pw1 + (int64_t)blockIdx.x * 2 * H * 20 + (int64_t)net * H * 20;
+  // acc[rt][t][j] = dZ1[row 16rt+4lg+j][n0+16t+li] is the A operand A[n][r] of
+  // the product (k = row, kk = j); B[r][k'] = S[16rt+4lg+kk][16hb + li] from LDS.
+  float* pw = pw1 + (int64_t)rb * 2 * H * 20 + (int64_t)net * H * 20;
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < CT; ++t) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[t][j] = acc[t][j] * (1.0f - h1[t][j] * h1[t][j]);   // tanh backward
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[rt][t][j] = acc[rt][t][j] * (1.0f - h1[rt][t][j] * h1[rt][t][j]);
 #pragma unroll
     for (int hb = 0; hb < 2; ++hb) {
       f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[t][kk], S[4 * lg + kk][16 * hb + li], d);
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[rt][t][kk], S[16 * rt + 4 * lg + kk][16 * hb + li], d);
       // d[j] = dW1aug[n = n0 + 16t + 4lg + j][k' = 16hb + li]
       const int kp = 16 * hb + li;
       if (kp < 20) {
@@ -358,6 +422,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       }
     }
   }
+  PHASE_PROBE(7);
 }
 
 // block-level f64 pair sum in fixed order
@@ -579,12 +644,10 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
 int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const float* P, const float* W2T,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream) {
-  if (!valid_h(H) || mb <= 0 || !src || !idx || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1) return -1;
-  dim3 g(n_head_wg(mb));
+  if (!valid_h(H) || mb <= 0 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1) return -1;
+  dim3 g(2 * n_head_wg(mb));                       // (row block, net) pairs
   hipStream_t s = (hipStream_t)stream;
-  // waves per workgroup: two tiles of 16 hidden columns per wave, so a CU
-  // keeps 16 waves' worth of W2 fetches in flight (the GEMM phases are
-  // L2-latency bound at one wave per SIMD)
+  // waves per workgroup: one 16-column tile per wave for both 16-row tiles
   if (H == 64)
     hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1);
@@ -630,3 +693,9 @@ int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const 
 const char* satrl_ppo_last_error(void) { return g_err.c_str(); }
 
 }  // extern "C"
+
+#ifdef SATRL_PHASE_PROBE
+extern "C" int satrl_probe_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(g_probe)) == hipSuccess ? 0 : -1;
+}
+#endif

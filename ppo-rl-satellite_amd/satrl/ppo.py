@@ -179,18 +179,23 @@ class FusedMinibatch:
         self.p2 = torch.empty(2 * self.S * H * H, **f32)
         self.nsq = torch.zeros(2 * self.nblk, dtype=torch.float64, device=dev)
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
+        # the rows of one group of minibatches, gathered contiguously once per
+        # group (one index_select) so rowpass reads them without an index hop
+        self.stage = torch.empty((self.group * self.mb, 32), **f32)
         self.graph = None
         self._src_ptr = None
 
     def rowpass(self, src, idx, mb=None):
         """satrl_ppo_rowpass alone (a pure function of src, idx and the
-        parameters: bench.py times it on its own for the roofline)."""
+        parameters: bench.py times it on its own for the roofline).  idx None:
+        rows 0..mb-1 of src."""
         L = self.L
         H = L.H
         mb = self.mb if mb is None else int(mb)
         n = 2 * mb * H
         H1, dZ2 = self.H1[:n], self.dZ2[:n]
-        check(_lib.lib().satrl_ppo_rowpass(H, mb, ptr(src), ptr(idx), ptr(L.P), ptr(L.W2T), float(L.epsilon),
+        check(_lib.lib().satrl_ppo_rowpass(H, mb, ptr(src), None if idx is None else ptr(idx), ptr(L.P), ptr(L.W2T),
+                                           float(L.epsilon),
                                            float(L.entropy_coef), float(L.max_action), ptr(H1), ptr(dZ2),
                                            ptr(self.ptail), ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass")
         return H1, dZ2
@@ -229,14 +234,28 @@ class FusedMinibatch:
                                  float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
                                  ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
 
+    def _group(self, src, ng):
+        """ng minibatches whose indices are in self.idx[:ng]: one gather of
+        their rows into self.stage, then ng steps on contiguous rows."""
+        mb = self.mb
+        torch.index_select(src, 0, self.idx[:ng].view(-1), out=self.stage[:ng * mb])
+        for k in range(ng):
+            self.step(self.stage[k * mb:(k + 1) * mb], None)
+
     def _capture(self, src):
+        # hipBLASLt sets up a GEMM shape on its first call, which is not
+        # capture-safe: run the dW2 product once eagerly into the scratch slabs
+        H, mb, S = self.L.H, self.mb, self.S
+        n = 2 * mb * H
+        torch.bmm(self.dZ2[:n].view(2 * S, mb // S, H).transpose(1, 2), self.H1[:n].view(2 * S, mb // S, H),
+                  out=self.p2.view(2 * S, H, H))
+        torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            for k in range(self.group):
-                self.step(src, self.idx[k])
+            self._group(src, self.group)
         self._src_ptr = src.data_ptr()
 
     def run(self, src, perm):
@@ -254,8 +273,7 @@ class FusedMinibatch:
                     self._capture(src)
                 self.graph.replay()
             else:
-                for j in range(ng):
-                    self.step(src, self.idx[j])
+                self._group(src, ng)
             k += ng
         if B % mb:
             tail = perm[nfull * mb:].contiguous()

@@ -210,3 +210,23 @@ def test_vec_trainer_graph_vs_eager_rollout():
         torch.cuda.synchronize()
         res.append((tr.buf.obs.clone(), tr.buf.rew.clone(), tr.buf.done.clone()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+
+
+def test_rowpass_contiguous_rows_match_gather():
+    """satrl_ppo_rowpass with idx=NULL on pre-gathered rows == the indexed gather (bitwise)."""
+    from satrl.ppo import PPOLearner
+    torch.manual_seed(3)
+    args = _args(hidden_width=128, mini_batch_size=1000, batch_size=8192)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    src = torch.randn((8192, 32), device="cuda", generator=g)
+    idx = torch.randperm(8192, device="cuda", generator=g)[:1000]
+    st = L.stepper(1000)
+    outs = []
+    for s_, i_ in ((src, idx), (src[idx].contiguous(), None)):
+        H1, dZ2 = st.rowpass(s_, i_)
+        torch.cuda.synchronize()
+        outs.append((H1.clone(), dZ2.clone(), st.ptail.clone(), st.pw1.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
