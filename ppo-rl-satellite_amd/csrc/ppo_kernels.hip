@@ -425,51 +425,58 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   PHASE_PROBE(7);
 }
 
-// block-level f64 pair sum in fixed order
+// ---------------------------------------------------------------------------
+// reduce: sums the three partial-slab families into G (fixed order) and/or
+// writes per-block squared norms per net (f64).  Everything moves as float4
+// (every region boundary and slab stride is a multiple of 4 floats, and a
+// float4 never straddles the actor/critic boundary).  Block ranges:
+//   [0, nb2)          W2 region: one float4 per thread, S split-K slabs [2][S][H][H]
+//   [nb2, nb2+nb1)    W1 region: 32 float4 columns x 8 chunks, nw1 slabs [nw1][2][H][20]
+//   [nb2+nb1, ...)    tail: 8 float4 columns x 32 chunks, nwg slabs [nwg][6H+12]
+// A chunk sums slabs c, c+CH, ... (all loads independent: one or two
+// latency rounds), then chunk 0 adds the CH partials in order.
+// ---------------------------------------------------------------------------
+struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg; };
+constexpr int kRedCH1 = 8, kRedCHt = 32;
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ double sq4(float4 v) {
+  return (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+}
+
+template <int CH>
+__device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, int64_t stride4, int nparts,
+                                             int64_t col, bool valid, float4* red) {
+  constexpr int EB = 256 / CH;
+  const int t = threadIdx.x, e = t % EB, c = t / EB;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+#pragma unroll 16
+    for (int w = c; w < nparts; w += CH) s = f4add(s, part[(int64_t)w * stride4 + col]);
+  }
+  red[t] = s;
+  __syncthreads();
+  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c == 0) {
+    for (int k = 0; k < CH; ++k) tot = f4add(tot, red[k * EB + e]);
+  }
+  return tot;
+}
+
+// block-level f64 pair sum in fixed order, result in every thread
 __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     a += __shfl_xor(a, off, 64);
     c += __shfl_xor(c, off, 64);
   }
-  const int w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh[2 * w] = a; sh[2 * w + 1] = c; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    a = 0.0; c = 0.0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) { sh[0] = a; sh[1] = c; }
-  __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// reduce: sums the three partial-slab families into G (fixed order) and/or
-// writes per-block squared norms per net.  Block ranges:
-//   [0, nb2)          W2 region, 4 elements per thread, S split-K slabs [2][S][H][H]
-//   [nb2, nb2+nb1)    W1 region, 64 elements x 4 chunks, nw1 slabs [nw1][2][H][20]
-//   [nb2+nb1, ...)    tail, 8 elements x 32 chunks, nwg slabs [nwg][6H+12]
-// ---------------------------------------------------------------------------
-struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg; };
-
-template <int E, int CH>
-__device__ __forceinline__ float chunk_sum(const float* __restrict__ part, int64_t stride, int nparts, int64_t el,
-                                           bool valid, float (*sh)[CH + 1]) {
-  const int t = threadIdx.x, e = t % E, c = t / E;
-  float s = 0.0f;
-  if (valid) {
-#pragma unroll 8
-    for (int w = c; w < nparts; w += CH) s += part[(int64_t)w * stride + el];
-  }
-  sh[e][c] = s;
-  __syncthreads();
-  float tot = 0.0f;
-  if (c == 0) {
-    for (int k = 0; k < CH; ++k) tot += sh[e][k];
-  }
-  __syncthreads();
-  return tot;
+  a = 0.0; c = 0.0;
+  for (int k = 0; k < nw; ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
 }
 
 __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode, const float* __restrict__ p2,
@@ -478,56 +485,55 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
                                                      double* __restrict__ steps) {
   const Layout L = layout(H);
   __shared__ double sh[8];
-  __shared__ float red[64][33];
+  __shared__ float4 red[256];
   double sa = 0.0, sc = 0.0;
   const int t = threadIdx.x;
-  const int64_t HH = (int64_t)H * H;
+  const int64_t HH4 = (int64_t)H * H / 4;
+  float4* G4 = reinterpret_cast<float4*>(G);
   int b = blockIdx.x;
   if (b < g.nb2) {                                                // W2: [2][S] slabs of H*H
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t e = (int64_t)b * 1024 + k * 256 + t;
-      if (e < L.W1) {
-        const int net = e >= HH;
-        float v;
-        if (mode & 1) {
-          const int64_t i = e - net * HH;
-          const float* q = p2 + (int64_t)net * g.S * HH + i;
-          v = 0.0f;
-          for (int s2 = 0; s2 < g.S; ++s2) v += q[(int64_t)s2 * HH];
-          G[e] = v;
-        } else {
-          v = G[e];
-        }
-        if (net) sc += (double)v * v; else sa += (double)v * v;
+    const int64_t e4 = (int64_t)b * 256 + t;
+    if (e4 < 2 * HH4) {
+      const int net = e4 >= HH4;
+      float4 v;
+      if (mode & 1) {
+        const float4* q = reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4 + (e4 - net * HH4);
+        v = q[0];
+        for (int s2 = 1; s2 < g.S; ++s2) v = f4add(v, q[(int64_t)s2 * HH4]);
+        G4[e4] = v;
+      } else {
+        v = G4[e4];
       }
+      if (net) sc += sq4(v); else sa += sq4(v);
     }
   } else if ((b -= g.nb2) < g.nb1) {                             // W1: [nw1] slabs of 2*H*20
-    const int64_t el = (int64_t)b * 64 + (t & 63);
-    const bool valid = el < 2LL * H * 20;
-    float v = 0.0f;
+    constexpr int EB = 256 / kRedCH1;
+    const int64_t n4 = 2LL * H * 20 / 4, col = (int64_t)b * EB + (t % EB);
+    const bool valid = col < n4, lead = t < EB;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
-      v = chunk_sum<64, 4>(p1, 2LL * H * 20, g.nw1, el, valid, (float(*)[5])red);
-      if ((t >> 6) == 0 && valid) G[L.W1 + el] = v;
-    } else if ((t >> 6) == 0 && valid) {
-      v = G[L.W1 + el];
+      v = chunk_sum4<kRedCH1>(reinterpret_cast<const float4*>(p1), n4, g.nw1, col, valid, red);
+      if (lead && valid) G4[L.W1 / 4 + col] = v;
+    } else if (lead && valid) {
+      v = G4[L.W1 / 4 + col];
     }
-    if ((t >> 6) == 0 && valid) {
-      if (el >= (int64_t)H * 20) sc += (double)v * v; else sa += (double)v * v;
+    if (lead && valid) {
+      if (col * 4 >= (int64_t)H * 20) sc += sq4(v); else sa += sq4(v);
     }
   } else {                                                        // tail: [nwg] slabs of 6H+12
     b -= g.nb1;
-    const int64_t el = (int64_t)b * 8 + (t & 7);
-    const bool valid = el < L.tail;
-    float v = 0.0f;
+    constexpr int EB = 256 / kRedCHt;
+    const int64_t n4 = L.tail / 4, col = (int64_t)b * EB + (t % EB);
+    const bool valid = col < n4, lead = t < EB;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
-      v = chunk_sum<8, 32>(pt, L.tail, g.nwg, el, valid, (float(*)[33])red);
-      if ((t >> 3) == 0 && valid) G[L.b2 + el] = v;
-    } else if ((t >> 3) == 0 && valid) {
-      v = G[L.b2 + el];
+      v = chunk_sum4<kRedCHt>(reinterpret_cast<const float4*>(pt), n4, g.nwg, col, valid, red);
+      if (lead && valid) G4[L.b2 / 4 + col] = v;
+    } else if (lead && valid) {
+      v = G4[L.b2 / 4 + col];
     }
-    if ((t >> 3) == 0 && valid) {
-      if (net_of(L, L.b2 + el, H)) sc += (double)v * v; else sa += (double)v * v;
+    if (lead && valid) {
+      if (net_of(L, L.b2 + col * 4, H)) sc += sq4(v); else sa += sq4(v);
     }
   }
   if (mode & 2) {
@@ -542,7 +548,20 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
 
 // ---------------------------------------------------------------------------
 // adam: torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (_single_tensor_adam)
+// Every block first folds the per-block norms (fixed order, identical in
+// every block).  Blocks [0, nbw): one 32x32 tile of a net's fc2.weight each,
+// float4 per thread, and the updated tile goes out transposed through LDS
+// into W2T (coalesced).  Blocks [nbw, ...): the rest of the layout, float4.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float step_size,
+                                           float bc2s, float w1, float w2, float beta2, float eps, int use_clip) {
+  if (use_clip) g = g * coef;                                      // grads.mul_(clip_coef_clamped)
+  m = m + w1 * (g - m);                                            // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * beta2 + w2 * (g * g);                                    // mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + eps;
+  return p + (-step_size) * (m / denom);                           // addcdiv_(m, denom, -step_size)
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double* __restrict__ nsq,
                                                    const double* __restrict__ steps, const double* __restrict__ bct,
                                                    int bct_len, const float* __restrict__ lr, float beta1,
@@ -553,42 +572,64 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float cst[2][3];                                      // coef, step_size, bc2_sqrt per net
+  __shared__ float tile[32][33];
+  const int t = threadIdx.x;
   double a = 0.0, c = 0.0;
-  for (int k = threadIdx.x; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
+  for (int k = t; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
   block_sum2(a, c, sh);
-  if (threadIdx.x < 2) {
-    const int n = threadIdx.x;
-    const double nn = n == 0 ? sh[0] : sh[1];
+  if (t < 2) {
+    const double nn = t == 0 ? a : c;
     const float nrm = (float)sqrt(nn);
-    cst[n][0] = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
+    cst[t][0] = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
     // bct[2*step] = 1 - beta1**step, bct[2*step+1] = sqrt(1 - beta2**step) (python float
     // math, as torch.optim.Adam computes them); constant 1.0 past the table
-    const int st = (int)steps[n];
+    const int st = (int)steps[t];
     const double bc1 = st < bct_len ? bct[2 * st] : 1.0;
     const double bc2s = st < bct_len ? bct[2 * st + 1] : 1.0;
-    cst[n][1] = (float)((double)lr[n] / bc1);
-    cst[n][2] = (float)bc2s;
+    cst[t][1] = (float)((double)lr[t] / bc1);
+    cst[t][2] = (float)bc2s;
   }
   __syncthreads();
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < L.total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int net = net_of(L, e, H);
-    float g = G[e];
-    if (use_clip) g = g * cst[net][0];                             // grads.mul_(clip_coef_clamped)
-    float m = M[e];
-    m = m + w1 * (g - m);                                          // exp_avg.lerp_(grad, 1 - beta1)
-    float v = V[e];
-    v = v * beta2 + w2 * (g * g);                                  // mul_(beta2).addcmul_(g, g, 1 - beta2)
-    const float denom = sqrtf(v) / cst[net][2] + eps;
-    const float pn = P[e] + (-cst[net][1]) * (m / denom);          // addcdiv_(m, denom, -step_size)
-    P[e] = pn;
-    M[e] = m;
-    V[e] = v;
-    if (W2T != nullptr && e < L.W1) {                              // keep fc2.weight^T for the dH1 MFMA
-      const int64_t HH = (int64_t)H * H, k = e % HH;
-      W2T[(e / HH) * HH + (k % H) * H + k / H] = pn;
-    }
+  const int ntc = H / 32, nbw = 2 * ntc * ntc;
+  const float4* G4 = reinterpret_cast<const float4*>(G);
+  float4* P4 = reinterpret_cast<float4*>(P);
+  float4* M4 = reinterpret_cast<float4*>(M);
+  float4* V4 = reinterpret_cast<float4*>(V);
+  int64_t e4;
+  int net;
+  if ((int)blockIdx.x < nbw) {
+    const int tb = blockIdx.x % (ntc * ntc);
+    net = blockIdx.x / (ntc * ntc);
+    const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
+    e4 = ((int64_t)net * H * H + (int64_t)n * H + k) / 4;
+  } else {
+    e4 = L.W1 / 4 + (int64_t)(blockIdx.x - nbw) * 256 + t;
+    if (e4 >= L.total / 4) return;                                 // (no barrier follows in this branch)
+    net = net_of(L, e4 * 4, H);
+  }
+  const float4 g = G4[e4];
+  float4 m = M4[e4], v = V4[e4];
+  const float4 p = P4[e4];
+  const float coef = cst[net][0], ss = cst[net][1], b2s = cst[net][2];
+  float4 pn;
+  pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  pn.z = adam_elem(g.z, m.z, v.z, p.z, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  pn.w = adam_elem(g.w, m.w, v.w, p.w, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  P4[e4] = pn;
+  M4[e4] = m;
+  V4[e4] = v;
+  if ((int)blockIdx.x < nbw && W2T != nullptr) {                   // keep fc2.weight^T for the dH1 MFMA
+    const int nl = t >> 3, kl = (t & 7) * 4;
+    tile[nl][kl] = pn.x; tile[nl][kl + 1] = pn.y; tile[nl][kl + 2] = pn.z; tile[nl][kl + 3] = pn.w;
+    __syncthreads();
+    const int tb = blockIdx.x % (ntc * ntc);
+    const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
+    // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
+    const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
+    reinterpret_cast<float4*>(W2T)[((int64_t)net * H * H + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
   }
 }
 
@@ -597,15 +638,19 @@ int n_w1_wg(int mb) { return n_head_wg(mb); }
 RedGeom geom(int H, int mb, int S) {
   const Layout L = layout(H);
   RedGeom g;
-  g.nb2 = (int)((L.W1 + 1023) / 1024);
-  g.nb1 = (int)((2LL * H * 20 + 63) / 64);
-  g.nbt = (int)((L.tail + 7) / 8);
+  g.nb2 = (int)((L.W1 / 4 + 255) / 256);
+  g.nb1 = (int)((2LL * H * 20 / 4 + (256 / kRedCH1) - 1) / (256 / kRedCH1));
+  g.nbt = (int)((L.tail / 4 + (256 / kRedCHt) - 1) / (256 / kRedCHt));
   g.S = S;
   g.nw1 = n_w1_wg(mb);
   g.nwg = n_head_wg(mb);
   return g;
 }
 int n_blocks(const RedGeom& g) { return g.nb2 + g.nb1 + g.nbt; }
+int n_adam_blocks(int H) {
+  const Layout L = layout(H);
+  return 2 * (H / 32) * (H / 32) + (int)(((L.total - L.W1) / 4 + 255) / 256);
+}
 
 bool valid_h(int H) { return H == 64 || H == 128 || H == 256; }
 
@@ -681,11 +726,9 @@ int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const 
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
                    float* P, float* M, float* V, float* W2T, void* stream) {
   if (!valid_h(H) || mb <= 0 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P || !M || !V) return -1;
-  const Layout L = layout(H);
   const int nblk = n_blocks(geom(H, mb, 1));
-  const int blocks = (int)((L.total + 1023) / 1024);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps, bct, bct_len,
-                     lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T);
+  hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps,
+                     bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T);
   LAUNCH_CHECK();
   return 0;
 }

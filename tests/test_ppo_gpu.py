@@ -177,6 +177,8 @@ def test_fused_step_vs_torch_autograd(H):
         got = P[k].reshape(ref.shape)
         assert torch.allclose(got, ref, rtol=1e-5, atol=2e-7), (k, (got - ref).abs().max().item())
     assert L.steps.cpu().tolist() == [1.0, 1.0]
+    # Adam also refreshed fc2.weight^T (the dH1 operand of the next rowpass)
+    assert torch.equal(L.W2T.view(2, H, H), L.P[:2 * H * H].view(2, H, H).transpose(1, 2))
 
 
 def test_vec_trainer_iteration_and_determinism():
