@@ -23,7 +23,7 @@ thread_local std::string g_err;
 #ifdef SATRL_PHASE_PROBE
 // development-only phase stamps (tools/_probe/phase_probe.py), never in the
 // shipped build: [workgroup][stamp][wave 0 | wave NW/2][s_memrealtime, s_memtime]
-__device__ unsigned long long g_probe[4096][8][2][2];
+__device__ unsigned long long g_probe[4096][16][2][2];
 #define PHASE_PROBE(k)                                                        \
   do {                                                                        \
     if (threadIdx.x == 0 || threadIdx.x == blockDim.x / 2) {                  \
@@ -191,6 +191,24 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   PHASE_PROBE(0);
 
   // ---- A: gather, fc1 on MFMA ------------------------------------------------
+  // this wave's W1aug rows [n][20] (k 0..19, zero-padded to 32; lane group g
+  // takes k = 8g .. 8g+7), issued first so they overlap the row gather
+  float4 bw1[CT][2];
+  {
+    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
+      bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lg < 2) {
+        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
+        bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
+      } else if (lg == 2) {
+        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
+      }
+    }
+  }
   for (int q = tid; q < R * 26; q += NT) {
     const int r = q / 26, c = q % 26, row = r0 + r;
     const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
@@ -200,6 +218,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
     const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
     S[r][c] = (c == 18 && r0 + r < mb) ? 1.0f : 0.0f;             // bias column of W1aug, zero pad
   }
+  PHASE_PROBE(8);
   // fc2 bias and output-layer weights of this wave's columns (used in C)
   float w3[CT][3], b2v[CT];
 #pragma unroll
@@ -213,26 +232,15 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
     }
   }
   __syncthreads();
+  PHASE_PROBE(9);
   f4 acc[RT][CT];
   float h1[RT][CT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  {
-    // W1aug rows [n][20] (k 0..19) padded to 32 with zeros: lane group g takes k = 8g .. 8g+7
-    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
-    float4 b[CT][2];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
-      b[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
-      b[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lg < 2) { b[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg); b[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4); }
-      else if (lg == 2) b[t][0] = *reinterpret_cast<const float4*>(bp + 16);
-    }
-    mfma_chunk<LDS_S, RT, CT>(&S[li][8 * lg], b, acc);
-  }
+  mfma_chunk<LDS_S, RT, CT>(&S[li][8 * lg], bw1, acc);
+  PHASE_PROBE(10);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -248,6 +256,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       }
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
+  PHASE_PROBE(11);
   __syncthreads();
   PHASE_PROBE(1);
 
