@@ -71,6 +71,23 @@ int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream);
 
+/* Rollout forward passes on the rowpass's own MLP code, so every row's result
+ * is independent of N and of the sharding, and the rollout's log-probs equal
+ * the update's first recomputation bit for bit.
+ * satrl_policy_act <- CPPO_main.py:122-123 (both agents' choose_action,
+ * ppo_continuous.py:176-189): for the actor (net 0) of each flat parameter
+ * set P0 (pursuer, agent 0) and P1 (evader, agent 1; nullable = one agent),
+ * mean = max_action*tanh(mean_layer), a = clamp(mean + exp(log_std)*z,
+ * +-max_action), per-dim Normal log-prob; z from Philox4x32-10 keyed by
+ * (seed, agent, env_offset + row, step + *step_base) exactly as
+ * satrl_gaussian_sample.  obs f32 [N][18], act/logp f32 [N][3].           */
+int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const float* P1, float max_action,
+                     uint64_t seed, int64_t env_offset, uint64_t step, const uint64_t* step_base, float* act0,
+                     float* logp0, float* act1, float* logp1, void* stream);
+/* critic value v f32 [N] of the flat parameters P (net 1) <- self.critic(s),
+ * ppo_continuous.py:200-201                                               */
+int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float* v_out, void* stream);
+
 const char* satrl_ppo_last_error(void);
 
 #ifdef __cplusplus

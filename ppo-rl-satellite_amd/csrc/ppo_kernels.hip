@@ -14,6 +14,7 @@
 #include <cmath>
 #include <string>
 
+#include "philox_device.h"
 #include "satrl_ppo.h"
 
 namespace {
@@ -168,27 +169,36 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 1), y, acc);
 }
 
+// Shared-memory block and forward pass (phases A, B and the output-layer dot
+// products of C) common to rowpass_kernel and policy_kernel, so the rollout's
+// policy/value forward and the update's forward are the same instructions in
+// the same order: logp_old from the rollout equals the update's first
+// recomputation bit for bit, and every row's result is independent of N.
 template <int H, int NW>
-__global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* __restrict__ src,
-                                                      const int64_t* __restrict__ idx, const float* __restrict__ P,
-                                                      const float* __restrict__ W2T, float epsilon, float ent_coef,
-                                                      float max_action, float* __restrict__ H1g,
-                                                      float* __restrict__ dZ2g, float* __restrict__ ptail,
-                                                      float* __restrict__ pw1) {
+struct MlpSmem {
+  static constexpr int R = kRows, LDA = H + 4, LDS_S = 36;
+  float h1s[R][LDA] __attribute__((aligned(16)));     // tanh(fc1)
+  float S[R][LDS_S] __attribute__((aligned(16)));     // [s(18) | 1 | 0...] per row
+  float osum[NW][R][3];                               // per-wave output-layer partial sums
+};
+
+// Rows r < nvalid of the block must be in S[r][0..17] when gather() returns;
+// gather(tid, NT) runs while this wave's W1 rows are in flight.  On return
+// acc = tanh(fc2) for this wave's columns, h1 = tanh(fc1) (for the fc1
+// backward), w3 = this wave's output-layer weights, and osum holds the
+// per-wave dot products (after a barrier).  h1out (nullable): row r of
+// tanh(fc1) goes to h1out[r * H + n].
+template <int H, int NW, class Gather>
+__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW>& sm, const float* __restrict__ P, int net, int nvalid,
+                                            Gather gather, float* __restrict__ h1out,
+                                            f4 (&acc)[kRows / 16][H / 16 / NW],
+                                            float (&h1)[kRows / 16][H / 16 / NW][4],
+                                            float (&w3)[H / 16 / NW][3]) {
   constexpr int R = kRows, RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
   static_assert(CT >= 1 && H % (16 * NW) == 0, "tile split");
   const Layout L = layout(H);
-  __shared__ __attribute__((aligned(16))) float h1s[R][LDA];     // tanh(fc1)
-  __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
-  __shared__ __attribute__((aligned(16))) float S[R][LDS_S];     // [s(18) | 1 | 0...] per row
-  __shared__ float ax[R][8];
-  __shared__ float osum[NW][R][3];
-  __shared__ float dz3s[R][4];
-  __shared__ float lsp[R][4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
-  const int net = blockIdx.x & 1, rb = blockIdx.x >> 1, n0 = w * (H / NW);
-  const int r0 = rb * R;
-  PHASE_PROBE(0);
+  const int n0 = w * (H / NW);
 
   // ---- A: gather, fc1 on MFMA ------------------------------------------------
   // this wave's W1aug rows [n][20] (k 0..19, zero-padded to 32; lane group g
@@ -209,18 +219,14 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       }
     }
   }
-  for (int q = tid; q < R * 26; q += NT) {
-    const int r = q / 26, c = q % 26, row = r0 + r;
-    const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
-    if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;             // s | a, logp_old, adv, v_target
-  }
+  gather(tid, NT);
   for (int q = tid; q < R * (LDS_S - 18); q += NT) {
     const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
-    S[r][c] = (c == 18 && r0 + r < mb) ? 1.0f : 0.0f;             // bias column of W1aug, zero pad
+    sm.S[r][c] = (c == 18 && r < nvalid) ? 1.0f : 0.0f;           // bias column of W1aug, zero pad
   }
   PHASE_PROBE(8);
   // fc2 bias and output-layer weights of this wave's columns (used in C)
-  float w3[CT][3], b2v[CT];
+  float b2v[CT];
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const int n = n0 + 16 * t + li;
@@ -233,13 +239,11 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   }
   __syncthreads();
   PHASE_PROBE(9);
-  f4 acc[RT][CT];
-  float h1[RT][CT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_chunk<LDS_S, RT, CT>(&S[li][8 * lg], bw1, acc);
+  mfma_chunk<LDS_S, RT, CT>(&sm.S[li][8 * lg], bw1, acc);
   PHASE_PROBE(10);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -251,8 +255,8 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
         const int r = 16 * rt + 4 * lg + j;
         const float h = tanhf(acc[rt][t][j]);                      // fc1 + tanh
         h1[rt][t][j] = h;
-        h1s[r][n] = h;
-        if (r0 + r < mb) H1g[((int64_t)net * mb + r0 + r) * H + n] = h;
+        sm.h1s[r][n] = h;
+        if (h1out != nullptr && r < nvalid) h1out[(int64_t)r * H + n] = h;
       }
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -261,10 +265,10 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  mfma_rows<H, LDA, H, RT, CT>(&h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  mfma_rows<H, LDA, H, RT, CT>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);
 
-  // ---- C: fc2 tanh, output layer(s), loss, dZ2 --------------------------------
+  // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
   const int NQ = net == 0 ? 3 : 1;                                  // output columns of this net
   float p[3][RT][4];
 #pragma unroll
@@ -292,11 +296,55 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float v = row16_sum(p[q][rt][j]);
-        if (li == 0) osum[w][16 * rt + 4 * lg + j][q] = v;
+        if (li == 0) sm.osum[w][16 * rt + 4 * lg + j][q] = v;
       }
   }
   __syncthreads();
   PHASE_PROBE(3);
+}
+
+// output-layer pre-activation of row r, column d: wave partials in fixed order
+template <int NW>
+__device__ __forceinline__ float out_sum(const float (*osum)[kRows][3], int r, int d) {
+  float od = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) od += osum[k][r][d];
+  return od;
+}
+
+template <int H, int NW>
+__global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* __restrict__ src,
+                                                      const int64_t* __restrict__ idx, const float* __restrict__ P,
+                                                      const float* __restrict__ W2T, float epsilon, float ent_coef,
+                                                      float max_action, float* __restrict__ H1g,
+                                                      float* __restrict__ dZ2g, float* __restrict__ ptail,
+                                                      float* __restrict__ pw1) {
+  constexpr int R = kRows, RT = R / 16, LDA = H + 4, CT = H / 16 / NW;
+  const Layout L = layout(H);
+  __shared__ MlpSmem<H, NW> sm;
+  __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
+  __shared__ float ax[R][8];
+  __shared__ float dz3s[R][4];
+  __shared__ float lsp[R][4];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
+  const int net = blockIdx.x & 1, rb = blockIdx.x >> 1, n0 = w * (H / NW);
+  const int r0 = rb * R;
+  auto& S = sm.S;
+  PHASE_PROBE(0);
+
+  f4 acc[RT][CT];
+  float h1[RT][CT][4];
+  float w3[CT][3];
+  auto gather = [&](int t0, int nt) {
+    for (int q = t0; q < R * 26; q += nt) {
+      const int r = q / 26, c = q % 26, row = r0 + r;
+      const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
+      if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
+    }
+  };
+  mlp_forward<H, NW>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+
+  // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
     const int r = tid, row = r0 + r;
     float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
@@ -306,10 +354,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          float od = 0.0f;
-#pragma unroll
-          for (int k = 0; k < NW; ++k) od += osum[k][r][d];
-          th[d] = tanhf(od + P[L.b3a + d]);
+          th[d] = tanhf(out_sum<NW>(sm.osum, r, d) + P[L.b3a + d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           const float sd = expf(P[L.ls + d]);
           var[d] = sd * sd;
@@ -336,10 +381,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
           dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        float oc = 0.0f;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) oc += osum[k][r][0];
-        const float vc = oc + P[L.b3c];
+        const float vc = out_sum<NW>(sm.osum, r, 0) + P[L.b3c];
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
@@ -432,6 +474,60 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
     }
   }
   PHASE_PROBE(7);
+}
+
+// ---------------------------------------------------------------------------
+// policy: the rollout's forward passes on the rowpass's own MLP code
+// (mlp_forward), one workgroup per 32-row block and net.
+//   MODE 0  actor -> mean = max_action*tanh(.) -> Normal sample -> clamp ->
+//           per-dim log-prob (ppo_continuous.py:176-189) for `nagents`
+//           parameter sets (blockIdx % nagents = agent: P0 pursuer, P1
+//           evader; the actor is net 0 of each flat layout)
+//   MODE 1  critic value (net 1 of P0), ppo_continuous.py:200-201
+// ---------------------------------------------------------------------------
+template <int H, int NW, int MODE>
+__global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float* __restrict__ obs,
+                                                     const float* __restrict__ P0, const float* __restrict__ P1,
+                                                     int nagents, float max_action, uint32_t k00, uint32_t k01,
+                                                     uint32_t k10, uint32_t k11, int64_t env_offset, uint64_t step,
+                                                     const uint64_t* __restrict__ step_base,
+                                                     float* __restrict__ act0, float* __restrict__ logp0,
+                                                     float* __restrict__ act1, float* __restrict__ logp1,
+                                                     float* __restrict__ value) {
+  constexpr int R = kRows, RT = R / 16, CT = H / 16 / NW;
+  const Layout L = layout(H);
+  __shared__ MlpSmem<H, NW> sm;
+  const int agent = MODE == 0 ? (int)(blockIdx.x % nagents) : 0;
+  const int64_t r0 = (int64_t)(MODE == 0 ? blockIdx.x / nagents : blockIdx.x) * R;
+  const float* P = agent == 0 ? P0 : P1;
+  const int nvalid = (int)(N - r0 < R ? N - r0 : R);
+  auto gather = [&](int t0, int nt) {
+    for (int q = t0; q < R * 18; q += nt) {
+      const int r = q / 18, c = q % 18;
+      sm.S[r][c] = r < nvalid ? obs[(r0 + r) * 18 + c] : 0.0f;
+    }
+  };
+  f4 acc[RT][CT];
+  float h1[RT][CT][4];
+  float w3[CT][3];
+  mlp_forward<H, NW>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  const int r = threadIdx.x;
+  if (r >= nvalid) return;                                       // no barrier follows
+  const int64_t i = r0 + r;
+  if (MODE == 1) {
+    value[i] = out_sum<NW>(sm.osum, r, 0) + P[L.b3c];
+    return;
+  }
+  float z[4];
+  philox_normal4((uint64_t)(env_offset + i), step + (step_base ? *step_base : 0ull), agent == 0 ? k00 : k10,
+                 agent == 0 ? k01 : k11, z);
+  float* act = agent == 0 ? act0 : act1;
+  float* logp = agent == 0 ? logp0 : logp1;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float mu = max_action * tanhf(out_sum<NW>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
+    gaussian_act(mu, P[L.ls + d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -738,6 +834,47 @@ int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const 
   const int nblk = n_blocks(geom(H, mb, 1));
   hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps,
                      bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const float* P1, float max_action,
+                     uint64_t seed, int64_t env_offset, uint64_t step, const uint64_t* step_base, float* act0,
+                     float* logp0, float* act1, float* logp1, void* stream) {
+  if (!valid_h(H) || N <= 0 || !obs || !P0 || !act0 || !logp0) return -1;
+  if (P1 && (!act1 || !logp1)) return -1;
+  const int nag = P1 ? 2 : 1;
+  uint32_t k00, k01, k10, k11;
+  philox_key(seed, 0, k00, k01);
+  philox_key(seed, 1, k10, k11);
+  const dim3 g((unsigned)(nag * ((N + kRows - 1) / kRows)));
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 64)
+    hipLaunchKernelGGL((policy_kernel<64, 4, 0>), g, dim3(256), 0, s, N, obs, P0, P1, nag, max_action, k00, k01, k10,
+                       k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
+  else if (H == 128)
+    hipLaunchKernelGGL((policy_kernel<128, 8, 0>), g, dim3(512), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
+                       k10, k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
+  else
+    hipLaunchKernelGGL((policy_kernel<256, 16, 0>), g, dim3(1024), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
+                       k10, k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float* v_out, void* stream) {
+  if (!valid_h(H) || N <= 0 || !obs || !P || !v_out) return -1;
+  const dim3 g((unsigned)((N + kRows - 1) / kRows));
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 64)
+    hipLaunchKernelGGL((policy_kernel<64, 4, 1>), g, dim3(256), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
+                       (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
+  else if (H == 128)
+    hipLaunchKernelGGL((policy_kernel<128, 8, 1>), g, dim3(512), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
+                       (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
+  else
+    hipLaunchKernelGGL((policy_kernel<256, 16, 1>), g, dim3(1024), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
+                       (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
   LAUNCH_CHECK();
   return 0;
 }

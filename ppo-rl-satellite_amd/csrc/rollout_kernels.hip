@@ -3,6 +3,7 @@
 
 #include <string>
 
+#include "philox_device.h"
 #include "satrl_rollout.h"
 
 namespace {
@@ -42,34 +43,9 @@ __global__ void __launch_bounds__(256) gae_kernel(int64_t T, int64_t N, const fl
   }
 }
 
-// ---------------------------------------------------------------------------
-// Philox4x32-10 counter-based RNG
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int rnd = 0; rnd < 10; ++rnd) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-    c[0] = n0;
-    c[1] = (uint32_t)p1;
-    c[2] = n2;
-    c[3] = (uint32_t)p0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-}
-
-__device__ __forceinline__ float u01_open0(uint32_t x) {   // (0, 1]
-  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
-}
-__device__ __forceinline__ float u01(uint32_t x) {         // [0, 1)
-  return (float)(x >> 8) * (1.0f / 16777216.0f);
-}
-
 // choose_action (ppo_continuous.py:184-188): a = clamp(mean + std*z, +-max);
-// log_prob(a) per dim as torch.distributions.Normal.log_prob.
+// log_prob(a) per dim as torch.distributions.Normal.log_prob.  Noise:
+// philox_device.h, keyed by (seed, agent, global env id, step).
 __global__ void __launch_bounds__(256) gaussian_kernel(int64_t N, const float* __restrict__ mean,
                                                        const float* __restrict__ log_std, float max_action,
                                                        uint32_t k0, uint32_t k1, int64_t env_offset,
@@ -78,34 +54,11 @@ __global__ void __launch_bounds__(256) gaussian_kernel(int64_t N, const float* _
                                                        float* __restrict__ logp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
-  const uint64_t gid = (uint64_t)(env_offset + i);
   if (step_base) step += *step_base;
-  uint32_t c[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
-  philox(c, k0, k1);
   float z[4];
-  {
-    const float r0 = sqrtf(-2.0f * logf(u01_open0(c[0])));
-    const float t0 = 6.283185307179586f * u01(c[1]);
-    const float r1 = sqrtf(-2.0f * logf(u01_open0(c[2])));
-    const float t1 = 6.283185307179586f * u01(c[3]);
-    z[0] = r0 * cosf(t0);
-    z[1] = r0 * sinf(t0);
-    z[2] = r1 * cosf(t1);
-    z[3] = r1 * sinf(t1);
-  }
-  const float kLogSqrt2Pi = 0.9189385332046727f;   // math.log(math.sqrt(2 * math.pi))
+  philox_normal4((uint64_t)(env_offset + i), step, k0, k1, z);
 #pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const float ls = log_std[d];
-    const float sd = expf(ls);                      // std = exp(log_std)
-    const float m = mean[i * 3 + d];
-    float a = m + sd * z[d];                        // Normal.sample()
-    a = fminf(fmaxf(a, -max_action), max_action);   // torch.clamp
-    const float var = sd * sd;
-    const float dv = a - m;
-    act[i * 3 + d] = a;
-    logp[i * 3 + d] = (-(dv * dv) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi;
-  }
+  for (int d = 0; d < 3; ++d) gaussian_act(mean[i * 3 + d], log_std[d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
 }
 
 __global__ void __launch_bounds__(256) moments_kernel(int64_t n, const float* __restrict__ x,
@@ -154,8 +107,8 @@ int satrl_gaussian_sample(int64_t N, const float* mean, const float* log_std, fl
                           uint32_t agent, int64_t env_offset, uint64_t step, const uint64_t* step_base,
                           float* act_out, float* logp_out, void* stream) {
   if (N <= 0 || !mean || !log_std || !act_out || !logp_out) return -1;
-  const uint32_t k0 = (uint32_t)seed ^ (agent * 0x85EBCA6Bu);
-  const uint32_t k1 = (uint32_t)(seed >> 32) ^ (agent * 0xC2B2AE35u + 0x27D4EB2Fu);
+  uint32_t k0, k1;
+  philox_key(seed, agent, k0, k1);
   hipLaunchKernelGGL(gaussian_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, N, mean,
                      log_std, max_action, k0, k1, env_offset, step, step_base, act_out, logp_out);
   HIP_CHECK_LAUNCH();

@@ -84,6 +84,9 @@ _SIGS = {
                         C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp, _vp, _vp,
                            _vp], C.c_int),
+    "satrl_policy_act": ([C.c_int, _i64, _vp, _vp, _vp, C.c_float, C.c_uint64, _i64, C.c_uint64, _vp, _vp, _vp, _vp,
+                          _vp, _vp], C.c_int),
+    "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_last_error": ([], C.c_char_p),
 }
 

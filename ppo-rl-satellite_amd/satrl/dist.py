@@ -1,0 +1,72 @@
+"""Data-parallel plumbing: one process per GPU, envs sharded
+by global env id, and exactly four collectives -- the start-up parameter
+broadcast, one all-reduce of (sum, sum of squares, count) of the advantages
+per update, one all-reduce of the flat gradient per minibatch (both nets,
+one bucket, before clipping so every rank clips identically), and the
+episode-statistics sum.  Plain torch.distributed calls on whatever device
+the tensors live on: RCCL over xGMI on the GPUs, gloo in the CPU tests.
+``pg=None`` means a single process (every function is then local)."""
+from __future__ import annotations
+
+import torch
+
+
+def world_size(pg) -> int:
+    if pg is None:
+        return 1
+    import torch.distributed as dist
+    return dist.get_world_size(pg)
+
+
+def rank(pg) -> int:
+    if pg is None:
+        return 0
+    import torch.distributed as dist
+    return dist.get_rank(pg)
+
+
+def env_offset(pg, n_local: int) -> int:
+    """First global env id of this rank (rank r owns [r*n, (r+1)*n))."""
+    return rank(pg) * int(n_local)
+
+
+def broadcast_(tensors, pg, src: int = 0):
+    """Start-up: every rank takes rank src's parameters (in place)."""
+    if pg is None:
+        return
+    import torch.distributed as dist
+    for t in tensors:
+        dist.broadcast(t, src=src, group=pg)
+
+
+def global_mean_std(local3: torch.Tensor, pg):
+    """local3 = [sum, sum of squares, count] (f64) of this rank's advantages
+    -> global mean and unbiased std (ppo_continuous.py:209-210 uses
+    torch.std, i.e. n-1), both f64 tensors."""
+    buf = local3.to(torch.float64).clone()
+    if pg is not None:
+        import torch.distributed as dist
+        dist.all_reduce(buf, group=pg)
+    s, s2, n = buf[0], buf[1], buf[2]
+    mean = s / n
+    var = (s2 - n * mean * mean) / (n - 1)
+    return mean, var.clamp_min(0).sqrt()
+
+
+def average_(flat: torch.Tensor, pg) -> torch.Tensor:
+    """Per minibatch: every rank's gradient of its own minibatch mean ->
+    the mean over ranks (= the gradient of the mean over all ranks' rows)."""
+    if pg is not None:
+        import torch.distributed as dist
+        dist.all_reduce(flat, group=pg)
+        flat.div_(world_size(pg))
+    return flat
+
+
+def sum_(t: torch.Tensor, pg) -> torch.Tensor:
+    """Episode statistics: totals over ranks (returns a new tensor)."""
+    out = t.clone()
+    if pg is not None:
+        import torch.distributed as dist
+        dist.all_reduce(out, group=pg)
+    return out

@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import dist as _dist
 from ._lib import check, ptr, stream_ptr
 
 LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
@@ -134,6 +135,28 @@ def gaussian_sample(mean, log_std, max_action, seed, agent, env_offset, step, ac
     return act_out, logp_out
 
 
+def policy_act(H, obs, P0, P1, max_action, seed, env_offset, step, act0, logp0, act1=None, logp1=None,
+               step_base=None):
+    """Both agents' choose_action for a batch of observations on the fused
+    MLP kernel (satrl_policy_act): P0/P1 are the pursuer's / evader's flat
+    parameter buffers (PPOLearner.P), agent ids 0 / 1 in the noise key."""
+    N = obs.shape[0]
+    _lib.require_cuda(obs, torch.float32, (N, 18), "obs")
+    for t, nm in ((act0, "act0"), (logp0, "logp0")) + (((act1, "act1"), (logp1, "logp1")) if P1 is not None else ()):
+        _lib.require_cuda(t, torch.float32, (N, 3), nm)
+    check(_lib.lib().satrl_policy_act(int(H), N, ptr(obs), ptr(P0), ptr(P1), float(max_action),
+                                      int(seed) & (2**64 - 1), int(env_offset), int(step), ptr(step_base), ptr(act0),
+                                      ptr(logp0), ptr(act1), ptr(logp1), stream_ptr()), "satrl_policy_act")
+
+
+def policy_value(H, obs, P, v_out):
+    """critic(obs) on the fused MLP kernel (satrl_policy_value)."""
+    N = obs.shape[0]
+    _lib.require_cuda(obs, torch.float32, (N, 18), "obs")
+    check(_lib.lib().satrl_policy_value(int(H), N, ptr(obs), ptr(P), ptr(v_out), stream_ptr()), "satrl_policy_value")
+    return v_out
+
+
 def moments(x, out=None):
     out = torch.zeros(2, dtype=torch.float64, device=x.device) if out is None else out
     x = x.reshape(-1)
@@ -223,11 +246,9 @@ class FusedMinibatch:
             check(lib.satrl_ppo_reduce(H, mb, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        ptr(self.nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
-            import torch.distributed as dist
             check(lib.satrl_ppo_reduce(H, mb, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G), None,
                                        None, sp), "satrl_ppo_reduce")
-            dist.all_reduce(L.G, group=L.pg)                                  # one bucket, both nets
-            L.G.div_(dist.get_world_size(L.pg))
+            _dist.average_(L.G, L.pg)                                         # one bucket, both nets
             check(lib.satrl_ppo_reduce(H, mb, S, 2, None, None, None, ptr(L.G), ptr(self.nsq), ptr(L.steps), sp),
                   "satrl_ppo_reduce")
         check(lib.satrl_ppo_adam(H, mb, ptr(self.nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
@@ -419,15 +440,9 @@ class PPOLearner:
             return adv
         if self.pg is None:
             return (adv - adv.mean()) / (adv.std() + 1e-5)
-        import torch.distributed as dist
-        m = moments(adv)
         cnt = torch.tensor([float(adv.numel())], dtype=torch.float64, device=adv.device)
-        buf = torch.cat([m, cnt])
-        dist.all_reduce(buf, group=self.pg)
-        s, s2, n = buf[0], buf[1], buf[2]
-        mean = s / n
-        var = (s2 - n * mean * mean) / (n - 1)
-        return (adv - mean.float()) / (var.clamp_min(0).sqrt().float() + 1e-5)
+        mean, std = _dist.global_mean_std(torch.cat([moments(adv), cnt]), self.pg)
+        return (adv - mean.float()) / (std.float() + 1e-5)
 
     def update_packed(self, src, total_steps, perms=None, generator=None):
         """K epochs of minibatch steps over the packed table src [B, 32]

@@ -20,9 +20,10 @@ import time
 import numpy as np
 import torch
 
+from . import dist as _dist
 from .buffer import ReplayBuffer, RolloutBuffer
 from .env import VecSatellites
-from .ppo import PPO_continuous, PPOLearner, gae, gaussian_sample
+from .ppo import PPO_continuous, PPOLearner, gae, gaussian_sample, policy_act, policy_value
 
 
 class args_param:  # noqa: N801
@@ -203,11 +204,7 @@ class VecTrainer:
         self.other_lp = torch.zeros((self.N, 3), dtype=torch.float32, device=self.device)
         self.step_base = torch.zeros(1, dtype=torch.int64, device=self.device)   # Philox step offset (u64 bits)
         self.gen = torch.Generator(device=self.device)
-        rank = 0
-        if pg is not None:
-            import torch.distributed as dist
-            rank = dist.get_rank(pg)
-        self.gen.manual_seed(self.seed * 1000003 + rank)
+        self.gen.manual_seed(self.seed * 1000003 + _dist.rank(pg))
         self.use_graphs = use_graphs
         self.chunk = max(1, min(int(args.rollout_graph_chunk), self.T))
         self._graphs = {}
@@ -218,10 +215,10 @@ class VecTrainer:
         self.env.reset(self.flag, obs_out=self.buf.obs[0])
 
     def _broadcast_params(self):
-        import torch.distributed as dist
-        for p in list(self.pursuer.actor.parameters()) + list(self.pursuer.critic.parameters()) + \
-                list(self.evader.actor.parameters()) + list(self.evader.critic.parameters()):
-            dist.broadcast(p.data, src=0, group=self.pg)
+        # the module parameters are views into each learner's flat P
+        _dist.broadcast_([self.pursuer.P, self.evader.P], self.pg)
+        self.pursuer.sync_w2t()
+        self.evader.sync_w2t()
 
     # -- rollout ------------------------------------------------------------------
     def _policy_step(self, t):
@@ -232,13 +229,9 @@ class VecTrainer:
             pa, plp, ea, elp = buf.act[t], buf.logp[t], self.other_a, self.other_lp
         else:                                    # evader transitions are stored (CPPO_main.py:210)
             pa, plp, ea, elp = self.other_a, self.other_lp, buf.act[t], buf.logp[t]
-        with torch.no_grad():
-            mp = self.pursuer.actor(obs_t)       # both agents act on s (CPPO_main.py:122-123)
-            gaussian_sample(mp, self.pursuer.actor.log_std, 1.6, self.seed, 0, self.env_offset, t, act_out=pa,
-                            logp_out=plp, step_base=self.step_base)
-            me = self.evader.actor(obs_t)
-            gaussian_sample(me, self.evader.actor.log_std, 1.6, self.seed, 1, self.env_offset, t, act_out=ea,
-                            logp_out=elp, step_base=self.step_base)
+        # both agents act on s (CPPO_main.py:122-123): one fused launch, pursuer = agent 0
+        policy_act(self.pursuer.H, obs_t, self.pursuer.P, self.evader.P, 1.6, self.seed, self.env_offset, t,
+                   pa, plp, ea, elp, step_base=self.step_base)
         self.env.step_autoreset(pa, ea, obs_out=buf.obs[t + 1], reward_out=buf.rew[t], done_out=buf.done[t])
 
     def _chunk_graph(self, c):
@@ -281,9 +274,7 @@ class VecTrainer:
     def compute_advantages(self, chunk_steps=64):
         buf, L = self.buf, self.learner
         with torch.no_grad():
-            for t0 in range(0, self.T + 1, chunk_steps):
-                t1 = min(self.T + 1, t0 + chunk_steps)
-                buf.values[t0:t1] = L.critic(buf.obs[t0:t1].reshape(-1, 18)).reshape(t1 - t0, self.N)
+            policy_value(L.H, buf.obs.view(-1, 18), L.P, buf.values.view(-1))     # critic(s), all T+1 rows
             gae(buf.rew, buf.done, buf.values, L.gamma, L.lamda, adv_out=buf.adv, vt_out=buf.vtarget)
             adv_n = L.normalize_adv(buf.adv.reshape(-1))
             buf.pack(adv_n)
@@ -294,11 +285,7 @@ class VecTrainer:
     def finish_iteration(self):
         # next rollout starts from the current observation
         self.buf.obs[0].copy_(self.buf.obs[self.T])
-        st = self.env.stats
-        if self.pg is not None:
-            import torch.distributed as dist
-            st = st.clone()
-            dist.all_reduce(st, group=self.pg)
+        st = _dist.sum_(self.env.stats, self.pg)
         self.episodes = float(st[0].item())
         self.iteration_count += 1
         return st.cpu().numpy()

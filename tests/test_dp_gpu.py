@@ -1,0 +1,128 @@
+"""Data-parallel minibatch step on the GPU: two ranks (gloo over CUDA
+tensors, both on cuda:0) each step their half of a minibatch through the
+DP path of FusedMinibatch (reduce mode 1 -> all-reduce of G -> mode 2 ->
+Adam).  Both ranks must end bitwise identical, and equal (within the fused
+step's tolerance) to one process stepping the whole minibatch."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG_DIR
+
+pytestmark = pytest.mark.gpu
+
+H, MB, B = 64, 256, 4096
+TESTS_DIR = os.path.dirname(os.path.abspath(__file__))
+
+
+def _setup(pg, mb):
+    sys.path.insert(0, PKG_DIR)
+    from satrl.ppo import PPOLearner
+    from satrl.trainer import args_param
+    torch.manual_seed(11)
+    args = args_param(hidden_width=H, mini_batch_size=mb, batch_size=B, chkpt_dir="/tmp")
+    args.state_dim, args.action_dim, args.max_action = 18, 3, 1.6
+    L = PPOLearner(args, "pursuer", device="cuda:0", pg=pg, use_graph=False)
+    with torch.no_grad():
+        for p in list(L.actor.parameters()) + list(L.critic.parameters()):
+            p.add_(torch.randn_like(p) * 0.05)
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    src = torch.zeros((B, 32), device="cuda:0")
+    src[:, 0:18] = torch.randn((B, 18), device="cuda:0", generator=g)
+    src[:, 18:21] = torch.rand((B, 3), device="cuda:0", generator=g) * 3.2 - 1.6
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda:0", generator=g)
+    src[:, 24] = torch.randn(B, device="cuda:0", generator=g)
+    src[:, 25] = torch.randn(B, device="cuda:0", generator=g) * 5
+    idx = torch.randperm(B, device="cuda:0", generator=g)[:2 * MB]
+    L.sync_w2t()
+    return L, src, idx
+
+
+def _rank(rank, port, q):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        L, src, idx = _setup(dist.group.WORLD, MB)
+        L.stepper(MB).step(src, idx[rank * MB:(rank + 1) * MB].contiguous())
+        torch.cuda.synchronize()
+        q.put((rank, L.G.cpu().numpy(), L.P.cpu().numpy(), L.W2T.cpu().numpy()))   # by value
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_step_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (torch.from_numpy(g), torch.from_numpy(p_), torch.from_numpy(w)))
+               for r, g, p_, w in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (g0, p0, w0), (g1, p1, w1) = res[0], res[1]
+    assert torch.equal(g0, g1) and torch.equal(p0, p1) and torch.equal(w0, w1)
+    # one process, the whole 2*MB minibatch
+    L, src, idx = _setup(None, 2 * MB)
+    L.stepper(2 * MB).step(src, idx)
+    torch.cuda.synchronize()
+    gref, pref = L.G.cpu(), L.P.cpu()
+    assert (g0 - gref).abs().max().item() <= 2e-5 * gref.abs().max().item()
+    assert torch.allclose(p0, pref, rtol=1e-5, atol=2e-7)
+
+
+def _collect_rank(rank, port, q):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        sys.path.insert(0, PKG_DIR)
+        from satrl.trainer import VecTrainer, args_param
+        args = args_param(batch_size=32 * 24, mini_batch_size=128, hidden_width=64, K_epochs=1, num_envs=32,
+                          horizon=24, max_episode_steps=10, seed=1, rollout_graph_chunk=8, chkpt_dir="/tmp")
+        tr = VecTrainer(args, flag=0, d_capture=15000.0, pg=dist.group.WORLD, env_offset=rank * 32)
+        tr.collect()
+        torch.cuda.synchronize()
+        q.put((rank, tr.buf.obs.cpu().numpy(), tr.buf.rew.cpu().numpy(), tr.buf.act.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rollout_is_sharding_invariant():
+    """2 ranks x 32 envs (env ids 0-31 and 32-63) == 1 process x 64 envs, bitwise:
+    noise is keyed by global env id and parameters are broadcast from rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_collect_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (o, rw, a) for r, o, rw, a in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sys.path.insert(0, PKG_DIR)
+    from satrl.trainer import VecTrainer, args_param
+    args = args_param(batch_size=64 * 24, mini_batch_size=128, hidden_width=64, K_epochs=1, num_envs=64, horizon=24,
+                      max_episode_steps=10, seed=1, rollout_graph_chunk=8, chkpt_dir="/tmp")
+    tr = VecTrainer(args, flag=0, d_capture=15000.0)
+    tr.collect()
+    torch.cuda.synchronize()
+    obs, rew, act = tr.buf.obs.cpu().numpy(), tr.buf.rew.cpu().numpy(), tr.buf.act.cpu().numpy()
+    import numpy as np
+    for r in range(2):
+        o, rw, a = res[r]
+        assert np.array_equal(o, obs[:, 32 * r:32 * (r + 1)])
+        assert np.array_equal(rw, rew[:, 32 * r:32 * (r + 1)])
+        assert np.array_equal(a, act[:, 32 * r:32 * (r + 1)])

@@ -232,3 +232,40 @@ def test_rowpass_contiguous_rows_match_gather():
         outs.append((H1.clone(), dZ2.clone(), st.ptail.clone(), st.pw1.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_policy_act_and_value_kernels():
+    """satrl_policy_act / satrl_policy_value vs the torch modules + satrl_gaussian_sample
+    (same Philox draw); every row independent of N and of its position (bitwise)."""
+    from satrl.ppo import PPOLearner, gaussian_sample, policy_act, policy_value
+    torch.manual_seed(5)
+    args = _args(hidden_width=256)
+    Lp = PPOLearner(args, "pursuer", use_graph=False)
+    Le = PPOLearner(args, "evader", use_graph=False)
+    with torch.no_grad():
+        for L in (Lp, Le):
+            for p in list(L.actor.parameters()) + list(L.critic.parameters()):
+                p.add_(torch.randn_like(p) * 0.05)
+    N = 1000
+    g = torch.Generator(device="cuda").manual_seed(2)
+    obs = torch.randn((N, 18), device="cuda", generator=g)
+    sb = torch.tensor([7], dtype=torch.int64, device="cuda")
+    out = [torch.empty((N, 3), device="cuda") for _ in range(4)]
+    policy_act(256, obs, Lp.P, Le.P, 1.6, 123, 4096, 5, *out, step_base=sb)
+    with torch.no_grad():
+        for k, L in enumerate((Lp, Le)):
+            mean = L.actor(obs)
+            a_ref, lp_ref = gaussian_sample(mean, L.actor.log_std, 1.6, 123, k, 4096, 5 + 7)
+            assert torch.allclose(out[2 * k], a_ref, rtol=1e-5, atol=1e-5)
+            assert torch.allclose(out[2 * k + 1], lp_ref, rtol=1e-4, atol=1e-4)
+        v = torch.empty(N, device="cuda")
+        policy_value(256, obs, Lp.P, v)
+        assert torch.allclose(v, Lp.critic(obs).reshape(-1), rtol=1e-5, atol=1e-5)
+    # rows are independent of N / position: a sub-block with the matching env offset
+    sub = [torch.empty((37, 3), device="cuda") for _ in range(4)]
+    policy_act(256, obs[100:137].contiguous(), Lp.P, Le.P, 1.6, 123, 4096 + 100, 5, *sub, step_base=sb)
+    for a, b in zip(out, sub):
+        assert torch.equal(a[100:137], b)
+    v2 = torch.empty(37, device="cuda")
+    policy_value(256, obs[100:137].contiguous(), Lp.P, v2)
+    assert torch.equal(v[100:137], v2)
