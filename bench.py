@@ -194,6 +194,7 @@ def main():
             "ppo_updates_per_s": a.steps / elapsed,
             "rollout_env_steps_per_s": n_total * a.horizon / (rollout_ms * 1e-3),
             "rollout_ms": rollout_ms, "gae_ms": gae_ms, "update_ms": update_ms,
+            "env_kernel_env_steps_per_s": a.num_envs / (env_us * 1e-6),
             "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
             "episodes_finished_total": float(stats[0]),
             "roofline": {"kernel": "satrl_ppo_rowpass<256,16> (hand-written HIP, f32 MFMA 16x16x4)", "bound": "mfma",

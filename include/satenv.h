@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SATENV_ABI_VERSION 1
+#define SATENV_ABI_VERSION 2
 #define SATENV_OBS_DIM 18    /* [Pp-Ep, Pv-Ev, Pp, Pv, Ep, Ev]  environment.py:76-77 */
 #define SATENV_ACT_DIM 3
 #define SATENV_F64_PLANES 15 /* Pp[3] Pv[3] Ep[3] Ev[3] fuel_c fuel_t dis, each [num_envs] */
@@ -61,6 +61,14 @@ typedef struct satenv_params {
     int32_t flag;              /* Flag, environment.py:36                                     */
     int32_t fuel_c0_mode;      /* SATENV_NUM_* of fuel_c0 (ctor: python int)                  */
     int32_t fuel_t0_mode;
+    /* ABI 2: propagator of the relative states per 100-s step.  0 = the
+     * reference's closed-form CW STM (stm[], default); 1 = RK4 on the CW ODE
+     * x'' = 2w y' + 3w^2 x, y'' = -2w x', z'' = -w^2 z with rk4_substeps
+     * equal steps (optional mode; the reference STM's [1][4] entry is
+     * 4s/w - 3*tau, so the two differ by design).          */
+    double cw_omega;           /* w = sqrt(mu / 42164000**3), satellite_function.py:761 */
+    int32_t propagator;
+    int32_t rk4_substeps;
 } satenv_params;
 
 typedef struct satenv_env satenv_env;   /* opaque */
@@ -116,6 +124,13 @@ int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* str
 
 /* synchronises the handle's device; *status = first sticky device error (0 = none) */
 int satenv_check(satenv_env* h, int32_t* status);
+
+/* RK4 two-body + J2 propagator of 轨道外推-龙格库塔算法.py (StateEq :15-31,
+ * RungeKutta :35-41; mu = 398600 km^3/s^2, Re = 6378.137 km, J2 =
+ * 0.00108263), one lane per state: `steps` RK4 steps of size h seconds.
+ * rv_in / rv_out: SoA f64 [6][n] (x, y, z, vx, vy, vz planes, km and
+ * km/s); in place allowed.                                               */
+int satenv_rk4_j2(int64_t n, const double* rv_in, double h, int32_t steps, double* rv_out, void* stream);
 
 #ifdef __cplusplus
 }

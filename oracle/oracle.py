@@ -32,7 +32,8 @@ class OrcEnv(C.Structure):
 class OrcParams(C.Structure):
     _fields_ = [("d_capture", C.c_double), ("d_range", C.c_double), ("win_reward", C.c_double),
                 ("burn_reward", C.c_double), ("max_episode_steps", C.c_int32), ("mu", C.c_double),
-                ("R_cw", C.c_double * 3), ("V_cw", C.c_double * 3), ("stm", C.c_double * 36)]
+                ("R_cw", C.c_double * 3), ("V_cw", C.c_double * 3), ("stm", C.c_double * 36),
+                ("cw_omega", C.c_double), ("propagator", C.c_int32), ("rk4_substeps", C.c_int32)]
 
 
 def build() -> str:
@@ -68,6 +69,10 @@ def lib():
         L.orc_rollout.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcEnv), C.c_int64, C.c_int32,
                                   fp, fp, ip, dp, ip, C.c_int32]
         L.orc_rollout.restype = C.c_int
+        L.orc_rk4_j2_rhs.argtypes = [dp, dp]
+        L.orc_rk4_j2_step.argtypes = [dp, C.c_double, dp]
+        L.orc_rk4_j2_propagate.argtypes = [dp, C.c_double, C.c_int32]
+        L.orc_cw_rk4.argtypes = [dp, C.c_double, C.c_double, C.c_int32, dp]
         _lib = L
     return _lib
 
@@ -76,11 +81,35 @@ def _dp(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
-def params(d_capture=15000.0, max_episode_steps=1000, d_range=100000.0):
+def params(d_capture=15000.0, max_episode_steps=1000, d_range=100000.0, propagator=0, rk4_substeps=10):
     p = OrcParams()
     lib().orc_default_params(C.byref(p), float(d_capture), int(max_episode_steps))
     p.d_range = float(d_range)
+    p.propagator = int(propagator)
+    p.rk4_substeps = int(rk4_substeps)
     return p
+
+
+def rk4_j2(rv0, h, steps):
+    """轨道外推-龙格库塔算法.py RungeKutta applied `steps` times, batched [n][6]."""
+    rv = np.array(rv0, dtype=np.float64, copy=True).reshape(-1, 6)
+    for row in rv:
+        buf = np.ascontiguousarray(row)
+        lib().orc_rk4_j2_propagate(_dp(buf), float(h), int(steps))
+        row[:] = buf
+    return rv
+
+
+def rk4_j2_rhs(rv):
+    out = np.zeros(6)
+    lib().orc_rk4_j2_rhs(_dp(np.ascontiguousarray(rv, dtype=np.float64)), _dp(out))
+    return out
+
+
+def cw_rk4(x, w, t, nsub):
+    y = np.zeros(6)
+    lib().orc_cw_rk4(_dp(np.ascontiguousarray(x, dtype=np.float64)), float(w), float(t), int(nsub), _dp(y))
+    return y
 
 
 def stm(t=100.0):
@@ -113,8 +142,8 @@ def danger_zone(Rc, Vc, Rt, Vt, fuel, fuel_mode):
 class OracleEnv:
     """N=1 environment on the C restatement (environment.py:8-343 semantics)."""
 
-    def __init__(self, d_capture=15000.0, max_episode_steps=1000, d_range=100000.0):
-        self.p = params(d_capture, max_episode_steps, d_range)
+    def __init__(self, d_capture=15000.0, max_episode_steps=1000, d_range=100000.0, propagator=0, rk4_substeps=10):
+        self.p = params(d_capture, max_episode_steps, d_range, propagator=propagator, rk4_substeps=rk4_substeps)
         self.e = OrcEnv()
         lib().orc_env_init(C.byref(self.e))
 
@@ -152,9 +181,10 @@ class OracleEnv:
             setattr(e, k, int(st[k]))
 
 
-def rollout(n_envs, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=1, flag=0):
+def rollout(n_envs, steps, pa, ea, d_capture=15000.0, max_episode_steps=1000, nthreads=1, flag=0, propagator=0,
+            rk4_substeps=10):
     """Batched replay from reset (CPU baseline).  pa/ea: float32 [steps, n, 3]."""
-    p = params(d_capture, max_episode_steps)
+    p = params(d_capture, max_episode_steps, propagator=propagator, rk4_substeps=rk4_substeps)
     envs = (OrcEnv * n_envs)()
     for i in range(n_envs):
         lib().orc_env_init(C.byref(envs[i]))

@@ -77,6 +77,75 @@ static void stm_apply(const double M[36], const double x[6], double y[6]) {
     }
 }
 
+/* ---- 轨道外推-龙格库塔算法.py: RK4 two-body + J2 --------------------------
+ * numpy semantics: RV[k] are np.float64 scalars, so `x ** 2` etc. are
+ * pow() calls (glibc, builtins disabled in the Makefile); python-float
+ * constant prefixes are evaluated left to right as written.              */
+static const double kMuKm = 398600.0, kRe = 6378.137, kJ2 = 0.00108263;   /* :9-11 */
+
+void orc_rk4_j2_rhs(const double rv[6], double f[6]) {                   /* StateEq :15-31 */
+    const double x = rv[0], y = rv[1], z = rv[2];
+    const double r = sqrt((pow(x, 2.0) + pow(y, 2.0)) + pow(z, 2.0));
+    const double gx = (-kMuKm * x) / pow(r, 3.0);
+    const double gy = (-kMuKm * y) / pow(r, 3.0);
+    const double gz = (-kMuKm * z) / pow(r, 3.0);
+    const double c = ((-3.0 / 2.0 * kJ2) * pow(kRe, 2.0)) * kMuKm;       /* -3 / 2 * J2 * Re ** 2 * mu */
+    const double dgx = ((c * x) / pow(r, 5.0)) * (1.0 - 5.0 * pow(z / r, 2.0));
+    const double dgy = ((c * y) / pow(r, 5.0)) * (1.0 - 5.0 * pow(z / r, 2.0));
+    const double dgz = ((c * z) / pow(r, 5.0)) * (3.0 - 5.0 * pow(z / r, 2.0));
+    f[0] = rv[3]; f[1] = rv[4]; f[2] = rv[5];
+    f[3] = gx + dgx; f[4] = gy + dgy; f[5] = gz + dgz;
+}
+
+/* RungeKutta :35-41: K2 = f(r0 + h/2*K1), K3 = f(r0 + h/2*K2),
+ * K4 = f(r0 + h*K3), r1 = r0 + h/6*(K1 + 2*K2 + 2*K3 + K4) elementwise   */
+typedef void (*rhs_fn)(const double*, double*, const void*);
+static void rk4_step(rhs_fn fn, const void* ctx, const double r0[6], double h, double out[6]) {
+    double k1[6], k2[6], k3[6], k4[6], t[6];
+    const double h2 = h / 2.0, h6 = h / 6.0;
+    fn(r0, k1, ctx);
+    for (int i = 0; i < 6; ++i) t[i] = r0[i] + h2 * k1[i];
+    fn(t, k2, ctx);
+    for (int i = 0; i < 6; ++i) t[i] = r0[i] + h2 * k2[i];
+    fn(t, k3, ctx);
+    for (int i = 0; i < 6; ++i) t[i] = r0[i] + h * k3[i];
+    fn(t, k4, ctx);
+    for (int i = 0; i < 6; ++i) out[i] = r0[i] + h6 * (((k1[i] + 2.0 * k2[i]) + 2.0 * k3[i]) + k4[i]);
+}
+
+static void j2_rhs_ctx(const double* x, double* f, const void* ctx) { (void)ctx; orc_rk4_j2_rhs(x, f); }
+
+void orc_rk4_j2_step(const double rv[6], double h, double out[6]) { rk4_step(j2_rhs_ctx, NULL, rv, h, out); }
+
+void orc_rk4_j2_propagate(double rv[6], double h, int32_t steps) {
+    for (int32_t i = 0; i < steps; ++i) {
+        double y[6];
+        orc_rk4_j2_step(rv, h, y);
+        memcpy(rv, y, sizeof(y));
+    }
+}
+
+/* CW ODE right-hand side (Hill frame, metres); w = the STM's mean motion */
+static void cw_rhs_ctx(const double* x, double* f, const void* ctx) {
+    const double w = *(const double*)ctx, w2 = w * w;
+    f[0] = x[3]; f[1] = x[4]; f[2] = x[5];
+    f[3] = (2.0 * w) * x[4] + (3.0 * w2) * x[0];
+    f[4] = (-2.0 * w) * x[3];
+    f[5] = -w2 * x[2];
+}
+
+void orc_cw_rk4(const double x[6], double w, double t, int32_t nsub, double y[6]) {
+    const double h = t / (double)nsub;
+    double s[6];
+    memcpy(s, x, sizeof(s));
+    for (int32_t i = 0; i < nsub; ++i) {
+        double o[6];
+        rk4_step(cw_rhs_ctx, &w, s, h, o);
+        memcpy(s, o, sizeof(o));
+    }
+    memcpy(y, s, sizeof(s));
+}
+
 /* ---- satellite_function.py:161-255 calculate_orbital_elements ---------- */
 int orc_orbital_elements(double miu, const double R0[3], const double V0[3], double out[6]) {
     const double r_norm = norm3(R0), v_norm = norm3(V0), r_dot_v = dot3(R0, V0);
@@ -377,6 +446,9 @@ void orc_default_params(orc_params* p, double d_capture, int32_t max_episode_ste
     p->R_cw[0] = 27098000; p->R_cw[1] = 32306000; p->R_cw[2] = 0;   /* :338 */
     p->V_cw[0] = -2350; p->V_cw[1] = 1970; p->V_cw[2] = 0;          /* :339 */
     orc_stm(100, p->stm);                                            /* :121 */
+    p->cw_omega = sqrt(3.986e14 / (double)((__int128)42164000 * 42164000 * 42164000));
+    p->propagator = 0;
+    p->rk4_substeps = 10;
 }
 
 void orc_env_init(orc_env* e) {
@@ -480,8 +552,13 @@ int orc_step(const orc_params* p, orc_env* e, const float pa_in[3], const float 
     double xc[6] = {e->Pp[0], e->Pp[1], e->Pp[2], e->Pv[0], e->Pv[1], e->Pv[2]};
     double xt[6] = {e->Ep[0], e->Ep[1], e->Ep[2], e->Ev[0], e->Ev[1], e->Ev[2]};
     double yc[6], yt[6];
-    stm_apply(p->stm, xc, yc);
-    stm_apply(p->stm, xt, yt);
+    if (p->propagator == 1) {                       /* optional RK4 on the CW ODE */
+        orc_cw_rk4(xc, p->cw_omega, 100.0, p->rk4_substeps, yc);
+        orc_cw_rk4(xt, p->cw_omega, 100.0, p->rk4_substeps, yt);
+    } else {
+        stm_apply(p->stm, xc, yc);
+        stm_apply(p->stm, xt, yt);
+    }
     for (int k = 0; k < 3; ++k) {
         e->Pp[k] = yc[k]; e->Pv[k] = yc[3 + k]; e->Ep[k] = yt[k]; e->Ev[k] = yt[3 + k];
     }

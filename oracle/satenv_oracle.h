@@ -40,6 +40,9 @@ typedef struct {
     double mu;            /* 3.986e14 */
     double R_cw[3], V_cw[3];
     double stm[36];       /* row-major 6x6, satellite_function.py:766-773 */
+    double cw_omega;      /* mean motion of the STM (satellite_function.py:761) */
+    int32_t propagator;   /* 0: closed-form STM (reference), 1: RK4 on the CW ODE */
+    int32_t rk4_substeps; /* RK4 steps per 100-s env step (propagator 1)         */
 } orc_params;
 
 void orc_default_params(orc_params* p, double d_capture, int32_t max_episode_steps);
@@ -57,6 +60,17 @@ int  orc_orbital_elements(double mu, const double R[3], const double V[3], doubl
 /* fsolve(P_fai_equation, guess) of satellite_function.py:558-565 */
 double orc_solve_alpha(double mu, double dvm, double theta, double v1x, double v1y,
                        double h, double guess, int32_t* nfev);
+
+/* RK4 two-body + J2 propagator of 轨道外推-龙格库塔算法.py (km, km/s):
+ * StateEq (:15-31) and one RungeKutta step (:35-41); propagate applies
+ * `steps` steps of size h in place.                                       */
+void orc_rk4_j2_rhs(const double rv[6], double f[6]);
+void orc_rk4_j2_step(const double rv[6], double h, double out[6]);
+void orc_rk4_j2_propagate(double rv[6], double h, int32_t steps);
+/* RK4 on the Clohessy-Wiltshire ODE x'' = 2w y' + 3w^2 x, y'' = -2w x',
+ * z'' = -w^2 z over t seconds in nsub equal steps (propagator 1; the
+ * RungeKutta stage combination of the script above)                      */
+void orc_cw_rk4(const double x[6], double w, double t, int32_t nsub, double y[6]);
 
 /* batched replay for the CPU baseline: n envs x steps, actions [steps][n][3] */
 int  orc_rollout(const orc_params* p, orc_env* envs, int64_t n, int32_t steps,

@@ -333,4 +333,60 @@ __device__ __forceinline__ float norm3f(float a0, float a1, float a2) {
   return sqrtf((float)s);
 }
 
+// ---------------------------------------------------------------------------
+// RK4 propagators.  rk4_step is the RungeKutta combination of
+// 轨道外推-龙格库塔算法.py:35-41 (K2 = f(r0 + h/2 K1), K3 = f(r0 + h/2 K2),
+// K4 = f(r0 + h K3), r1 = r0 + h/6 ((K1 + 2K2) + 2K3) + K4), elementwise in
+// that order.  The stage weights stay kernel-uniform scalars (SGPRs): a
+// Butcher table in LDS would add a load per stage and change the
+// reference's rounding order.
+// ---------------------------------------------------------------------------
+template <class F>
+__device__ __forceinline__ void rk4_step(F f, const double (&r0)[6], double h, double (&out)[6]) {
+  double k1[6], k2[6], k3[6], k4[6], t[6];
+  const double h2 = h / 2.0, h6 = h / 6.0;
+  f(r0, k1);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) t[i] = r0[i] + h2 * k1[i];
+  f(t, k2);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) t[i] = r0[i] + h2 * k2[i];
+  f(t, k3);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) t[i] = r0[i] + h * k3[i];
+  f(t, k4);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) out[i] = r0[i] + h6 * (((k1[i] + 2.0 * k2[i]) + 2.0 * k3[i]) + k4[i]);
+}
+
+// StateEq (:15-31), km units; `**` on numpy scalars is pow()
+__device__ __forceinline__ void j2_rhs(const double (&rv)[6], double (&f)[6]) {
+  constexpr double kMu = 398600.0, kRe = 6378.137, kJ2 = 0.00108263;
+  const double x = rv[0], y = rv[1], z = rv[2];
+  const double r = sqrt((pow(x, 2.0) + pow(y, 2.0)) + pow(z, 2.0));
+  const double r3 = pow(r, 3.0), r5 = pow(r, 5.0), zr2 = pow(z / r, 2.0);
+  const double c = ((-3.0 / 2.0 * kJ2) * pow(kRe, 2.0)) * kMu;     // -3 / 2 * J2 * Re ** 2 * mu
+  f[0] = rv[3]; f[1] = rv[4]; f[2] = rv[5];
+  f[3] = (-kMu * x) / r3 + ((c * x) / r5) * (1.0 - 5.0 * zr2);
+  f[4] = (-kMu * y) / r3 + ((c * y) / r5) * (1.0 - 5.0 * zr2);
+  f[5] = (-kMu * z) / r3 + ((c * z) / r5) * (3.0 - 5.0 * zr2);
+}
+
+// RK4 on the CW ODE (propagator 1), t seconds in nsub steps
+__device__ __forceinline__ void cw_rk4(double (&s)[6], double w, double t, int nsub) {
+  const double w2 = w * w, h = t / (double)nsub;
+  auto f = [w, w2](const double (&x)[6], double (&o)[6]) {
+    o[0] = x[3]; o[1] = x[4]; o[2] = x[5];
+    o[3] = (2.0 * w) * x[4] + (3.0 * w2) * x[0];
+    o[4] = (-2.0 * w) * x[3];
+    o[5] = -w2 * x[2];
+  };
+  for (int i = 0; i < nsub; ++i) {
+    double o[6];
+    rk4_step(f, s, h, o);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s[k] = o[k];
+  }
+}
+
 }  // namespace satenv

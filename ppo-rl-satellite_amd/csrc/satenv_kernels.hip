@@ -29,6 +29,10 @@ constexpr int kPlaneDz = 0, kPlaneCount = 1, kPlaneBits = 2;
 
 thread_local std::string g_last_error;
 
+bool params_ok(const satenv_params* p) {
+  return (p->propagator == 0 || p->propagator == 1) && p->rk4_substeps >= 1;
+}
+
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
@@ -145,21 +149,33 @@ __global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, 
     fuel_sub(fuel_c, fcm, p_zero, (fabsf(pa[0]) + fabsf(pa[1])) + fabsf(pa[2]));   // :106
     fuel_sub(fuel_t, ftm, e_zero, (fabsf(ea[0]) + fabsf(ea[1])) + fabsf(ea[2]));   // :107
 
-    // Clohessy-Wiltshire STM (satellite_function.py:776-779), OpenBLAS dgemv_t order
-    double y[12];
+    if (prm.propagator == 1) {                                              // optional: RK4 on the CW ODE
 #pragma unroll
-    for (int craft = 0; craft < 2; ++craft) {
-      const double* x = k + 6 * craft;
+      for (int craft = 0; craft < 2; ++craft) {
+        double x[6];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const double* M = prm.stm + 6 * r;
-        const double p0 = M[0] * x[0], p1 = M[1] * x[1], p2 = M[2] * x[2];
-        const double p3 = M[3] * x[3], p4 = M[4] * x[4], p5 = M[5] * x[5];
-        y[6 * craft + r] = (((p0 + p2) + (p1 + p3)) + p4) + p5;
+        for (int c = 0; c < 6; ++c) x[c] = k[6 * craft + c];
+        cw_rk4(x, prm.cw_omega, 100.0, prm.rk4_substeps);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) k[6 * craft + c] = x[c];
       }
-    }
+    } else {
+      // Clohessy-Wiltshire STM (satellite_function.py:776-779), OpenBLAS dgemv_t order
+      double y[12];
 #pragma unroll
-    for (int c = 0; c < 12; ++c) k[c] = y[c];
+      for (int craft = 0; craft < 2; ++craft) {
+        const double* x = k + 6 * craft;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          const double* M = prm.stm + 6 * r;
+          const double p0 = M[0] * x[0], p1 = M[1] * x[1], p2 = M[2] * x[2];
+          const double p3 = M[3] * x[3], p4 = M[4] * x[4], p5 = M[5] * x[5];
+          y[6 * craft + r] = (((p0 + p2) + (p1 + p3)) + p4) + p5;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 12; ++c) k[c] = y[c];
+    }
     const double r0 = k[0] - k[6], r1 = k[1] - k[7], r2 = k[2] - k[8];
     dis = norm3(r0, r1, r2);                                                // :132
 
@@ -286,6 +302,24 @@ __global__ void __launch_bounds__(256) solve_alpha_kernel(int64_t n, const doubl
   out[i] = hybrd1(A, sin(theta), dvm, x[5]);
 }
 
+// batched RK4 two-body + J2 propagation (轨道外推-龙格库塔算法.py), SoA [6][n]
+__global__ void __launch_bounds__(256) rk4_j2_kernel(int64_t n, const double* __restrict__ in, double h,
+                                                     int32_t steps, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) s[c] = in[c * n + i];
+  for (int32_t k = 0; k < steps; ++k) {
+    double o[6];
+    rk4_step(j2_rhs, s, h, o);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) s[c] = o[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 6; ++c) out[c * n + i] = s[c];
+}
+
 }  // namespace
 
 struct satenv_env {
@@ -350,11 +384,17 @@ int satenv_default_params(satenv_params* p) {
   std::memcpy(p->init_kin, kin, sizeof(kin));
   p->max_episode_steps = 1000;   // CPPO_main.py:28
   p->flag = 0;
+  // mean motion exactly as State_transition_matrix computes it (satellite_function.py:758-761):
+  // r ** 3 is an exact python int, rounded once when it meets the float mu
+  p->cw_omega = std::sqrt(3.986e14 / (double)((__int128)42164000 * 42164000 * 42164000));
+  p->propagator = 0;
+  p->rk4_substeps = 10;
   return SATENV_OK;
 }
 
 int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, int device) {
   if (!out || !p || num_envs <= 0) return fail(SATENV_ERR_ARG, "satenv_create: bad arguments");
+  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_create: propagator must be 0/1, rk4_substeps >= 1");
   HIP_TRY(hipSetDevice(device));
   satenv_env* h = new satenv_env();
   h->n = num_envs;
@@ -398,6 +438,7 @@ int satenv_num_envs(const satenv_env* h, int64_t* n) {
 
 int satenv_set_params(satenv_env* h, const satenv_params* p) {
   if (!h || !p) return fail(SATENV_ERR_ARG, "satenv_set_params: null");
+  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_set_params: propagator must be 0/1, rk4_substeps >= 1");
   h->prm = *p;
   return SATENV_OK;
 }
@@ -467,6 +508,14 @@ int satenv_danger_zone(int64_t n, const double* states, const double* fuel, cons
 int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* stream) {
   if (n <= 0 || !in || !alpha_out) return fail(SATENV_ERR_ARG, "satenv_solve_alpha: bad args");
   hipLaunchKernelGGL(solve_alpha_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, in, alpha_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_rk4_j2(int64_t n, const double* rv_in, double h, int32_t steps, double* rv_out, void* stream) {
+  if (n <= 0 || !rv_in || !rv_out || steps < 0) return fail(SATENV_ERR_ARG, "satenv_rk4_j2: bad args");
+  hipLaunchKernelGGL(rk4_j2_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, rv_in, h, steps,
+                     rv_out);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

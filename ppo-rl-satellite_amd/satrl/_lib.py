@@ -33,7 +33,8 @@ class SatenvParams(C.Structure):
                 ("burn_reward", C.c_double), ("mu", C.c_double), ("R_cw", C.c_double * 3),
                 ("V_cw", C.c_double * 3), ("stm", C.c_double * 36), ("fuel_c0", C.c_double),
                 ("fuel_t0", C.c_double), ("init_kin", C.c_double * 12), ("max_episode_steps", C.c_int32),
-                ("flag", C.c_int32), ("fuel_c0_mode", C.c_int32), ("fuel_t0_mode", C.c_int32)]
+                ("flag", C.c_int32), ("fuel_c0_mode", C.c_int32), ("fuel_t0_mode", C.c_int32),
+                ("cw_omega", C.c_double), ("propagator", C.c_int32), ("rk4_substeps", C.c_int32)]
 
 
 class NativeError(RuntimeError):
@@ -71,6 +72,7 @@ _SIGS = {
     "satenv_check": ([_vp, C.POINTER(_i32)], C.c_int),
     "satenv_danger_zone": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_solve_alpha": ([_i64, _vp, _vp, _vp], C.c_int),
+    "satenv_rk4_j2": ([_i64, _vp, C.c_double, _i32, _vp, _vp], C.c_int),
     "satrl_gae": ([_i64, _i64, _vp, _vp, _vp, C.c_float, C.c_float, _vp, _vp, _vp], C.c_int),
     "satrl_gaussian_sample": ([_i64, _vp, _vp, C.c_float, C.c_uint64, C.c_uint32, _i64, C.c_uint64, _vp, _vp, _vp,
                                _vp],

@@ -30,7 +30,10 @@ STATE_I32 = ["dz", "episode_count", "bits"]
 def default_params(**overrides) -> _lib.SatenvParams:
     p = _lib.SatenvParams()
     check(_lib.lib().satenv_default_params(C.byref(p)), "satenv_default_params")
+    names = {f[0] for f in _lib.SatenvParams._fields_}
     for k, v in overrides.items():
+        if k not in names:
+            raise TypeError(f"unknown satenv parameter {k!r} (include/satenv.h satenv_params)")
         if k in ("R_cw", "V_cw", "stm", "init_kin"):
             getattr(p, k)[:] = [float(x) for x in np.asarray(v, dtype=np.float64).ravel()]
         else:
@@ -42,6 +45,21 @@ def stm(t: float = 100.0) -> np.ndarray:
     out = (C.c_double * 36)()
     check(_lib.lib().satenv_stm(float(t), out), "satenv_stm")
     return np.array(out[:]).reshape(6, 6)
+
+
+def rk4_j2(rv, h, steps, out=None):
+    """RK4 two-body + J2 propagation of 轨道外推-龙格库塔算法.py (km, km/s) for a
+    batch of states rv [n][6] (f64, CUDA): `steps` steps of h seconds on the
+    satenv_rk4_j2 kernel (one lane per state, SoA planes internally)."""
+    n = rv.shape[0]
+    _lib.require_cuda(rv, torch.float64, (n, 6), "rv")
+    soa = rv.t().contiguous()
+    check(_lib.lib().satenv_rk4_j2(n, ptr(soa), float(h), int(steps), ptr(soa), stream_ptr()), "satenv_rk4_j2")
+    res = soa.t()
+    if out is None:
+        return res.contiguous()
+    out.copy_(res)
+    return out
 
 
 def _num_mode(v) -> int:

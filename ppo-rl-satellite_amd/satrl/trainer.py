@@ -234,8 +234,34 @@ class VecTrainer:
                    pa, plp, ea, elp, step_base=self.step_base)
         self.env.step_autoreset(pa, ea, obs_out=buf.obs[t + 1], reward_out=buf.rew[t], done_out=buf.done[t])
 
+    def set_flag(self, flag):
+        """Switch the learning agent (Flag 0: pursuer, CPPO_main.py:94-161;
+        Flag 1: evader, CPPO_main.py:163-230).  Every env restarts under the
+        new Flag; rollout graphs are cached per Flag (they route the learner's
+        actions into the buffer)."""
+        flag = int(flag)
+        if flag not in (0, 1):
+            raise ValueError("Flag 0 (pursuer) or 1 (evader)")
+        self.flag = flag
+        self.learner = self.pursuer if flag == 0 else self.evader
+        self.env.reset(flag, obs_out=self.buf.obs[0])
+
+    def self_play(self, phases, iterations_per_phase, timers=None):
+        """Alternating training (the reference's Sign == 0 runs
+        train_pursuer_network then train_evader_network, CPPO_main.py:336-338):
+        `phases` phases of `iterations_per_phase` iterations, starting with the
+        current Flag.  Returns the per-iteration statistics."""
+        out = []
+        for k in range(int(phases)):
+            if k:
+                self.set_flag(1 - self.flag)
+            for _ in range(int(iterations_per_phase)):
+                out.append((self.flag, self.iteration(timers)))
+        return out
+
     def _chunk_graph(self, c):
-        if c not in self._graphs:
+        key = (self.flag, c)
+        if key not in self._graphs:
             t0 = c * self.chunk
             t1 = min(self.T, t0 + self.chunk)
             s = torch.cuda.Stream()
@@ -246,8 +272,8 @@ class VecTrainer:
             with torch.cuda.graph(g, pool=self._pool):
                 for t in range(t0, t1):
                     self._policy_step(t)
-            self._graphs[c] = g
-        return self._graphs[c]
+            self._graphs[key] = g
+        return self._graphs[key]
 
     def collect(self):
         """T environment steps for all N envs (CPPO_main.py:119-147)."""

@@ -37,7 +37,7 @@ def test_host_helpers_without_gpu():
     import numpy as np
     import satrl._lib as L
     from satrl import env as E
-    assert L.lib().satenv_abi_version() == 1
+    assert L.lib().satenv_abi_version() == 2
     p = E.default_params()
     assert p.max_episode_steps == 1000 and p.fuel_c0 == 320 and p.d_range == 100000
     # host STM equals the oracle's / reference's matrix bit for bit

@@ -152,3 +152,59 @@ def test_autoreset_matches_oracle(satrl_env, oracle):
     assert agree.mean() >= 0.995
     st = env.stats.cpu().numpy()
     assert st[0] == D.sum()
+
+
+# --- RK4 propagators ---------------------------------------
+def test_rk4_j2_kernel_vs_reference_vectors(satrl_env):
+    """satenv_rk4_j2 vs 轨道外推-龙格库塔算法.py (golden vectors from the
+    reference's own functions).  The device pow() is not glibc's, so the
+    bar is relative: |diff| <= 1e-12 * |state| after up to 600 steps."""
+    g = golden("rk4_j2")
+    rv0 = torch.tensor(g["rv0"], dtype=torch.float64, device="cuda")
+    worst = 0.0
+    for k, (h, n) in enumerate(zip(g["h"], g["steps"])):
+        got = satrl_env.rk4_j2(rv0, float(h), int(n)).cpu().numpy()
+        ref = g["rv"][k]
+        scale = np.abs(ref).max(axis=1, keepdims=True)
+        err = (np.abs(got - ref) / scale).max()
+        worst = max(worst, err)
+        assert err <= 1e-12, (h, n, err)
+    print(f"rk4_j2 parity: worst rel {worst:.2e}")
+
+
+def test_env_rk4_cw_mode_bitexact_vs_oracle(satrl_env, oracle):
+    """propagator 1 (RK4 on the CW ODE, 10 substeps): per-step obs and state
+    bit-exact vs the oracle (no transcendental on the propagation path),
+    reward within the env tolerance."""
+    n, T = 24, 40
+    rng = np.random.default_rng(9)
+    pa = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    env = satrl_env.VecSatellites(n, d_capture=15000.0, max_episode_steps=30, propagator=1, rk4_substeps=10)
+    env.reset(0)
+    orc = [oracle.OracleEnv(15000.0, 30, propagator=1, rk4_substeps=10) for _ in range(n)]
+    for o in orc:
+        o.reset(0)
+    cnt = np.zeros(n, dtype=np.int32)
+    obs64 = torch.empty((n, 18), dtype=torch.float64, device="cuda")
+    for t in range(T):
+        cnt += 1
+        _, r, d = env.step(torch.tensor(pa[t], device="cuda"), torch.tensor(ea[t], device="cuda"),
+                           torch.tensor(cnt, device="cuda"), obs64_out=obs64)
+        obs = obs64.cpu().numpy(); r = r.cpu().numpy(); d = d.cpu().numpy()
+        for i, o in enumerate(orc):
+            oo, orr, od = o.step(pa[t, i], ea[t, i], int(cnt[i]))
+            assert np.array_equal(obs[i], oo), (t, i)
+            assert bool(d[i]) == od
+            assert abs(r[i] - orr) <= 1e-12 * max(1.0, abs(orr)), (t, i, r[i], orr)
+            if od:
+                o.reset(0)
+                cnt[i] = 0
+        if d.any():
+            env.reset(0, mask=torch.tensor(d.astype(np.uint8), device="cuda"))
+    f, i32 = env.get_state()
+    f = f.cpu().numpy()
+    for i, o in enumerate(orc):
+        st = o.get_state()
+        assert np.array_equal(f[0:3, i], st["Pp"]) and np.array_equal(f[3:6, i], st["Pv"])
+        assert np.array_equal(f[6:9, i], st["Ep"]) and np.array_equal(f[9:12, i], st["Ev"])

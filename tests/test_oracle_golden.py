@@ -115,3 +115,51 @@ def test_stm_matches_reference_matrix(oracle):
                     [0, 0, c, 0, 0, s / omega], [3 * omega * s, 0, 0, c, 2 * s, 0],
                     [6 * omega * (c - 1), 0, 0, -2 * s, 4 * c - 3, 0], [0, 0, -omega * s, 0, 0, c]])
     assert np.array_equal(oracle.stm(100.0), ref)
+
+
+# --- RK4 propagators ---------------------------------------
+def test_rk4_j2_restatement_bitexact(oracle):
+    """轨道外推-龙格库塔算法.py StateEq / RungeKutta (functions extracted from the
+    script with ast, tests/golden/capture_rk4.py) vs the C restatement."""
+    g = golden("rk4_j2")
+    f0 = np.array([oracle.rk4_j2_rhs(x) for x in g["rv0"]])
+    assert np.array_equal(f0, g["f0"])
+    for k, (h, n) in enumerate(zip(g["h"], g["steps"])):
+        assert np.array_equal(oracle.rk4_j2(g["rv0"], h, n), g["rv"][k]), (h, n)
+
+
+def test_cw_rk4_converges_to_the_cw_solution(oracle):
+    """Known answer: RK4 on x'' = 2w y' + 3w^2 x, y'' = -2w x', z'' = -w^2 z
+    approaches the closed-form CW solution (4th order); the reference STM
+    differs from it only in its [1][4] entry (4s/w - 3*tau, :768)."""
+    w = oracle.params().cw_omega
+    t = 100.0
+    s, c, tau = np.sin(w * t), np.cos(w * t), w * t
+    exact = np.array([[4 - 3 * c, 0, 0, s / w, 2 * (1 - c) / w, 0],
+                      [6 * (s - tau), 1, 0, -2 * (1 - c) / w, 4 * s / w - 3 * t, 0],
+                      [0, 0, c, 0, 0, s / w], [3 * w * s, 0, 0, c, 2 * s, 0],
+                      [6 * w * (c - 1), 0, 0, -2 * s, 4 * c - 3, 0], [0, 0, -w * s, 0, 0, c]])
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        x = np.concatenate([rng.uniform(-2e5, 2e5, 3), rng.uniform(-5, 5, 3)])
+        e1 = np.abs(oracle.cw_rk4(x, w, t, 1) - exact @ x).max()
+        e2 = np.abs(oracle.cw_rk4(x, w, t, 2) - exact @ x).max()
+        assert np.abs(oracle.cw_rk4(x, w, t, 10) - exact @ x).max() <= 1e-9 * np.abs(x).max()
+        assert e2 < e1 / 10 or e1 < 1e-9                                 # ~2^4 per halving
+    ref = oracle.stm(100.0)
+    diff = np.abs(ref - exact) > 1e-12 * np.abs(exact).max()
+    assert diff.sum() == 1 and diff[1, 4]
+
+
+def test_env_rk4_mode_differs_from_stm_only_through_propagation(oracle):
+    """propagator 1 steps the same env logic: with identical actions the two
+    modes agree on the first step's terminal logic inputs up to the
+    propagator difference (same resets, same fuel)."""
+    n, T = 16, 30
+    rng = np.random.default_rng(1)
+    pa = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    r0, d0 = oracle.rollout(n, T, pa, ea, d_capture=15000.0, max_episode_steps=12)
+    r1, d1 = oracle.rollout(n, T, pa, ea, d_capture=15000.0, max_episode_steps=12, propagator=1, rk4_substeps=10)
+    assert np.array_equal(d0, d1)                     # timeouts at the same steps, no captures either way
+    assert not np.array_equal(r0, r1)

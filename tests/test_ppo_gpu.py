@@ -269,3 +269,30 @@ def test_policy_act_and_value_kernels():
     v2 = torch.empty(37, device="cuda")
     policy_value(256, obs[100:137].contiguous(), Lp.P, v2)
     assert torch.equal(v[100:137], v2)
+
+
+def test_self_play_alternates_learner_and_flag():
+    """VecTrainer.self_play: phase 1 trains the pursuer under Flag 0, phase 2
+    the evader under Flag 1 (every env restarted with Flag 1); the idle
+    agent's parameters do not move."""
+    from satrl.env import unpack_bits
+    from satrl.trainer import VecTrainer
+    args = _args(batch_size=64 * 16, mini_batch_size=256, hidden_width=64, K_epochs=1, num_envs=64, horizon=16,
+                 max_episode_steps=12, seed=4, rollout_graph_chunk=8, update_graph_group=2)
+    tr = VecTrainer(args, flag=0, d_capture=15000.0)
+    p0 = tr.pursuer.P.clone(); e0 = tr.evader.P.clone()
+    tr.self_play(1, 1)
+    torch.cuda.synchronize()
+    assert not torch.equal(tr.pursuer.P, p0) and torch.equal(tr.evader.P, e0)
+    p1 = tr.pursuer.P.clone()
+    tr.set_flag(1)
+    _, i32 = tr.env.get_state()
+    assert all(unpack_bits(int(b))["flag"] == 1 for b in i32[2].cpu().tolist())
+    tr.iteration()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.pursuer.P, p1) and not torch.equal(tr.evader.P, e0)
+    _, i32 = tr.env.get_state()
+    assert all(unpack_bits(int(b))["flag"] == 1 for b in i32[2].cpu().tolist())   # autoreset keeps Flag 1
+    assert tr.env.check_errors() == 0
+    stats = tr.self_play(2, 1)            # continues with Flag 1, then switches back to 0
+    assert [f for f, _ in stats] == [1, 0] and tr.learner is tr.pursuer
