@@ -170,6 +170,30 @@ def main():
     env_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
     env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
 
+    # ---- §8f propagators: RK4 two-body + J2 batch kernel, and the env step in RK4-CW mode
+    from satrl.env import VecSatellites, rk4_j2
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rv = torch.empty((a.num_envs, 6), dtype=torch.float64, device="cuda")
+    rv[:, :3] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 7000.0
+    rv[:, 3:] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 5.0
+    rk_steps = 100
+    rk4_j2(rv, 1.0, 2)
+    e0.record()
+    rk4_j2(rv, 1.0, rk_steps)
+    e1.record()
+    torch.cuda.synchronize()
+    rk4_ms = e0.elapsed_time(e1)
+    env_rk = VecSatellites(a.num_envs, d_capture=a.d_capture, max_episode_steps=1000, propagator=1, rk4_substeps=10)
+    env_rk.reset(0)
+    for _ in range(10):
+        env_rk.step_autoreset(pa, ea, obs, rew, dn)
+    e0.record()
+    for _ in range(a.kernel_iters):
+        env_rk.step_autoreset(pa, ea, obs, rew, dn)
+    e1.record()
+    torch.cuda.synchronize()
+    env_rk_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+
     rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
     update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
     gae_ms = sum(timers["gae_ms"]) / len(timers["gae_ms"])
@@ -210,6 +234,10 @@ def main():
             "roofline_update": {"bound": "mfma", "achieved": upd_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                                 "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
                                 "flop_per_transition_epoch": flop_per_transition_epoch},
+            "propagators": {"rk4_j2_state_steps_per_s": a.num_envs * rk_steps / (rk4_ms * 1e-3),
+                            "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
+                            "env_rk4_cw_avg_launch_us": env_rk_us,
+                            "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
