@@ -7,9 +7,9 @@
  * passes, clip_grad_norm_(0.5) per net and Adam(eps) per net.  Actor and
  * critic (same hidden width H, tanh) are stepped together on the same
  * minibatch rows.  Per minibatch: satrl_ppo_rowpass (everything that is
- * row-parallel, incl. the two H x H products on f32 MFMA), the dW2 weight
- * gradient as a plain library GEMM (hipBLASLt via torch.bmm, split-K),
- * satrl_ppo_reduce and satrl_ppo_adam.
+ * row-parallel, incl. the two H x H products on f32 MFMA), satrl_ppo_dw2
+ * (the dW2 weight gradient, split-K over rows), satrl_ppo_reduce and
+ * satrl_ppo_adam.
  *
  * Flat parameter / gradient / Adam-moment layout (f32, see satrl_ppo_layout):
  *   W2   [2][H][H]     fc2.weight (actor, critic)
@@ -20,8 +20,8 @@
  *   ls   [4]           actor log_std (3 used)
  *   W3c  [H]           critic fc3.weight
  *   b3c  [4]           critic fc3.bias (1 used)
- * Gradients are produced as split-K partial slabs (dW2 from the GEMM split
- * S ways, [dW1|db1] and the "tail" b2..b3c (6H+12 floats) from
+ * Gradients are produced as split-K partial slabs (dW2 from satrl_ppo_dw2
+ * split S ways, [dW1|db1] and the "tail" b2..b3c (6H+12 floats) from
  * satrl_ppo_rowpass) and summed by satrl_ppo_reduce in a fixed order, so a
  * step is bitwise deterministic.  Packed transition rows (src) are [B][32] f32:
  * s(18) a(3) logp(3) adv(1) v_target(1) pad(6).
@@ -42,19 +42,31 @@ int satrl_ppo_layout(int H, int64_t* offsets /* [SATRL_PPO_NOFF] */);
 /* number of partial slabs (32-row blocks) and of norm blocks for a minibatch of mb rows */
 int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
 
+/* `net` (rowpass, reduce, adam): -1 = actor and critic in one launch, 0 =
+ * actor only, 1 = critic only.  The two nets share nothing in a minibatch
+ * step but the rows, and a one-net call touches only that net's elements
+ * of every buffer, so the actor and critic chains may run concurrently on
+ * two streams (each with its own nsq buffer).                              */
+
+/* dW2 = dZ2^T H1 per net (the fc2 weight gradient) split-K S ways into the
+ * slabs p2 [2][S][H][H] (f32 MFMA, fixed summation order).  S must be
+ * satrl_ppo_dw2_splits(H, mb) (about one workgroup per CU, no empty split). */
+int satrl_ppo_dw2_splits(int H, int mb);
+int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream);
+
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
  * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and
- * advance steps [2] (f64); mode 3: both.  (mode 1 | all-reduce(G) | mode 2
+ * advance steps [net] (f64); mode 3: both.  (mode 1 | all-reduce(G) | mode 2
  * under data parallelism.)  Every sum has a fixed order.                  */
-int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const float* p1, const float* pt, float* G,
-                     double* nsq, double* steps, void* stream);
+int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, const float* p1, const float* pt,
+                     float* G, double* nsq, double* steps, void* stream);
 
 /* clip_grad_norm_(max_norm) per net (use_clip) + torch Adam (lerp form) per
  * net: lr [2] f32 device; bct f64 [bct_len][2] = {1 - beta1**k, sqrt(1 -
  * beta2**k)} for step k computed on the host with python-float math (as
  * torch.optim.Adam does), 1.0 past the table.                             */
-int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const double* bct, int bct_len,
+int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
                    float* P, float* M, float* V, float* W2T /* nullable: also write fc2.weight^T */,
                    void* stream);
@@ -67,7 +79,7 @@ int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const 
  * and dZ2 [2][mb][H] (inputs of the dW2 GEMM), the tail partial slabs
  * [n_head_wg][6H+12] and the [dW1 | db1] partial slabs [n_head_wg][2][H][20]
  * (n_head_wg = ceil(mb/32), satrl_ppo_sizes).                             */
-int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const float* P, const float* W2T,
+int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const float* W2T,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream);
 

@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
                                                       const float* __restrict__ W2T, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
-                                                      float* __restrict__ pw1) {
+                                                      float* __restrict__ pw1, int net_sel) {
   constexpr int R = kRows, RT = R / 16, LDA = H + 4, CT = H / 16 / NW;
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW> sm;
@@ -327,7 +327,9 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   __shared__ float dz3s[R][4];
   __shared__ float lsp[R][4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
-  const int net = blockIdx.x & 1, rb = blockIdx.x >> 1, n0 = w * (H / NW);
+  // net_sel < 0: both nets, blockIdx = (row block, net); else that net only
+  const int net = net_sel < 0 ? (int)(blockIdx.x & 1) : net_sel;
+  const int rb = net_sel < 0 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, n0 = w * (H / NW);
   const int r0 = rb * R;
   auto& S = sm.S;
   PHASE_PROBE(0);
@@ -531,18 +533,104 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
 }
 
 // ---------------------------------------------------------------------------
+// dW2 = dZ2^T H1 per net (fc2.weight.grad), split-K over the minibatch rows.
+// Workgroup (net, 64x64 output tile, split s) sums rows [s*KR, (s+1)*KR) of
+// its tile into slab p2[net][s] with f32 MFMA 16x16x4 (4 waves; wave w owns
+// tile rows 16w.., all four 16-column tiles).  32-row chunks of dZ2 and H1
+// stream global -> LDS by LDS-DMA (global_load_lds_dwordx4) through a ring of
+// kDwD slots with kDwD-1 chunks in flight: counted vmcnt + raw s_barrier, no
+// VGPR staging.  The LDS image is XOR-swizzled on the source address (16-float
+// groups ^ row&3) so the MFMA operand reads are bank-conflict free.  Block
+// b -> split b % S: with S = 8 every split's 16 tiles share one XCD's L2.
+// Every sum has a fixed order.
+// ---------------------------------------------------------------------------
+constexpr int kDwKC = 32, kDwD = 4;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int H>
+__global__ void __launch_bounds__(256) dw2_kernel(int mb, int S, int KR, int net_sel, const float* __restrict__ H1g,
+                                                  const float* __restrict__ dZ2g, float* __restrict__ p2) {
+  constexpr int TT = H / 64;
+  __shared__ __attribute__((aligned(16))) float ring[kDwD][2][kDwKC][64];   // [slot][dZ2 | H1][row][64 cols]
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, li = l & 15, lg = l >> 4;
+  const int b = blockIdx.x, s = b % S, tile = (b / S) % (TT * TT);
+  const int net = net_sel < 0 ? b / (S * TT * TT) : net_sel;
+  const int n0 = (tile / TT) * 64, m0 = (tile % TT) * 64;
+  const int r_begin = s * KR, nvalid = min(mb, r_begin + KR) - r_begin;
+  const float* Z = dZ2g + (int64_t)net * mb * H;
+  const float* Y = H1g + (int64_t)net * mb * H;
+  const int nchunks = KR / kDwKC;
+  // wave w stages rows 8w..8w+7 of a chunk: two 1-KB pieces (4 rows x 64 floats) per operand
+  auto stage = [&](int c) {
+    const int slot = c % kDwD;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = 8 * w + 4 * u + (l >> 4), c4 = (l & 15) ^ (4 * (row & 3));   // swizzled source
+      const int r = min(r_begin + c * kDwKC + row, mb - 1);                       // rows past the end: masked below
+      __builtin_amdgcn_global_load_lds(Z + (int64_t)r * H + n0 + 4 * c4, (lds_void_t*)&ring[slot][0][8 * w + 4 * u][0],
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Y + (int64_t)r * H + m0 + 4 * c4, (lds_void_t*)&ring[slot][1][8 * w + 4 * u][0],
+                                       16, 0, 0);
+    }
+  };
+  f4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < kDwD - 1; ++c) stage(c < nchunks ? c : nchunks - 1);
+  for (int c = 0; c < nchunks; ++c) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDwD - 2) * 4) : "memory");   // this wave's part of chunk c landed
+    __builtin_amdgcn_s_barrier();                                            // every wave's part; slot c-1 free
+    stage(c + kDwD - 1 < nchunks ? c + kDwD - 1 : nchunks - 1);             // (tail: a harmless reload)
+    const int slot = c % kDwD, rows = nvalid - c * kDwKC;                    // rows >= `rows` are not ours
+    // all of the chunk's operands first (40 ds_reads in flight), then the MFMAs
+    float a[kDwKC / 4], bm[kDwKC / 4][4];
+#pragma unroll
+    for (int ks = 0; ks < kDwKC / 4; ++ks) {
+      // A[n][k] = dZ2[row][n 16w+li], B[k][m] = H1[row][m 16j+li], row = 4ks+lg (row & 3 == lg)
+      const int row = 4 * ks + lg;
+      a[ks] = ring[slot][0][row][16 * (w ^ lg) + li];
+      if (row >= rows) a[ks] = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bm[ks][j] = ring[slot][1][row][16 * (j ^ lg) + li];
+    }
+#pragma unroll
+    for (int ks = 0; ks < kDwKC / 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = mfma4(a[ks], bm[ks][j], acc[j]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // acc[j][q] = dW2[n0 + 16w + 4lg + q][m0 + 16j + li]
+  float* out = p2 + ((int64_t)net * S + s) * H * H;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(int64_t)(n0 + 16 * w + 4 * lg + q) * H + m0 + 16 * j + li] = acc[j][q];
+}
+
+int dw2_splits(int H, int mb, int net) {
+  const int tiles = (net < 0 ? 2 : 1) * (H / 64) * (H / 64);
+  int S = 256 / tiles;
+  const int maxS = (mb + kDwKC - 1) / kDwKC;
+  if (S > maxS) S = maxS;
+  if (S < 1) S = 1;
+  const int KR = ((mb + S - 1) / S + kDwKC - 1) / kDwKC * kDwKC;
+  return (mb + KR - 1) / KR;                                     // no empty split
+}
+
+// ---------------------------------------------------------------------------
 // reduce: sums the three partial-slab families into G (fixed order) and/or
 // writes per-block squared norms per net (f64).  Everything moves as float4
 // (every region boundary and slab stride is a multiple of 4 floats, and a
 // float4 never straddles the actor/critic boundary).  Block ranges:
-//   [0, nb2)          W2 region: one float4 per thread, S split-K slabs [2][S][H][H]
+//   [0, nb2)          W2 region: 64 float4 columns x 4 chunks, S split-K slabs [2][S][H][H]
 //   [nb2, nb2+nb1)    W1 region: 32 float4 columns x 8 chunks, nw1 slabs [nw1][2][H][20]
 //   [nb2+nb1, ...)    tail: 8 float4 columns x 32 chunks, nwg slabs [nwg][6H+12]
 // A chunk sums slabs c, c+CH, ... (all loads independent: one or two
 // latency rounds), then chunk 0 adds the CH partials in order.
 // ---------------------------------------------------------------------------
-struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg; };
-constexpr int kRedCH1 = 8, kRedCHt = 32;
+struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
+constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -596,25 +684,27 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
   const int64_t HH4 = (int64_t)H * H / 4;
   float4* G4 = reinterpret_cast<float4*>(G);
   int b = blockIdx.x;
-  if (b < g.nb2) {                                                // W2: [2][S] slabs of H*H
-    const int64_t e4 = (int64_t)b * 256 + t;
-    if (e4 < 2 * HH4) {
-      const int net = e4 >= HH4;
-      float4 v;
-      if (mode & 1) {
-        const float4* q = reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4 + (e4 - net * HH4);
-        v = q[0];
-        for (int s2 = 1; s2 < g.S; ++s2) v = f4add(v, q[(int64_t)s2 * HH4]);
-        G4[e4] = v;
-      } else {
-        v = G4[e4];
-      }
+  if (b < g.nb2) {                                                // W2: [2][S] split-K slabs of H*H
+    constexpr int EB = 256 / kRedCH2;
+    const int64_t col = (g.net > 0 ? HH4 : 0) + (int64_t)b * EB + (t % EB);
+    const bool valid = col < (g.net < 0 ? 2 : g.net + 1) * HH4, lead = t < EB;
+    const int net = col >= HH4;                                   // EB divides HH4: one net per block
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (mode & 1) {
+      v = chunk_sum4<kRedCH2>(reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4, HH4, g.S,
+                              col - net * HH4, valid, red);
+      if (lead && valid) G4[col] = v;
+    } else if (lead && valid) {
+      v = G4[col];
+    }
+    if (lead && valid) {
       if (net) sc += sq4(v); else sa += sq4(v);
     }
   } else if ((b -= g.nb2) < g.nb1) {                             // W1: [nw1] slabs of 2*H*20
     constexpr int EB = 256 / kRedCH1;
-    const int64_t n4 = 2LL * H * 20 / 4, col = (int64_t)b * EB + (t % EB);
-    const bool valid = col < n4, lead = t < EB;
+    const int64_t n4 = 2LL * H * 20 / 4, h4 = (int64_t)H * 20 / 4;
+    const int64_t col = (g.net > 0 ? h4 : 0) + (int64_t)b * EB + (t % EB);
+    const bool valid = col < (g.net == 0 ? h4 : n4), lead = t < EB;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCH1>(reinterpret_cast<const float4*>(p1), n4, g.nw1, col, valid, red);
@@ -629,7 +719,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
     b -= g.nb1;
     constexpr int EB = 256 / kRedCHt;
     const int64_t n4 = L.tail / 4, col = (int64_t)b * EB + (t % EB);
-    const bool valid = col < n4, lead = t < EB;
+    const bool valid = col < n4 && (g.net < 0 || net_of(L, L.b2 + col * 4, H) == g.net), lead = t < EB;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCHt>(reinterpret_cast<const float4*>(pt), n4, g.nwg, col, valid, red);
@@ -646,7 +736,10 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
     if (t == 0) {
       nsq[2 * blockIdx.x] = sa;
       nsq[2 * blockIdx.x + 1] = sc;
-      if (blockIdx.x == 0) { steps[0] += 1.0; steps[1] += 1.0; }
+      if (blockIdx.x == 0) {
+        if (g.net != 1) steps[0] += 1.0;
+        if (g.net != 0) steps[1] += 1.0;
+      }
     }
   }
 }
@@ -673,7 +766,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
                                                    float beta2, float eps, float max_norm, int use_clip,
                                                    const float* __restrict__ G, float* __restrict__ P,
                                                    float* __restrict__ M, float* __restrict__ V,
-                                                   float* __restrict__ W2T) {
+                                                   float* __restrict__ W2T, int net_sel) {
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float cst[2][3];                                      // coef, step_size, bc2_sqrt per net
@@ -682,7 +775,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   double a = 0.0, c = 0.0;
   for (int k = t; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
   block_sum2(a, c, sh);
-  if (t < 2) {
+  if (t < 2 && (net_sel < 0 || net_sel == t)) {
     const double nn = t == 0 ? a : c;
     const float nrm = (float)sqrt(nn);
     cst[t][0] = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
@@ -697,7 +790,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   __syncthreads();
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
-  const int ntc = H / 32, nbw = 2 * ntc * ntc;
+  const int ntc = H / 32, nbw = (net_sel < 0 ? 2 : 1) * ntc * ntc;
   const float4* G4 = reinterpret_cast<const float4*>(G);
   float4* P4 = reinterpret_cast<float4*>(P);
   float4* M4 = reinterpret_cast<float4*>(M);
@@ -706,13 +799,14 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   int net;
   if ((int)blockIdx.x < nbw) {
     const int tb = blockIdx.x % (ntc * ntc);
-    net = blockIdx.x / (ntc * ntc);
+    net = net_sel < 0 ? (int)(blockIdx.x / (ntc * ntc)) : net_sel;
     const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
     e4 = ((int64_t)net * H * H + (int64_t)n * H + k) / 4;
   } else {
     e4 = L.W1 / 4 + (int64_t)(blockIdx.x - nbw) * 256 + t;
     if (e4 >= L.total / 4) return;                                 // (no barrier follows in this branch)
     net = net_of(L, e4 * 4, H);
+    if (net_sel >= 0 && net != net_sel) return;
   }
   const float4 g = G4[e4];
   float4 m = M4[e4], v = V4[e4];
@@ -730,7 +824,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
     const int nl = t >> 3, kl = (t & 7) * 4;
     tile[nl][kl] = pn.x; tile[nl][kl + 1] = pn.y; tile[nl][kl + 2] = pn.z; tile[nl][kl + 3] = pn.w;
     __syncthreads();
-    const int tb = blockIdx.x % (ntc * ntc);
+    const int tb = blockIdx.x % (ntc * ntc);                       // (net as above)
     const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
     // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
     const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
@@ -740,21 +834,23 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
 
 int n_head_wg(int mb) { return (mb + kRows - 1) / kRows; }
 int n_w1_wg(int mb) { return n_head_wg(mb); }
-RedGeom geom(int H, int mb, int S) {
+RedGeom geom(int H, int mb, int S, int net = -1) {
   const Layout L = layout(H);
+  const int nn = net < 0 ? 2 : 1;                                  // nets covered
   RedGeom g;
-  g.nb2 = (int)((L.W1 / 4 + 255) / 256);
-  g.nb1 = (int)((2LL * H * 20 / 4 + (256 / kRedCH1) - 1) / (256 / kRedCH1));
+  g.nb2 = (int)((nn * (int64_t)H * H / 4 + (256 / kRedCH2) - 1) / (256 / kRedCH2));
+  g.nb1 = (int)((nn * (int64_t)H * 20 / 4 + (256 / kRedCH1) - 1) / (256 / kRedCH1));
   g.nbt = (int)((L.tail / 4 + (256 / kRedCHt) - 1) / (256 / kRedCHt));
   g.S = S;
   g.nw1 = n_w1_wg(mb);
   g.nwg = n_head_wg(mb);
+  g.net = net;
   return g;
 }
 int n_blocks(const RedGeom& g) { return g.nb2 + g.nb1 + g.nbt; }
-int n_adam_blocks(int H) {
+int n_adam_blocks(int H, int net) {
   const Layout L = layout(H);
-  return 2 * (H / 32) * (H / 32) + (int)(((L.total - L.W1) / 4 + 255) / 256);
+  return (net < 0 ? 2 : 1) * (H / 32) * (H / 32) + (int)(((L.total - L.W1) / 4 + 255) / 256);
 }
 
 bool valid_h(int H) { return H == 64 || H == 128 || H == 256; }
@@ -787,26 +883,27 @@ int satrl_ppo_layout(int H, int64_t* off) {
 int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
   if (!valid_h(H) || mb <= 0) return -1;
   if (nwg) *nwg = n_head_wg(mb);
-  if (nblk) *nblk = n_blocks(geom(H, mb, 1));
+  if (nblk) *nblk = n_blocks(geom(H, mb, 1, -1));                 // >= the per-net counts
   return 0;
 }
 
-int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const float* P, const float* W2T,
+int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const float* W2T,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream) {
-  if (!valid_h(H) || mb <= 0 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1) return -1;
-  dim3 g(2 * n_head_wg(mb));                       // (row block, net) pairs
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1)
+    return -1;
+  dim3 g((net < 0 ? 2 : 1) * n_head_wg(mb));      // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
   if (H == 64)
     hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
-                       max_action, H1, dZ2, ptail, pw1);
+                       max_action, H1, dZ2, ptail, pw1, net);
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
-                       max_action, H1, dZ2, ptail, pw1);
+                       max_action, H1, dZ2, ptail, pw1, net);
   else
     hipLaunchKernelGGL((rowpass_kernel<256, 16>), g, dim3(1024), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
-                       max_action, H1, dZ2, ptail, pw1);
+                       max_action, H1, dZ2, ptail, pw1, net);
   LAUNCH_CHECK();
   return 0;
 }
@@ -815,25 +912,48 @@ int satrl_ppo_rowpass(int H, int mb, const float* src, const int64_t* idx, const
 
 
 
-int satrl_ppo_reduce(int H, int mb, int S, int mode, const float* p2, const float* p1, const float* pt, float* G,
-                     double* nsq, double* steps, void* stream) {
-  if (!valid_h(H) || mb <= 0 || S < 1 || mode < 1 || mode > 3 || !G) return -1;
+int satrl_ppo_dw2_splits(int H, int mb) {
+  if (!valid_h(H) || mb <= 0) return -1;
+  return dw2_splits(H, mb, -1);
+}
+
+int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream) {
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || S < 1 || !H1 || !dZ2 || !p2) return -1;
+  const int KR = ((mb + S - 1) / S + kDwKC - 1) / kDwKC * kDwKC;
+  if ((int64_t)KR * (S - 1) >= mb) return -1;                    // an empty split: use satrl_ppo_dw2_splits
+  const dim3 g((unsigned)((net < 0 ? 2 : 1) * (H / 64) * (H / 64) * S));
+  hipStream_t st = (hipStream_t)stream;
+  if (H == 64)
+    hipLaunchKernelGGL(dw2_kernel<64>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
+  else if (H == 128)
+    hipLaunchKernelGGL(dw2_kernel<128>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
+  else
+    hipLaunchKernelGGL(dw2_kernel<256>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, const float* p1, const float* pt,
+                     float* G, double* nsq, double* steps, void* stream) {
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || S < 1 || mode < 1 || mode > 3 || !G) return -1;
   if ((mode & 1) && (!p2 || !p1 || !pt)) return -1;
   if ((mode & 2) && (!nsq || !steps)) return -1;
-  const RedGeom g = geom(H, mb, S);
+  const RedGeom g = geom(H, mb, S, net);
   hipLaunchKernelGGL(reduce_kernel, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1, pt, G,
                      nsq, steps);
   LAUNCH_CHECK();
   return 0;
 }
 
-int satrl_ppo_adam(int H, int mb, const double* nsq, const double* steps, const double* bct, int bct_len,
+int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
                    float* P, float* M, float* V, float* W2T, void* stream) {
-  if (!valid_h(H) || mb <= 0 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P || !M || !V) return -1;
-  const int nblk = n_blocks(geom(H, mb, 1));
-  hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq, steps,
-                     bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T);
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P ||
+      !M || !V)
+    return -1;
+  const int nblk = n_blocks(geom(H, mb, 1, net));
+  hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq,
+                     steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T, net);
   LAUNCH_CHECK();
   return 0;
 }

@@ -81,11 +81,13 @@ _SIGS = {
     "satrl_last_error": ([], C.c_char_p),
     "satrl_ppo_layout": ([C.c_int, C.POINTER(_i64)], C.c_int),
     "satrl_ppo_sizes": ([C.c_int, C.c_int, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
-    "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_adam": ([C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float, C.c_float,
-                        C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_rowpass": ([C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp, _vp, _vp,
-                           _vp], C.c_int),
+    "satrl_ppo_dw2_splits": ([C.c_int, C.c_int], C.c_int),
+    "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
+                        C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_rowpass": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp,
+                           _vp, _vp, _vp], C.c_int),
     "satrl_policy_act": ([C.c_int, _i64, _vp, _vp, _vp, C.c_float, C.c_uint64, _i64, C.c_uint64, _vp, _vp, _vp, _vp,
                           _vp, _vp], C.c_int),
     "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),

@@ -177,19 +177,31 @@ def ppo_layout(H):
 
 
 class FusedMinibatch:
-    """One PPO minibatch step for actor + critic on shared rows, 4 launches:
-    satrl_ppo_rowpass (gather, both MLPs forward/backward on f32 MFMA, losses),
-    the dW2 weight-gradient GEMM (hipBLASLt via torch.bmm, split-K S ways),
-    satrl_ppo_reduce and satrl_ppo_adam.  Captured into hipGraphs of
-    ``group`` consecutive minibatches, replayed over [group, mb] blocks of a
-    device permutation."""
+    """One PPO minibatch step for actor + critic on shared rows:
+    satrl_ppo_rowpass (gather, MLP forward/backward on f32 MFMA, losses),
+    satrl_ppo_dw2 (the dW2 weight gradient, split-K), satrl_ppo_reduce and
+    satrl_ppo_adam, both nets per launch.  The actor and
+    critic steps share nothing but the rows (ppo_continuous.py:216-239 runs
+    two independent optimisers); with ``split_chains`` they run as two
+    per-net chains on two streams (the critic on a side stream, fork/join per
+    group).  Under data parallelism both nets' gradients travel in one
+    all-reduce.  Groups of ``group`` minibatches are captured into a hipGraph
+    and replayed over [group, mb] blocks of a device permutation."""
 
-    def __init__(self, learner, mb, group, use_graph=True, splitk=4):
+    def __init__(self, learner, mb, group, use_graph=True, split_chains=False):
         self.L = learner
         self.mb = int(mb)
         self.group = int(group)
         self.use_graph = use_graph
-        self.S = splitk if self.mb % splitk == 0 else 1
+        # dW2: the hand-written split-K kernel for H <= 128 (hipBLASLt picks
+        # K-serial tiles there: 12.5 us vs 3 us at H = 64); at H = 256 the
+        # library GEMM (torch.bmm -> hipBLASLt, split-K 4) measured 13 us vs
+        # 15 us for satrl_ppo_dw2, so it stays a plain library GEMM
+        self.lib_gemm = learner.H >= 256
+        self.S = self.splits(learner.H, self.mb)
+        # two concurrent per-net chains: measured no faster than one fused chain at
+        # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
+        self.split = bool(split_chains) and learner.pg is None
         H, dev = learner.H, learner.device
         nwg, nblk = C.c_int64(), C.c_int64()
         check(_lib.lib().satrl_ppo_sizes(H, self.mb, C.byref(nwg), C.byref(nblk)), "satrl_ppo_sizes")
@@ -200,77 +212,118 @@ class FusedMinibatch:
         self.ptail = torch.empty(self.nwg * (6 * H + 12), **f32)
         self.pw1 = torch.empty(self.nwg * 2 * H * 20, **f32)
         self.p2 = torch.empty(2 * self.S * H * H, **f32)
-        self.nsq = torch.zeros(2 * self.nblk, dtype=torch.float64, device=dev)
+        self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
         # group (one index_select) so rowpass reads them without an index hop
         self.stage = torch.empty((self.group * self.mb, 32), **f32)
+        self.side = torch.cuda.Stream(device=dev) if self.split and torch.cuda.is_available() else None
         self.graph = None
         self._src_ptr = None
 
-    def rowpass(self, src, idx, mb=None):
+    def rowpass(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass alone (a pure function of src, idx and the
         parameters: bench.py times it on its own for the roofline).  idx None:
-        rows 0..mb-1 of src."""
+        rows 0..mb-1 of src.  net -1: both nets in one launch."""
         L = self.L
         H = L.H
         mb = self.mb if mb is None else int(mb)
         n = 2 * mb * H
         H1, dZ2 = self.H1[:n], self.dZ2[:n]
-        check(_lib.lib().satrl_ppo_rowpass(H, mb, ptr(src), None if idx is None else ptr(idx), ptr(L.P), ptr(L.W2T),
-                                           float(L.epsilon),
-                                           float(L.entropy_coef), float(L.max_action), ptr(H1), ptr(dZ2),
-                                           ptr(self.ptail), ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass")
+        check(_lib.lib().satrl_ppo_rowpass(H, mb, int(net), ptr(src), None if idx is None else ptr(idx), ptr(L.P),
+                                           ptr(L.W2T), float(L.epsilon), float(L.entropy_coef), float(L.max_action),
+                                           ptr(H1), ptr(dZ2), ptr(self.ptail), ptr(self.pw1), stream_ptr()),
+                  "satrl_ppo_rowpass")
         return H1, dZ2
 
     @staticmethod
     def rowpass_flops(H, mb):
-        """Algorithmic FLOPs of one rowpass launch (DESIGN.md "Roofline"):
-        per row and net fc1 forward + [dW1|db1] (2*18*H + H each), fc2 forward
-        and dH1 (2*H*H each); output layers forward/backward (actor 3 outputs
-        x 3 products, critic 1 x 3)."""
+        """Algorithmic FLOPs of one rowpass launch over both nets (DESIGN.md
+        "Roofline"): per row and net fc1 forward + [dW1|db1] (2*18*H + H
+        each), fc2 forward and dH1 (2*H*H each); output layers forward /
+        backward (actor 3 outputs x 3 products, critic 1 x 3)."""
         per_row = 2 * (2 * (2 * 18 * H + H) + 2 * (2 * H * H)) + 2 * 3 * 3 * H + 2 * 1 * 3 * H
         return per_row * mb
 
-    def step(self, src, idx, mb=None):
+    def splits(self, H, mb):
+        """split-K ways of the dW2 product for a minibatch of mb rows."""
+        if self.lib_gemm:
+            return 4 if mb % 4 == 0 else 1
+        S = _lib.lib().satrl_ppo_dw2_splits(int(H), int(mb))
+        if S < 1:
+            raise _lib.NativeError(f"satrl_ppo_dw2_splits({H}, {mb}) failed")
+        return S
+
+    def _dw2(self, H1, dZ2, mb, S, net):
+        """dW2 = dZ2^T @ H1 split-K S ways into the slabs p2 [2][S][H][H]."""
+        H = self.L.H
+        if not self.lib_gemm:
+            check(_lib.lib().satrl_ppo_dw2(H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), stream_ptr()),
+                  "satrl_ppo_dw2")
+            return
+        lo, hi = (0, 2) if net < 0 else (net, net + 1)
+        nb = hi - lo
+        z = dZ2[lo * mb * H:hi * mb * H].view(nb * S, mb // S, H)
+        y = H1[lo * mb * H:hi * mb * H].view(nb * S, mb // S, H)
+        torch.bmm(z.transpose(1, 2), y, out=self.p2[lo * S * H * H:hi * S * H * H].view(nb * S, H, H))
+
+    def _net_step(self, src, idx, mb, net):
         L = self.L
         H = L.H
-        mb = self.mb if mb is None else int(mb)
-        S = self.S if mb % self.S == 0 else 1
+        S = self.S if mb == self.mb else self.splits(H, mb)
         lib, sp = _lib.lib(), stream_ptr()
-        H1, dZ2 = self.rowpass(src, idx, mb)
-        # dW2 = dZ2^T @ H1 per net, split-K S ways -> slabs [2][S][H][H]
-        p2v = self.p2[:2 * S * H * H].view(2 * S, H, H)
-        torch.bmm(dZ2.view(2 * S, mb // S, H).transpose(1, 2), H1.view(2 * S, mb // S, H), out=p2v)
+        nsq = self.nsq[max(net, 0)]
+        H1, dZ2 = self.rowpass(src, idx, mb, net)
+        self._dw2(H1, dZ2, mb, S, net)
         if L.pg is None:
-            check(lib.satrl_ppo_reduce(H, mb, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
-                                       ptr(self.nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
+                                       ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
-            check(lib.satrl_ppo_reduce(H, mb, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G), None,
-                                       None, sp), "satrl_ppo_reduce")
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
+                                       None, None, sp), "satrl_ppo_reduce")
             _dist.average_(L.G, L.pg)                                         # one bucket, both nets
-            check(lib.satrl_ppo_reduce(H, mb, S, 2, None, None, None, ptr(L.G), ptr(self.nsq), ptr(L.steps), sp),
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 2, None, None, None, ptr(L.G), ptr(nsq), ptr(L.steps), sp),
                   "satrl_ppo_reduce")
-        check(lib.satrl_ppo_adam(H, mb, ptr(self.nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
+        check(lib.satrl_ppo_adam(H, mb, net, ptr(nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
                                  float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
                                  ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
 
+    def _chains(self, fn):
+        """fn(net) for the actor on the current stream and the critic on the
+        side stream (fork/join), or fn(-1) once when not split."""
+        if not self.split:
+            fn(-1)
+            return
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        fn(0)
+        with torch.cuda.stream(self.side):
+            fn(1)
+        cur.wait_stream(self.side)
+
+    def step(self, src, idx, mb=None):
+        mb = self.mb if mb is None else int(mb)
+        self._chains(lambda net: self._net_step(src, idx, mb, net))
+
     def _group(self, src, ng):
         """ng minibatches whose indices are in self.idx[:ng]: one gather of
-        their rows into self.stage, then ng steps on contiguous rows."""
+        their rows into self.stage, then ng steps per chain on contiguous rows."""
         mb = self.mb
         torch.index_select(src, 0, self.idx[:ng].view(-1), out=self.stage[:ng * mb])
-        for k in range(ng):
-            self.step(self.stage[k * mb:(k + 1) * mb], None)
+
+        def chain(net):
+            for k in range(ng):
+                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
+        self._chains(chain)
 
     def _capture(self, src):
-        # hipBLASLt sets up a GEMM shape on its first call, which is not
-        # capture-safe: run the dW2 product once eagerly into the scratch slabs
-        H, mb, S = self.L.H, self.mb, self.S
-        n = 2 * mb * H
-        torch.bmm(self.dZ2[:n].view(2 * S, mb // S, H).transpose(1, 2), self.H1[:n].view(2 * S, mb // S, H),
-                  out=self.p2.view(2 * S, H, H))
-        torch.cuda.synchronize()
+        if self.lib_gemm:
+            # hipBLASLt sets up a GEMM shape on its first call per stream, which is
+            # not capture-safe: run the dW2 products once eagerly into the scratch slabs
+            for net in ((0, 1) if self.split else (-1,)):
+                with torch.cuda.stream(self.side if net == 1 else torch.cuda.current_stream()):
+                    self._dw2(self.H1, self.dZ2, self.mb, self.S, net)
+            torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)

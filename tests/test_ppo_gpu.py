@@ -140,8 +140,8 @@ def test_update_matches_reference():
     assert abs(la - u["lr_after"][0]) <= 1e-6 * u["lr_after"][0] and abs(lc - u["lr_after"][1]) <= 1e-6 * u["lr_after"][1]
 
 
-@pytest.mark.parametrize("H", [64, 256])
-def test_fused_step_vs_torch_autograd(H):
+@pytest.mark.parametrize("H,split", [(64, False), (256, False), (256, True)])
+def test_fused_step_vs_torch_autograd(H, split):
     """satrl_ppo_rowpass (f32 MFMA) + hipBLASLt dW2 + reduce + Adam vs plain torch fp32 autograd +
     clip_grad_norm_ + torch.optim.Adam on the same minibatch."""
     from satrl.ppo import PPOLearner
@@ -163,7 +163,8 @@ def test_fused_step_vs_torch_autograd(H):
     idx = torch.randperm(B, device="cuda", generator=g)[:mb]
     grads, params = reference_step(L.actor, L.critic, src[idx], lr=args.lr_a)
     L.sync_w2t()
-    st = L.stepper(mb)
+    from satrl.ppo import FusedMinibatch
+    st = FusedMinibatch(L, mb, 1, use_graph=False, split_chains=split)
     st.step(src, idx)
     torch.cuda.synchronize()
     G = L.flat_views(L.G)
@@ -296,3 +297,22 @@ def test_self_play_alternates_learner_and_flag():
     assert tr.env.check_errors() == 0
     stats = tr.self_play(2, 1)            # continues with Flag 1, then switches back to 0
     assert [f for f, _ in stats] == [1, 0] and tr.learner is tr.pursuer
+
+
+@pytest.mark.parametrize("H,mb", [(64, 4096), (128, 1000), (256, 4096), (256, 777)])
+def test_dw2_kernel_vs_torch(H, mb):
+    """satrl_ppo_dw2 (split-K LDS-DMA MFMA kernel) summed over its slabs ==
+    dZ2^T @ H1 per net in fp64, within f32 accumulation error."""
+    from satrl import _lib
+    g = torch.Generator(device="cuda").manual_seed(H + mb)
+    H1 = torch.randn(2 * mb * H, device="cuda", generator=g)
+    dZ2 = torch.randn(2 * mb * H, device="cuda", generator=g)
+    S = _lib.lib().satrl_ppo_dw2_splits(H, mb)
+    assert S >= 1
+    p2 = torch.full((2 * S * H * H,), float("nan"), device="cuda")
+    _lib.check(_lib.lib().satrl_ppo_dw2(H, mb, -1, S, _lib.ptr(H1), _lib.ptr(dZ2), _lib.ptr(p2), _lib.stream_ptr()),
+               "satrl_ppo_dw2")
+    got = p2.view(2, S, H, H).double().sum(1)
+    ref = torch.bmm(dZ2.view(2, mb, H).double().transpose(1, 2), H1.view(2, mb, H).double())
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item() + 1e-4, err
