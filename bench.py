@@ -79,6 +79,20 @@ def cpu_baseline(seconds):
             "seconds": dt}
 
 
+def workload_name(a, world):
+    """Which BASELINE.json config this run is (configs[1..3]), or a plain description."""
+    desc = (f"num_envs={a.num_envs}/GPU x {world} GPU, hidden={a.hidden}, horizon={a.horizon}, GAE lambda=0.95, "
+            f"minibatch={a.minibatch}, {a.epochs} PPO epochs")
+    if a.horizon == 2048 and a.minibatch == 4096 and a.epochs == 10:
+        if world == 1 and a.num_envs == 16384 and a.hidden == 256:
+            return "BASELINE.json configs[2]: " + desc
+        if world == 1 and a.num_envs == 4096 and a.hidden == 64:
+            return "BASELINE.json configs[1]: " + desc
+        if world == 8 and a.num_envs == 8192:
+            return "BASELINE.json configs[3]: " + desc
+    return desc
+
+
 def main():
     a = parse()
     import torch
@@ -210,8 +224,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64+f32",
             "data": "synthetic: reference reset state, random-init (orthogonal, seed 0) policies",
-            "config": {"workload": "BASELINE.json configs[2]: num_envs=16384/GPU, hidden=256, horizon=2048, "
-                                   "GAE lambda=0.95, minibatch=4096, 10 PPO epochs",
+            "config": {"workload": workload_name(a, world),
                        "num_envs_per_gpu": a.num_envs, "num_envs_total": n_total, "horizon": a.horizon,
                        "hidden": a.hidden, "minibatch_per_gpu": a.minibatch, "epochs": a.epochs,
                        "d_capture": a.d_capture, "parallelism": f"dp{world}"},
@@ -221,12 +234,14 @@ def main():
             "env_kernel_env_steps_per_s": a.num_envs / (env_us * 1e-6),
             "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
             "episodes_finished_total": float(stats[0]),
-            "roofline": {"kernel": "satrl_ppo_rowpass<256,16> (hand-written HIP, f32 MFMA 16x16x4)", "bound": "mfma",
+            "roofline": {"kernel": f"satrl_ppo_rowpass<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA 16x16x4)",
+                         "bound": "mfma",
                          "achieved": rowpass_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": rowpass_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
                          "avg_launch_us": rowpass_us, "flop_per_launch": rowpass_flop,
                          "traffic_source": "profiles/r1_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)",
-                         "note": "f32 MFMA; every CU re-reads both fc2 weights from L2 per 16 rows (DESIGN.md)"},
+                         "note": "f32 MFMA; one net per workgroup of 32 rows, each streams that net's fc2 weights "
+                                 "from L2 per phase (DESIGN.md 3.4)"},
             "roofline_env": {"kernel": "satenv step_kernel<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
                              "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
