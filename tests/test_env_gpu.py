@@ -208,3 +208,27 @@ def test_env_rk4_cw_mode_bitexact_vs_oracle(satrl_env, oracle):
         st = o.get_state()
         assert np.array_equal(f[0:3, i], st["Pp"]) and np.array_equal(f[3:6, i], st["Pv"])
         assert np.array_equal(f[6:9, i], st["Ep"]) and np.array_equal(f[9:12, i], st["Ev"])
+
+
+@pytest.mark.parametrize("n", [1000, 33000])
+def test_autoreset_both_lane_layouts_vs_oracle(satrl_env, oracle, n):
+    """<= 32k envs run 4 lanes per env (the quad splits the fsolve branches),
+    more run one lane per env: both must match the oracle rollout.  Bar: the
+    env tolerance of this file -- rewards within 1e-6 rel except where a
+    libm-sensitive danger-zone count flips (<= 0.1 % of env-steps)."""
+    T = 24
+    rng = np.random.default_rng(n)
+    pa = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    rew_o, done_o = oracle.rollout(n, T, pa, ea, d_capture=15000.0, max_episode_steps=10, nthreads=8)
+    env = satrl_env.VecSatellites(n, d_capture=15000.0, max_episode_steps=10)
+    env.reset(0)
+    bad = 0
+    for t in range(T):
+        _, r, d = env.step_autoreset(torch.tensor(pa[t], device="cuda"), torch.tensor(ea[t], device="cuda"))
+        r = r.cpu().numpy().astype(np.float64)
+        ref = rew_o[t].astype(np.float32).astype(np.float64)
+        assert np.mean(d.cpu().numpy() != done_o[t]) <= 1e-3, t
+        bad += int(np.sum(np.abs(r - ref) > 1e-6 * np.maximum(1.0, np.abs(ref))))
+    assert bad <= 1e-3 * n * T, bad
+    assert env.check_errors() == 0
