@@ -174,9 +174,9 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
 // policy/value forward and the update's forward are the same instructions in
 // the same order: logp_old from the rollout equals the update's first
 // recomputation bit for bit, and every row's result is independent of N.
-template <int H, int NW>
+template <int H, int NW, int RR = kRows>
 struct MlpSmem {
-  static constexpr int R = kRows, LDA = H + 4, LDS_S = 36;
+  static constexpr int R = RR, LDA = H + 4, LDS_S = 36;
   float h1s[R][LDA] __attribute__((aligned(16)));     // tanh(fc1)
   float S[R][LDS_S] __attribute__((aligned(16)));     // [s(18) | 1 | 0...] per row
   float osum[NW][R][3];                               // per-wave output-layer partial sums
@@ -188,13 +188,13 @@ struct MlpSmem {
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
 // tanh(fc1) goes to h1out[r * H + n].
-template <int H, int NW, class Gather>
-__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW>& sm, const float* __restrict__ P, int net, int nvalid,
+template <int H, int NW, int R, class Gather>
+__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P, int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
-                                            f4 (&acc)[kRows / 16][H / 16 / NW],
-                                            float (&h1)[kRows / 16][H / 16 / NW][4],
+                                            f4 (&acc)[R / 16][H / 16 / NW],
+                                            float (&h1)[R / 16][H / 16 / NW][4],
                                             float (&w3)[H / 16 / NW][3]) {
-  constexpr int R = kRows, RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
+  constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
   static_assert(CT >= 1 && H % (16 * NW) == 0, "tile split");
   const Layout L = layout(H);
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
@@ -304,8 +304,8 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW>& sm, const float* __r
 }
 
 // output-layer pre-activation of row r, column d: wave partials in fixed order
-template <int NW>
-__device__ __forceinline__ float out_sum(const float (*osum)[kRows][3], int r, int d) {
+template <int NW, int R>
+__device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d) {
   float od = 0.0f;
 #pragma unroll
   for (int k = 0; k < NW; ++k) od += osum[k][r][d];
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
     }
   };
-  mlp_forward<H, NW>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  mlp_forward<H, NW, kRows>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanhf(out_sum<NW>(sm.osum, r, d) + P[L.b3a + d]);
+          th[d] = tanhf(out_sum<NW, kRows>(sm.osum, r, d) + P[L.b3a + d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           const float sd = expf(P[L.ls + d]);
           var[d] = sd * sd;
@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
           dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        const float vc = out_sum<NW>(sm.osum, r, 0) + P[L.b3c];
+        const float vc = out_sum<NW, kRows>(sm.osum, r, 0) + P[L.b3c];
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
@@ -487,6 +487,11 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
 //           evader; the actor is net 0 of each flat layout)
 //   MODE 1  critic value (net 1 of P0), ppo_continuous.py:200-201
 // ---------------------------------------------------------------------------
+// rows per policy/value workgroup (64-row tiles measured 62 vs 58.5 us per
+// rollout step at 16k envs: fewer, larger workgroups lose more to the tail
+// than the halved weight ingest saves)
+constexpr int kPolRows = 32;
+
 template <int H, int NW, int MODE>
 __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float* __restrict__ obs,
                                                      const float* __restrict__ P0, const float* __restrict__ P1,
@@ -496,9 +501,9 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
                                                      float* __restrict__ act0, float* __restrict__ logp0,
                                                      float* __restrict__ act1, float* __restrict__ logp1,
                                                      float* __restrict__ value) {
-  constexpr int R = kRows, RT = R / 16, CT = H / 16 / NW;
+  constexpr int R = kPolRows, RT = R / 16, CT = H / 16 / NW;
   const Layout L = layout(H);
-  __shared__ MlpSmem<H, NW> sm;
+  __shared__ MlpSmem<H, NW, R> sm;
   const int agent = MODE == 0 ? (int)(blockIdx.x % nagents) : 0;
   const int64_t r0 = (int64_t)(MODE == 0 ? blockIdx.x / nagents : blockIdx.x) * R;
   const float* P = agent == 0 ? P0 : P1;
@@ -512,12 +517,12 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  mlp_forward<H, NW, R>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
   if (MODE == 1) {
-    value[i] = out_sum<NW>(sm.osum, r, 0) + P[L.b3c];
+    value[i] = out_sum<NW, R>(sm.osum, r, 0) + P[L.b3c];
     return;
   }
   float z[4];
@@ -527,7 +532,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   float* logp = agent == 0 ? logp0 : logp1;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const float mu = max_action * tanhf(out_sum<NW>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
+    const float mu = max_action * tanhf(out_sum<NW, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
     gaussian_act(mu, P[L.ls + d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
   }
 }
@@ -967,7 +972,7 @@ int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const 
   uint32_t k00, k01, k10, k11;
   philox_key(seed, 0, k00, k01);
   philox_key(seed, 1, k10, k11);
-  const dim3 g((unsigned)(nag * ((N + kRows - 1) / kRows)));
+  const dim3 g((unsigned)(nag * ((N + kPolRows - 1) / kPolRows)));
   hipStream_t s = (hipStream_t)stream;
   if (H == 64)
     hipLaunchKernelGGL((policy_kernel<64, 4, 0>), g, dim3(256), 0, s, N, obs, P0, P1, nag, max_action, k00, k01, k10,
@@ -984,7 +989,7 @@ int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const 
 
 int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float* v_out, void* stream) {
   if (!valid_h(H) || N <= 0 || !obs || !P || !v_out) return -1;
-  const dim3 g((unsigned)((N + kRows - 1) / kRows));
+  const dim3 g((unsigned)((N + kPolRows - 1) / kPolRows));
   hipStream_t s = (hipStream_t)stream;
   if (H == 64)
     hipLaunchKernelGGL((policy_kernel<64, 4, 1>), g, dim3(256), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,

@@ -217,15 +217,11 @@ __device__ __noinline__ double hybrd1(double A, double st, double dvm, double x)
 // ---------------------------------------------------------------------------
 struct Pursuer { double u, dv2, e, f0, p, r, sf0, X, sq; };
 
-// One of the two fsolve branches of rf_extreme_point (k = 0: guess +pi/2,
-// :516-531; k = 1: guess -pi/2, :534-548).  `none` = the temp1 < 0 early
-// return (:477), where the reference returns (0, 0).
-__device__ __forceinline__ double rf_branch(const Pursuer& P, double f_c, int k, bool& none) {
+__device__ __forceinline__ void rf_extreme(const Pursuer& P, double f_c, double& rmax, double& rmin) {
   const double d = f_c - P.f0;
   const double sd = sin(d);
   const double temp1 = (sd * sd) / (P.u * (P.X * P.X) / (P.p * P.dv2) - 1.0);    // :466
-  none = !(0.0 <= temp1);                                                        // :477
-  if (none) return 0.0;
+  if (!(0.0 <= temp1)) { rmax = 0.0; rmin = 0.0; return; }                       // :477
   const double beta = atan(0.0 / sd);                                            // tan(fai)=0, :469
   const double sb = sin(beta), cb = cos(beta);
   const double dvm = sqrt(P.dv2 - P.u * (P.X * P.X) * (sb * sb) / P.p);          // :470
@@ -236,34 +232,25 @@ __device__ __forceinline__ double rf_branch(const Pursuer& P, double f_c, int k,
   sincos(theta, &st, &ct);
   const double vx0 = P.sq * P.e * P.sf0;                                         // :518
   const double vy0 = P.sq * P.X * cb;                                            // :519
-  const double ag = k == 0 ? kPi / 2 : -kPi / 2;                                 // :516, :534
-  double sg, cg;
-  sincos(ag, &sg, &cg);
-  const double v1x = vx0 + dvm * cg, v1y = vy0 + dvm * sg;
-  const double h = P.r * v1y;
-  const double A = (2.0 * P.u * (1.0 - ct)) / (h * v1y) - v1x * st / v1y;        // :560
-  const double al = hybrd1(A, st, dvm, ag);
-  double sa, ca;
-  sincos(al, &sa, &ca);
-  const double vx = vx0 + dvm * ca, vy = vy0 + dvm * sa;                         // :525-528
-  const double hm = P.r * vy;
-  return (hm * hm) / (P.u * (1.0 - ct) + hm * vy * ct - hm * vx * st);           // :530
-}
-
-// abs + sort of the two branch values (:549-554)
-__device__ __forceinline__ void rf_sort(double rf0, double rf1, double& rmax, double& rmin) {
-  rmax = fabs(rf0);
-  rmin = fabs(rf1);
-  if (rmax < rmin) { const double t = rmin; rmin = rmax; rmax = t; }
-}
-
-// satellite_function.py:462-556 rf_extreme_point('orbit_c1'/'orbit_c2'), fai = 0
-__device__ __forceinline__ void rf_extreme(const Pursuer& P, double f_c, double& rmax, double& rmin) {
-  bool none;
-  const double rf0 = rf_branch(P, f_c, 0, none);
-  if (none) { rmax = 0.0; rmin = 0.0; return; }
-  const double rf1 = rf_branch(P, f_c, 1, none);
-  rf_sort(rf0, rf1, rmax, rmin);
+  double rf[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double ag = k == 0 ? kPi / 2 : -kPi / 2;                               // :516, :534
+    double sg, cg;
+    sincos(ag, &sg, &cg);
+    const double v1x = vx0 + dvm * cg, v1y = vy0 + dvm * sg;
+    const double h = P.r * v1y;
+    const double A = (2.0 * P.u * (1.0 - ct)) / (h * v1y) - v1x * st / v1y;      // :560
+    const double al = hybrd1(A, st, dvm, ag);
+    double sa, ca;
+    sincos(al, &sa, &ca);
+    const double vx = vx0 + dvm * ca, vy = vy0 + dvm * sa;                       // :525-528
+    const double hm = P.r * vy;
+    rf[k] = (hm * hm) / (P.u * (1.0 - ct) + hm * vy * ct - hm * vx * st);        // :530
+  }
+  rmax = fabs(rf[0]);
+  rmin = fabs(rf[1]);
+  if (rmax < rmin) { const double t = rmin; rmin = rmax; rmax = t; }            // :549-554
 }
 
 // self.Delta_V_c ** 2 by numpy scalar type
@@ -273,16 +260,9 @@ __device__ __forceinline__ double fuel_sq(double fuel, int mode) {
 }
 
 // environment.py:317-332 + satellite_function.py:18-99,317-373.  Returns 0 or <0.
-// LPE = 1: one lane does the whole count.  LPE = 4: the four lanes of an
-// aligned quad (q = lane & 3) share one env; each runs one of the four
-// independent fsolve branches (orbit c1/c2 x guess +-pi/2) and the quad
-// exchanges the results, so the count is bit-identical to LPE = 1 and the
-// hybrd chains run side by side instead of one after another.  All four
-// lanes of a quad must reach this call together.
-template <int LPE = 1>
 __device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
                                            double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
-                                           double Ev1, double Ev2, double fuel, int fmode, int& count, int q = 0) {
+                                           double Ev1, double Ev2, double fuel, int fmode, int& count) {
   const double u = 3.986e14;                                // Time_window_of_danger_zone default u
   Elements C, T;
   int rc = orbital_elements(u, prm.R_cw[0] + Pp0, prm.R_cw[1] + Pp1, prm.R_cw[2] + Pp2, prm.V_cw[0] + Pv0,
@@ -315,20 +295,8 @@ __device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double
   const double u_c1 = atan(temp1), u_c2 = kPi + u_c1;
   const double u_t1 = atan(temp2), u_t2 = u_t1 + kPi;
   double mx1, mn1, mx2, mn2;
-  if constexpr (LPE == 4) {
-    bool none;
-    const double rf = rf_branch(P, (q < 2 ? u_c1 : u_c2) - C.omega, q & 1, none);
-    const double rfp = __shfl_xor(rf, 1, 64);                                    // the other guess, same orbit
-    double mx, mn;
-    rf_sort((q & 1) ? rfp : rf, (q & 1) ? rf : rfp, mx, mn);
-    if (none) { mx = 0.0; mn = 0.0; }
-    const double mxo = __shfl_xor(mx, 2, 64), mno = __shfl_xor(mn, 2, 64);      // the other orbit
-    mx1 = q < 2 ? mx : mxo; mn1 = q < 2 ? mn : mno;
-    mx2 = q < 2 ? mxo : mx; mn2 = q < 2 ? mno : mn;
-  } else {
-    rf_extreme(P, u_c1 - C.omega, mx1, mn1);
-    rf_extreme(P, u_c2 - C.omega, mx2, mn2);
-  }
+  rf_extreme(P, u_c1 - C.omega, mx1, mn1);
+  rf_extreme(P, u_c2 - C.omega, mx2, mn2);
   const double pt = T.a * (1.0 - T.e * T.e);
   const double r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                  // :363 (cross-wired f_t2)
   const double r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                  // :365

@@ -108,18 +108,11 @@ __device__ __forceinline__ void wave_stats(double* stats, double fin, double fin
 // ---------------------------------------------------------------------------
 // One environment step (environment.py:81-255), one lane per env.
 // ---------------------------------------------------------------------------
-// LPE lanes per env (an aligned quad for LPE = 4): every lane of the quad
-// runs the step redundantly on the same inputs (same values, so the loads
-// hit the same lines), the danger-zone count splits its four independent
-// fsolve branches across the quad (danger_zone<4>), and lane q = 0 alone
-// stores.  At 16k envs this gives 4 waves per CU instead of one.
-template <bool AUTORESET, int LPE>
+template <bool AUTORESET>
 __global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, double* __restrict__ f64,
                                                    int32_t* __restrict__ i32, StepIO io) {
-  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t i = gt / LPE;
-  const int q = (int)(gt % LPE);
-  const bool live = i < n, lead = q == 0;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < n;
   double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0, cap = 0.0;
   if (live) {
     double k[12];
@@ -197,9 +190,9 @@ __global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, 
       done = true;
     } else {
       int cnt = 0;
-      const int rc = danger_zone<LPE>(prm, k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9], k[10],
-                                      k[11], fuel_c, fcm, cnt, q);          // :150, :317-332
-      if (rc && lead) atomicCAS(io.err, 0, rc);
+      const int rc = danger_zone(prm, k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9], k[10], k[11],
+                                 fuel_c, fcm, cnt);                         // :150, :317-332
+      if (rc) atomicCAS(io.err, 0, rc);
       dz = cnt;
       double r = (dis < dis_prev) ? 1.0 : -1.0;                            // :161-164
       r += (prm.d_capture <= dis && dis <= 4 * prm.d_capture) ? -1.0 : -2.0;
@@ -221,11 +214,9 @@ __global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, 
       done = false;
     }
 
-    if (lead) {
-      if (io.rew64) io.rew64[i] = reward;
-      if (io.rew32) io.rew32[i] = (float)reward;
-      if (io.done) io.done[i] = done ? 1 : 0;
-    }
+    if (io.rew64) io.rew64[i] = reward;
+    if (io.rew32) io.rew32[i] = (float)reward;
+    if (io.done) io.done[i] = done ? 1 : 0;
     double ret = f64[kPlaneRet * n + i] + reward;
     rew_acc = reward;
     int vi_out = 0;
@@ -237,20 +228,16 @@ __global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, 
       vi_out = 1;
       count = 0;
     }
-    if (lead) {
-      write_obs(io.obs, io.obs64, i, k);
+    write_obs(io.obs, io.obs64, i, k);
 #pragma unroll
-      for (int c = 0; c < 12; ++c) f64[c * n + i] = k[c];
-      f64[12 * n + i] = fuel_c;
-      f64[13 * n + i] = fuel_t;
-      f64[14 * n + i] = dis;
-      f64[kPlaneRet * n + i] = ret;
-      i32[kPlaneDz * n + i] = dz;
-      i32[kPlaneCount * n + i] = count;
-      i32[kPlaneBits * n + i] = make_bits(fcm, ftm, vi_out, flag);
-    } else {
-      fin = 0.0; fin_ret = 0.0; rew_acc = 0.0; cap = 0.0;                  // counted once per env
-    }
+    for (int c = 0; c < 12; ++c) f64[c * n + i] = k[c];
+    f64[12 * n + i] = fuel_c;
+    f64[13 * n + i] = fuel_t;
+    f64[14 * n + i] = dis;
+    f64[kPlaneRet * n + i] = ret;
+    i32[kPlaneDz * n + i] = dz;
+    i32[kPlaneCount * n + i] = count;
+    i32[kPlaneBits * n + i] = make_bits(fcm, ftm, vi_out, flag);
   }
   if (io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
 }
@@ -343,22 +330,15 @@ struct satenv_env {
   int32_t* i32 = nullptr;
   int32_t* err = nullptr;
   int block = 64;
-  int lpe = 1;   // lanes per env in the step kernels
 };
 
 namespace {
 
 int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
-// env-step launch geometry.  Up to 32k envs, 4 lanes per env (the quad
-// splits the danger-zone fsolve branches) in 256-thread workgroups, so 16k
-// envs fill every SIMD once; measured 33 vs 63 us per step at 16k envs and
-// 29 vs 62 at 4k.  Beyond that the chip is full with one lane per env and
-// the quad's redundant work costs (79 vs 68 us at 64k), so LPE = 1 with
-// 64/128/256-lane workgroups.
-int pick_lpe(int64_t n) { return n <= 32768 ? 4 : 1; }
-int pick_block(int64_t n, int lpe) {
-  if (lpe > 1) return 256;
+// env-step launch geometry: N = 16384 envs is only 256 waves, so 64-lane
+// workgroups spread them over all 256 CUs instead of packing 4 per CU.
+int pick_block(int64_t n) {
   if (n <= 256 * 64) return 64;
   if (n <= 256 * 128) return 128;
   return 256;
@@ -420,8 +400,7 @@ int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, in
   h->n = num_envs;
   h->device = device;
   h->prm = *p;
-  h->lpe = pick_lpe(num_envs);
-  h->block = pick_block(num_envs, h->lpe);
+  h->block = pick_block(num_envs);
   hipError_t e = hipMalloc(&h->f64, sizeof(double) * kF64Planes * num_envs);
   if (e == hipSuccess) e = hipMalloc(&h->i32, sizeof(int32_t) * kI32Planes * num_envs);
   if (e == hipSuccess) e = hipMalloc(&h->err, sizeof(int32_t));
@@ -479,12 +458,8 @@ int satenv_step(satenv_env* h, const float* pa, const float* ea, const int32_t* 
                 double* obs64_out, double* reward_out, uint8_t* done_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step: null argument");
   StepIO io{pa, ea, episode_count, obs_out, obs64_out, reward_out, nullptr, done_out, nullptr, h->err};
-  if (h->lpe == 4)
-    hipLaunchKernelGGL((step_kernel<false, 4>), dim3(grid_for(h->n * 4, h->block)), dim3(h->block), 0,
-                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
-  else
-    hipLaunchKernelGGL((step_kernel<false, 1>), dim3(grid_for(h->n, h->block)), dim3(h->block), 0,
-                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
+  hipLaunchKernelGGL(step_kernel<false>, dim3(grid_for(h->n, h->block)), dim3(h->block), 0, (hipStream_t)stream,
+                     h->prm, h->n, h->f64, h->i32, io);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }
@@ -493,12 +468,8 @@ int satenv_step_autoreset(satenv_env* h, const float* pa, const float* ea, float
                           uint8_t* done_out, double* stats_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step_autoreset: null argument");
   StepIO io{pa, ea, nullptr, obs_out, nullptr, nullptr, reward_out, done_out, stats_out, h->err};
-  if (h->lpe == 4)
-    hipLaunchKernelGGL((step_kernel<true, 4>), dim3(grid_for(h->n * 4, h->block)), dim3(h->block), 0,
-                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
-  else
-    hipLaunchKernelGGL((step_kernel<true, 1>), dim3(grid_for(h->n, h->block)), dim3(h->block), 0,
-                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
+  hipLaunchKernelGGL(step_kernel<true>, dim3(grid_for(h->n, h->block)), dim3(h->block), 0, (hipStream_t)stream,
+                     h->prm, h->n, h->f64, h->i32, io);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }
