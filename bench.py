@@ -18,6 +18,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
 
@@ -77,6 +79,18 @@ def cpu_baseline(seconds):
                       f"(Flag 0, U(-1.6,1.6) f32 actions, d_capture 15000, max_episode_steps 1000), OpenMP {threads} "
                       f"threads on '{model}' (os.cpu_count()={os.cpu_count()})",
             "seconds": dt}
+
+
+def rd_cpu_baseline():
+    """One reference-default reachable-domain grid (RD_single_pulse.py params
+    :9-20) on the C restatement, 1 core, ms per grid."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        O.reachable_domain_grid(1e7, 0.2, np.pi / 2, 500.0, 1, 200, 200)
+    return (time.perf_counter() - t0) / reps * 1e3
 
 
 def workload_name(a, world):
@@ -208,6 +222,25 @@ def main():
     torch.cuda.synchronize()
     env_rk_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
 
+    # ---- §8f rank 4: reachable-domain grid (RD_single_pulse.py:40-148), the reference's
+    # default 1 x 201 x 201 direction grid for a batch of orbits in one launch
+    from satrl import reachable as RD
+    rd_sets = 256
+    gr = np.random.default_rng(5)
+    rd_orb = RD.orbits_tensor(gr.uniform(7e6, 5e7, rd_sets), gr.uniform(0.0, 0.8, rd_sets),
+                              gr.uniform(0.05, 2 * np.pi - 0.05, rd_sets), gr.uniform(50.0, 1000.0, rd_sets),
+                              device="cuda")
+    rd_out = RD.reachable_domain_grid(rd_orb, 1, 200, 200)
+    rd_reach = int((rd_out[2] == 1).sum())
+    rd_iters = 5
+    e0.record()
+    for _ in range(rd_iters):
+        RD.reachable_domain_grid(rd_orb, 1, 200, 200)
+    e1.record()
+    torch.cuda.synchronize()
+    rd_ms = e0.elapsed_time(e1) / rd_iters
+    del rd_out
+
     rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
     update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
     gae_ms = sum(timers["gae_ms"]) / len(timers["gae_ms"])
@@ -219,6 +252,7 @@ def main():
 
     if rank == 0:
         cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_baseline_seconds)
+        rd_cpu_ms = None if a.no_cpu_baseline else rd_cpu_baseline()
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -253,6 +287,11 @@ def main():
                             "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
                             "env_rk4_cw_avg_launch_us": env_rk_us,
                             "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6)},
+            "reachable_domain": {"grids_per_s": rd_sets / (rd_ms * 1e-3), "ms_per_launch": rd_ms,
+                                 "sample": f"{rd_sets} random orbits x 201 x 201 directions (RD_single_pulse "
+                                           "defaults N1=1, N2=N3=200), one launch incl. output zero-fill",
+                                 "reachable_directions": rd_reach,
+                                 "cpu_oracle_ms_per_grid": rd_cpu_ms},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

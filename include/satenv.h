@@ -132,6 +132,28 @@ int satenv_check(satenv_env* h, int32_t* status);
  * km/s); in place allowed.                                               */
 int satenv_rk4_j2(int64_t n, const double* rv_in, double h, int32_t steps, double* rv_out, void* stream);
 
+/* Reachable domain of a single impulse, single_pluse_model/RD_single_pulse.py
+ * Reachable_Domain (:40-148, module params :9-20), for nsets orbits at once.
+ * orbits: device array [nsets].  The direction grid is the reference's:
+ * impulse dV = -delta_max + 2 delta_max jj/N1 (jj = 1..N1), gama = 2 pi i/N2
+ * (i = 0..N2), alpha = -pi/2 + pi j/N3 (j = 0..N3); direction
+ * d = ((jj-1)(N2+1) + i)(N3+1) + j, ndir = N1 (N2+1) (N3+1).
+ * status u8 [nsets][ndir]: 0 unreachable (:81), 1 reachable, 2 reachable but
+ * gama - f outside both theta branches (:87-90; the reference then reuses a
+ * stale theta).  rf_max / rf_min f64 [nsets][ndir][3]: the points
+ * max/min(|rf_max|, |rf_min|) * P of :123-124 where status == 1; other
+ * entries are left untouched.  Compacting status == 1 in d order gives the
+ * RF_max / RF_min lists Reachable_Domain passes to Curve_fitting (:140).   */
+typedef struct {
+    double a;          /* params['a'], semi-major axis [m]          */
+    double e0;         /* params['e0'], eccentricity                */
+    double f;          /* params['f'], true anomaly of the burn     */
+    double delta_max;  /* params['delta_max'], max impulse [m/s]    */
+    double mu;         /* params['u'] = 3.986e14                    */
+} satenv_rd_orbit;
+int satenv_reachable_domain(int64_t nsets, const satenv_rd_orbit* orbits, int32_t n1, int32_t n2, int32_t n3,
+                            double* rf_max, double* rf_min, uint8_t* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,8 @@ def lib():
         L.orc_rk4_j2_step.argtypes = [dp, C.c_double, dp]
         L.orc_rk4_j2_propagate.argtypes = [dp, C.c_double, C.c_int32]
         L.orc_cw_rk4.argtypes = [dp, C.c_double, C.c_double, C.c_int32, dp]
+        L.orc_reachable_domain.argtypes = [C.POINTER(OrcRdParams), dp, dp, C.POINTER(C.c_uint8)]
+        L.orc_reachable_domain.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -116,6 +118,33 @@ def stm(t=100.0):
     out = np.zeros(36)
     lib().orc_stm(float(t), _dp(out))
     return out.reshape(6, 6)
+
+
+class OrcRdParams(C.Structure):
+    _fields_ = [("a", C.c_double), ("e0", C.c_double), ("f", C.c_double), ("delta_max", C.c_double),
+                ("mu", C.c_double), ("n1", C.c_int32), ("n2", C.c_int32), ("n3", C.c_int32)]
+
+
+def reachable_domain_grid(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14):
+    """RD_single_pulse.py:40-148 over the whole direction grid: returns
+    (rf_max [n][3], rf_min [n][3], status [n] u8) with n = n1*(n2+1)*(n3+1)."""
+    p = OrcRdParams(float(a), float(e0), float(f), float(delta_max), float(mu), int(n1), int(n2), int(n3))
+    n = int(n1) * (int(n2) + 1) * (int(n3) + 1)
+    mx = np.zeros((n, 3))
+    mn = np.zeros((n, 3))
+    st = np.zeros(n, dtype=np.uint8)
+    lib().orc_reachable_domain(C.byref(p), _dp(mx), _dp(mn), st.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return mx, mn, st
+
+
+def reachable_domain(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14):
+    """The RF_max / RF_min point lists Reachable_Domain hands to Curve_fitting
+    (RD_single_pulse.py:138-140), in the reference's loop order."""
+    mx, mn, st = reachable_domain_grid(a, e0, f, delta_max, n1, n2, n3, mu)
+    if (st == 2).any():
+        raise ValueError("gama - f outside the theta branches of RD_single_pulse.py:87-90")
+    keep = st == 1
+    return mx[keep], mn[keep]
 
 
 def solve_alpha(u, dvm, theta, v1x, v1y, h, guess):

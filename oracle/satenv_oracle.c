@@ -436,6 +436,66 @@ int orc_danger_zone(const double R0_c[3], const double V0_c[3], const double R0_
     return 0;
 }
 
+/* ---- single_pluse_model/RD_single_pulse.py:40-148 Reachable_Domain -------- */
+/* Direction d = ((jj-1)*(N2+1) + i)*(N3+1) + j.  status[d]: 0 unreachable,
+ * 1 reachable (rf_max/rf_min hold the two points of :123-124), 2 reachable but
+ * gama-f outside both theta branches of :87-90 (the reference then reuses a
+ * stale theta from an earlier direction; reported instead of restated).     */
+static double py_max(double a, double b) { return (b > a) ? b : a; }   /* builtin max(a, b) */
+static double py_min(double a, double b) { return (b < a) ? b : a; }
+
+int64_t orc_reachable_domain(const orc_rd_params* p, double* rf_max, double* rf_min, uint8_t* status) {
+    const double u = p->mu, e0 = p->e0, f = p->f;
+    const double X = 1 + e0 * cos(f);
+    const double r0 = p->a * (1 - sq2(e0)) / X;                              /* :47 */
+    const double p0 = p->a * (1 - sq2(e0));                                  /* :48 */
+    const double sq = sqrt(u / p0);
+    int64_t d = 0, reach = 0;
+    for (int32_t jj = 1; jj <= p->n1; ++jj) {
+        const double dV = -p->delta_max + (2 * p->delta_max * jj) / p->n1;   /* :64 */
+        const double dV2 = sq2(dV);
+        for (int32_t i = 0; i <= p->n2; ++i) {
+            const double gama = (ORC_2PI * i) / p->n2;                        /* :66 */
+            const double g = gama - f;
+            const double sg = sin(g);
+            for (int32_t j = 0; j <= p->n3; ++j, ++d) {
+                const double alpha = -ORC_PI / 2 + (ORC_PI * j) / p->n3;      /* :68 */
+                const double P[3] = {sin(gama) * cos(alpha), cos(gama) * cos(alpha), sin(alpha)};
+                const double temp1 = sq2(sg) / (u * sq2(X) / (p0 * dV2) - 1);  /* :79 */
+                const double ta = tan(alpha);
+                status[d] = 0;
+                if (!(0 <= sq2(ta) && sq2(ta) <= temp1)) continue;             /* :81 */
+                const double beta = atan(ta / sg);                              /* :82 */
+                const double dvm = sqrt(dV2 - u * sq2(X) * sq2(sin(beta)) / p0);  /* :84 */
+                double theta;
+                if ((-2 * ORC_PI <= g && g < -ORC_PI) || (0 <= g && g < ORC_PI))
+                    theta = acos(cos(g) * cos(alpha));                          /* :88 */
+                else if ((-ORC_PI <= g && g < 0) || (ORC_PI <= g && g < 2 * ORC_PI))
+                    theta = ORC_2PI - acos(cos(g) * cos(alpha));                /* :90 */
+                else { status[d] = 2; continue; }
+                double rf[2];
+                for (int k = 0; k < 2; ++k) {
+                    const double ag = (k == 0) ? ORC_PI / 2 : -ORC_PI / 2;     /* :93, :109 */
+                    const double v1x = sq * e0 * sin(f) + dvm * cos(ag);
+                    const double v1y = sq * X * cos(beta) + dvm * sin(ag);
+                    const double h = r0 * v1y;
+                    const double al = orc_solve_alpha(u, dvm, theta, v1x, v1y, h, ag, 0);   /* :150-157 */
+                    const double vx = sq * e0 * sin(f) + dvm * cos(al);       /* :102-104 */
+                    const double vy = sq * X * cos(beta) + dvm * sin(al);
+                    const double hm = r0 * vy;
+                    rf[k] = sq2(hm) / (u * (1 - cos(theta)) + hm * vy * cos(theta) - hm * vx * sin(theta));
+                }
+                const double mx = py_max(fabs(rf[0]), fabs(rf[1]));           /* :123 */
+                const double mn = py_min(fabs(rf[0]), fabs(rf[1]));           /* :124 */
+                for (int c = 0; c < 3; ++c) { rf_max[3 * d + c] = mx * P[c]; rf_min[3 * d + c] = mn * P[c]; }
+                status[d] = 1;
+                ++reach;
+            }
+        }
+    }
+    return reach;
+}
+
 /* ---- environment.py ------------------------------------------------------- */
 void orc_default_params(orc_params* p, double d_capture, int32_t max_episode_steps) {
     p->d_capture = d_capture;            /* train_* overwrite env.d_capture (CPPO_main.py:98) */

@@ -72,6 +72,14 @@ void orc_rk4_j2_propagate(double rv[6], double h, int32_t steps);
  * RungeKutta stage combination of the script above)                      */
 void orc_cw_rk4(const double x[6], double w, double t, int32_t nsub, double y[6]);
 
+/* reachable-domain direction grid, RD_single_pulse.py:40-148 (params :9-20) */
+typedef struct {
+    double a, e0, f, delta_max, mu;
+    int32_t n1, n2, n3;
+} orc_rd_params;
+/* fills n1*(n2+1)*(n3+1) directions; returns the number with status 1 */
+int64_t orc_reachable_domain(const orc_rd_params* p, double* rf_max, double* rf_min, uint8_t* status);
+
 /* batched replay for the CPU baseline: n envs x steps, actions [steps][n][3] */
 int  orc_rollout(const orc_params* p, orc_env* envs, int64_t n, int32_t steps,
                  const float* pa, const float* ea, int32_t* episode_count,

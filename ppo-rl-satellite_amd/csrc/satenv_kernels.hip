@@ -320,6 +320,117 @@ __global__ void __launch_bounds__(256) rk4_j2_kernel(int64_t n, const double* __
   for (int c = 0; c < 6; ++c) out[c * n + i] = s[c];
 }
 
+// ---------------------------------------------------------------------------
+// single_pluse_model/RD_single_pulse.py:40-148 Reachable_Domain, batched over
+// orbits.  Direction d = ((jj-1)*(N2+1) + i)*(N3+1) + j.  Only a few percent
+// of the directions pass the reachability test (:81), so a workgroup first
+// classifies kRdTile directions (cheap: one sin, one tan), compacts the
+// reachable ones into an LDS list and then runs the two hybrd solves over
+// the list with packed lanes instead of one mostly-idle lane per direction.
+// ---------------------------------------------------------------------------
+constexpr int kRdBlock = 256, kRdPer = 4, kRdTile = kRdBlock * kRdPer;
+
+struct RdDir { double dV2, gama, alpha, g; };
+
+__device__ __forceinline__ RdDir rd_dir(const satenv_rd_orbit& o, int n1, int n2, int n3, int d) {
+  const int per = (n2 + 1) * (n3 + 1);
+  const int jj = d / per + 1, rem = d - (jj - 1) * per;
+  const int i = rem / (n3 + 1), j = rem - i * (n3 + 1);
+  RdDir r;
+  const double dV = -o.delta_max + (2.0 * o.delta_max * jj) / n1;   // :64
+  r.dV2 = dV * dV;
+  r.gama = (kTwoPi * i) / n2;                                       // :66
+  r.alpha = -kPi / 2 + (kPi * j) / n3;                              // :68
+  r.g = r.gama - o.f;
+  return r;
+}
+
+__device__ __forceinline__ double rd_X(const satenv_rd_orbit& o) { return 1.0 + o.e0 * cos(o.f); }
+
+// 0 unreachable, 1 reachable, 2 reachable but gama - f outside both theta branches (:87-90)
+__device__ __forceinline__ int rd_status(const satenv_rd_orbit& o, double p0, double X, const RdDir& r) {
+  const double sg = sin(r.g);
+  const double temp1 = (sg * sg) / (o.mu * (X * X) / (p0 * r.dV2) - 1.0);   // :79
+  const double ta = tan(r.alpha);
+  if (!(0.0 <= ta * ta && ta * ta <= temp1)) return 0;                        // :81
+  const double g = r.g;
+  if ((-kTwoPi <= g && g < -kPi) || (0.0 <= g && g < kPi)) return 1;
+  if ((-kPi <= g && g < 0.0) || (kPi <= g && g < kTwoPi)) return 1;
+  return 2;
+}
+
+__global__ void __launch_bounds__(kRdBlock) rd_kernel(const satenv_rd_orbit* __restrict__ orbits, int32_t n1,
+                                                      int32_t n2, int32_t n3, int32_t ndir, int32_t tiles,
+                                                      double* __restrict__ rf_max, double* __restrict__ rf_min,
+                                                      uint8_t* __restrict__ status) {
+  __shared__ int list[kRdTile];
+  __shared__ int cnt;
+  const int64_t set = blockIdx.x / tiles;
+  const int d0 = (int)(blockIdx.x - set * tiles) * kRdTile;
+  const satenv_rd_orbit o = orbits[set];
+  const double X = rd_X(o);
+  const double p0 = o.a * (1.0 - o.e0 * o.e0);                    // :48
+  const double r0 = p0 / X;                                       // :47
+  const double sq = sqrt(o.mu / p0);
+  const double vx0 = sq * o.e0 * sin(o.f);                        // :95
+  const int64_t base = set * (int64_t)ndir;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kRdPer; ++q) {
+    const int d = d0 + q * kRdBlock + (int)threadIdx.x;
+    if (d < ndir) {
+      const int st = rd_status(o, p0, X, rd_dir(o, n1, n2, n3, d));
+      status[base + d] = (uint8_t)st;
+      if (st == 1) list[atomicAdd(&cnt, 1)] = d;
+    }
+  }
+  __syncthreads();
+  const int m = cnt;
+  for (int k = (int)threadIdx.x; k < m; k += kRdBlock) {
+    const int d = list[k];
+    const RdDir r = rd_dir(o, n1, n2, n3, d);
+    const double sg = sin(r.g);
+    const double ta = tan(r.alpha);
+    const double beta = atan(ta / sg);                                          // :82
+    double sb, cb;
+    sincos(beta, &sb, &cb);
+    const double dvm = sqrt(r.dV2 - o.mu * (X * X) * (sb * sb) / p0);         // :84
+    const double ca = cos(r.alpha);
+    const double ac = acos(cos(r.g) * ca);
+    const double theta = ((-kTwoPi <= r.g && r.g < -kPi) || (0.0 <= r.g && r.g < kPi)) ? ac : kTwoPi - ac;   // :87-90
+    double st, ct;
+    sincos(theta, &st, &ct);
+    const double vy0 = sq * X * cb;                                             // :96
+    double rf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const double ag = s == 0 ? kPi / 2 : -kPi / 2;                           // :93, :109
+      double sgs, cgs;
+      sincos(ag, &sgs, &cgs);
+      const double v1x = vx0 + dvm * cgs, v1y = vy0 + dvm * sgs;
+      const double h = r0 * v1y;                                                // :98
+      const double A = (2.0 * o.mu * (1.0 - ct)) / (h * v1y) - v1x * st / v1y; // :152
+      const double al = hybrd1(A, st, dvm, ag);                                 // :150-157
+      double sa, cal;
+      sincos(al, &sa, &cal);
+      const double vx = vx0 + dvm * cal, vy = vy0 + dvm * sa;                   // :102-104
+      const double hm = r0 * vy;
+      rf[s] = (hm * hm) / (o.mu * (1.0 - ct) + hm * vy * ct - hm * vx * st);   // :106, :121
+    }
+    const double a0 = fabs(rf[0]), a1 = fabs(rf[1]);
+    const double mx = (a1 > a0) ? a1 : a0;                                      // builtin max, :123
+    const double mn = (a1 < a0) ? a1 : a0;                                      // builtin min, :124
+    double sgm, cgm;
+    sincos(r.gama, &sgm, &cgm);
+    const double P[3] = {sgm * ca, cgm * ca, sin(r.alpha)};                     // :71
+    double* omx = rf_max + 3 * (base + d);
+    double* omn = rf_min + 3 * (base + d);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { omx[c] = mx * P[c]; omn[c] = mn * P[c]; }
+  }
+}
+
 }  // namespace
 
 struct satenv_env {
@@ -516,6 +627,20 @@ int satenv_rk4_j2(int64_t n, const double* rv_in, double h, int32_t steps, doubl
   if (n <= 0 || !rv_in || !rv_out || steps < 0) return fail(SATENV_ERR_ARG, "satenv_rk4_j2: bad args");
   hipLaunchKernelGGL(rk4_j2_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, rv_in, h, steps,
                      rv_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_reachable_domain(int64_t nsets, const satenv_rd_orbit* orbits, int32_t n1, int32_t n2, int32_t n3,
+                            double* rf_max, double* rf_min, uint8_t* status, void* stream) {
+  if (nsets <= 0 || !orbits || !rf_max || !rf_min || !status || n1 < 1 || n2 < 1 || n3 < 1)
+    return fail(SATENV_ERR_ARG, "satenv_reachable_domain: bad args (N1, N2, N3 >= 1)");
+  const int64_t ndir = (int64_t)n1 * (n2 + 1) * (n3 + 1);
+  const int64_t tiles = (ndir + kRdTile - 1) / kRdTile;
+  if (ndir > INT32_MAX || nsets * tiles > INT32_MAX)
+    return fail(SATENV_ERR_ARG, "satenv_reachable_domain: grid too large");
+  hipLaunchKernelGGL(rd_kernel, dim3((unsigned)(nsets * tiles)), dim3(kRdBlock), 0, (hipStream_t)stream, orbits, n1,
+                     n2, n3, (int32_t)ndir, (int32_t)tiles, rf_max, rf_min, status);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

@@ -1,0 +1,91 @@
+"""Reachable domain of a single impulse on the GPU.
+
+Restates single_pluse_model/RD_single_pulse.py:Reachable_Domain (:40-148)
+as the satenv_reachable_domain kernel: the N1 x (N2+1) x (N3+1) direction
+grid, the reachability test (:79-81), beta / Delta_Vm / theta (:82-90), two
+hybrd solves per direction (:93-121, fsolve of :150-157) and the extreme
+points max/min(|rf|) * P (:123-124).  Many orbits run in one launch
+(`reachable_domain_grid`), which is what a vectorised Flag-2 env needs; the
+reference runs one orbit per call at ~0.9 s.
+
+`params` / `Incoming_parameters` / `Reachable_Domain` mirror the module's
+globals-driven API (:9-37) but return the point lists (RF_max, RF_min) that
+the reference hands to curve_fitting.Curve_fitting (:140); the ellipse fit
+itself is host-side sklearn/scipy post-processing and is not part of this
+engine.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+
+# RD_single_pulse.py:9-20
+params = {
+    "a": 10 ** 7,
+    "i": 0,
+    "e0": 0.2,
+    "f": np.pi / 2,
+    "delta_max": 500,
+    "u": 3.986e14,
+    "N1": 1,
+    "N2": 200,
+    "N3": 200,
+    "delta_l": 1500,
+}
+
+UNREACHABLE, REACHABLE, THETA_UNDEFINED = 0, 1, 2
+
+
+def orbits_tensor(a, e0, f, delta_max, mu=3.986e14, device="cuda"):
+    """[nsets][5] f64 rows (a, e0, f, delta_max, mu) = satenv_rd_orbit; scalars broadcast."""
+    cols = np.broadcast_arrays(*[np.asarray(v, dtype=np.float64) for v in (a, e0, f, delta_max, mu)])
+    arr = np.stack([c.reshape(-1) for c in cols], axis=1)
+    return torch.tensor(arr, dtype=torch.float64, device=device)
+
+
+def reachable_domain_grid(orbits, n1=1, n2=200, n3=200, stream=None):
+    """Dense grid for every orbit: (rf_max [nsets][ndir][3], rf_min, status
+    [nsets][ndir] u8) with ndir = n1*(n2+1)*(n3+1), direction order of the
+    reference loops (jj, i, j).  Entries with status != 1 are zero."""
+    _lib.require_cuda(orbits, torch.float64, None, "orbits")
+    if orbits.dim() != 2 or orbits.shape[1] != 5 or not orbits.is_contiguous():
+        raise ValueError("orbits must be a contiguous [nsets][5] f64 tensor")
+    nsets = orbits.shape[0]
+    ndir = int(n1) * (int(n2) + 1) * (int(n3) + 1)
+    dev = orbits.device
+    rf_max = torch.zeros((nsets, ndir, 3), dtype=torch.float64, device=dev)
+    rf_min = torch.zeros_like(rf_max)
+    status = torch.empty((nsets, ndir), dtype=torch.uint8, device=dev)
+    check(_lib.lib().satenv_reachable_domain(nsets, ptr(orbits), int(n1), int(n2), int(n3), ptr(rf_max),
+                                             ptr(rf_min), ptr(status), stream_ptr(stream)),
+          "satenv_reachable_domain")
+    return rf_max, rf_min, status
+
+
+def reachable_domain(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14, device="cuda"):
+    """RF_max, RF_min ([m][3] f64, on `device`) of one orbit, in the
+    reference's append order (RD_single_pulse.py:123-124, :138-139)."""
+    orbits = orbits_tensor(a, e0, f, delta_max, mu, device)
+    mx, mn, st = reachable_domain_grid(orbits, n1, n2, n3)
+    st = st[0]
+    if bool((st == THETA_UNDEFINED).any()):
+        raise ValueError("gama - f outside the theta branches of RD_single_pulse.py:87-90 "
+                         "(the reference would reuse a stale theta)")
+    keep = st == REACHABLE
+    return mx[0][keep], mn[0][keep]
+
+
+def Reachable_Domain(device="cuda"):
+    """RD_single_pulse.Reachable_Domain on the module `params`; returns the
+    (RF_max, RF_min) numpy point lists instead of the fitted ellipse."""
+    p = params
+    mx, mn = reachable_domain(p["a"], p["e0"], p["f"], p["delta_max"], p["N1"], p["N2"], p["N3"], p["u"], device)
+    return mx.cpu().numpy(), mn.cpu().numpy()
+
+
+def Incoming_parameters(data, delta_max, device="cuda"):
+    """RD_single_pulse.py:22-37: orbit elements data = [a, e, i, ., ., f]."""
+    params["a"], params["i"], params["e0"], params["f"] = data[0], data[2], data[1], data[5]
+    params["delta_max"] = delta_max
+    return Reachable_Domain(device)

@@ -163,3 +163,40 @@ def test_env_rk4_mode_differs_from_stm_only_through_propagation(oracle):
     r1, d1 = oracle.rollout(n, T, pa, ea, d_capture=15000.0, max_episode_steps=12, propagator=1, rk4_substeps=10)
     assert np.array_equal(d0, d1)                     # timeouts at the same steps, no captures either way
     assert not np.array_equal(r0, r1)
+
+
+# --- reachable-domain grid ---------------------------------
+def _rd_cases():
+    g = golden("rd_grid")
+    return g, int(g["ncases"])
+
+
+def test_reachable_domain_restatement_bitexact(oracle):
+    """RD_single_pulse.Reachable_Domain point lists (Curve_fitting replaced by
+    a recorder, tests/golden/capture_rd.py) vs the C restatement: bit-exact
+    against the glibc-libm capture, <= 4 ulp-ish against the as-is (SVML)
+    capture; the NaN points of the 0/0 direction (gama = f, alpha = 0) kept."""
+    g, n = _rd_cases()
+    for k in range(n):
+        a, e0, f, dm, u, n1, n2, n3 = g[f"prm_{k}"]
+        mx, mn = oracle.reachable_domain(a, e0, f, dm, int(n1), int(n2), int(n3), u)
+        for name, got in (("max", mx), ("min", mn)):
+            assert np.array_equal(got, g[f"rf{name}_glibc_{k}"], equal_nan=True), (k, name)
+            ref = g[f"rf{name}_{k}"]
+            assert got.shape == ref.shape
+            assert np.array_equal(np.isnan(got), np.isnan(ref))
+            ok = ~np.isnan(ref)
+            assert np.allclose(got[ok], ref[ok], rtol=1e-14, atol=1e-9), (k, name)
+
+
+def test_reachable_domain_grid_status(oracle):
+    """dV = 0 (N1 = 2, jj = 1) leaves at most alpha = 0 reachable; f = 0 puts
+    gama - f = 2 pi outside both theta branches (status 2, the reference
+    would reuse a stale theta) and the list API refuses it."""
+    mx, mn, st = oracle.reachable_domain_grid(2.4e7, 0.7, 2.5, 800.0, 2, 60, 60)
+    first = st[: 61 * 61].reshape(61, 61)
+    assert set(np.nonzero(first)[1]) <= {30} and (st == 1).sum() > 100
+    _, _, st0 = oracle.reachable_domain_grid(1e7, 0.2, 0.0, 500.0, 1, 40, 40)
+    assert (st0 == 2).sum() >= 1 and (st0.reshape(41, 41)[:-1] != 2).all()
+    with pytest.raises(ValueError):
+        oracle.reachable_domain(1e7, 0.2, 0.0, 500.0, 1, 40, 40)
