@@ -83,14 +83,20 @@ def cpu_baseline(seconds):
 
 def rd_cpu_baseline():
     """One reference-default reachable-domain grid (RD_single_pulse.py params
-    :9-20) on the C restatement, 1 core, ms per grid."""
+    :9-20) on the C restatement and its Curve_fitting on the numpy/scipy
+    restatement, 1 core: (ms per grid, ms per Curve_fitting)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    t0 = time.perf_counter()
+    import ellipse_oracle as EO
     reps = 3
+    t0 = time.perf_counter()
     for _ in range(reps):
-        O.reachable_domain_grid(1e7, 0.2, np.pi / 2, 500.0, 1, 200, 200)
-    return (time.perf_counter() - t0) / reps * 1e3
+        mx, mn = O.reachable_domain(1e7, 0.2, np.pi / 2, 500.0, 1, 200, 200)
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        EO.curve_fitting(mx, mn)
+    t2 = time.perf_counter()
+    return (t1 - t0) / reps * 1e3, (t2 - t1) / reps * 1e3
 
 
 def workload_name(a, world):
@@ -239,7 +245,15 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     rd_ms = e0.elapsed_time(e1) / rd_iters
-    del rd_out
+    ell, ell_info = RD.ellipse_fit(*rd_out)
+    e0.record()
+    for _ in range(rd_iters):
+        RD.ellipse_fit(*rd_out)
+    e1.record()
+    torch.cuda.synchronize()
+    ell_ms = e0.elapsed_time(e1) / rd_iters
+    ell_ok = int((ell_info > 0).sum())
+    del rd_out, ell, ell_info
 
     rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
     update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
@@ -291,7 +305,11 @@ def main():
                                  "sample": f"{rd_sets} random orbits x 201 x 201 directions (RD_single_pulse "
                                            "defaults N1=1, N2=N3=200), one launch incl. output zero-fill",
                                  "reachable_directions": rd_reach,
-                                 "cpu_oracle_ms_per_grid": rd_cpu_ms},
+                                 "cpu_oracle_ms_per_grid": rd_cpu_ms[0] if rd_cpu_ms else None,
+                                 "ellipse_fit_ms_per_launch": ell_ms,
+                                 "ellipse_fits_per_s": 2 * rd_sets / (ell_ms * 1e-3), "ellipse_fits_ok": ell_ok,
+                                 "grid_plus_fit_orbits_per_s": rd_sets / ((rd_ms + ell_ms) * 1e-3),
+                                 "cpu_oracle_ms_per_curve_fitting": rd_cpu_ms[1] if rd_cpu_ms else None},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

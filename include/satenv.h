@@ -154,6 +154,24 @@ typedef struct {
 int satenv_reachable_domain(int64_t nsets, const satenv_rd_orbit* orbits, int32_t n1, int32_t n2, int32_t n3,
                             double* rf_max, double* rf_min, uint8_t* status, void* stream);
 
+/* curve_fitting.Curve_fitting(RF_max, RF_min)  single_pluse_model/curve_fitting.py:475-576
+ * on the dense grids of satenv_reachable_domain (same rf_max / rf_min /
+ * status buffers, ndir directions per set), one workgroup per (set, envelope).
+ * ellipse_out f64 [nsets][2][5]: (xc, yc, a, b, theta) of the RF_max
+ * (farthest point per angular bin) and RF_min (nearest) ellipse, as the
+ * [2][5] array Curve_fitting returns.  info_out i32 [nsets][2]: > 0 the
+ * least-squares function evaluations; < 0 no fit (parameters NaN):
+ *   -1  a status-2 direction in the set (the reference's stale theta),
+ *   -2  more than 8192 distinct reachable points,
+ *   -3  fewer than 2 points, or fewer than 5 angular bins (5 parameters).
+ * Optional (nullable) intermediates: fit_points_out f64 [nsets][2][128][2]
+ * = the points the least squares fits (one per angular bin, the filtered
+ * set of :564, NaN-padded), center_out f64 [nsets][2][2] = the
+ * EllipticEnvelope location of :547.                                      */
+int satenv_ellipse_fit(int64_t nsets, int32_t ndir, const double* rf_max, const double* rf_min, const uint8_t* status,
+                       double* ellipse_out, int32_t* info_out, double* fit_points_out, double* center_out,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@
 
 #include "satenv.h"
 #include "satenv_device.h"
+#include "ellipse_device.h"
 
 using namespace satenv;
 
@@ -641,6 +642,19 @@ int satenv_reachable_domain(int64_t nsets, const satenv_rd_orbit* orbits, int32_
     return fail(SATENV_ERR_ARG, "satenv_reachable_domain: grid too large");
   hipLaunchKernelGGL(rd_kernel, dim3((unsigned)(nsets * tiles)), dim3(kRdBlock), 0, (hipStream_t)stream, orbits, n1,
                      n2, n3, (int32_t)ndir, (int32_t)tiles, rf_max, rf_min, status);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_ellipse_fit(int64_t nsets, int32_t ndir, const double* rf_max, const double* rf_min, const uint8_t* status,
+                       double* ellipse_out, int32_t* info_out, double* fit_points_out, double* center_out,
+                       void* stream) {
+  if (nsets <= 0 || ndir <= 0 || !rf_max || !rf_min || !status || !ellipse_out || !info_out)
+    return fail(SATENV_ERR_ARG, "satenv_ellipse_fit: bad args");
+  if (2 * nsets > INT32_MAX) return fail(SATENV_ERR_ARG, "satenv_ellipse_fit: too many sets");
+  hipLaunchKernelGGL(ellipse::ellipse_kernel, dim3((unsigned)(2 * nsets)), dim3(ellipse::kThreads), 0,
+                     (hipStream_t)stream, ndir, rf_max, rf_min, status, ellipse_out, info_out, fit_points_out,
+                     center_out);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

@@ -8,11 +8,13 @@ points max/min(|rf|) * P (:123-124).  Many orbits run in one launch
 (`reachable_domain_grid`), which is what a vectorised Flag-2 env needs; the
 reference runs one orbit per call at ~0.9 s.
 
+`ellipse_fit` restates curve_fitting.Curve_fitting (:475-576) as the
+satenv_ellipse_fit kernel on the same dense grids (no host round trip):
+EllipticEnvelope center, angular-bin filtering and scipy's trf least squares.
+
 `params` / `Incoming_parameters` / `Reachable_Domain` mirror the module's
-globals-driven API (:9-37) but return the point lists (RF_max, RF_min) that
-the reference hands to curve_fitting.Curve_fitting (:140); the ellipse fit
-itself is host-side sklearn/scipy post-processing and is not part of this
-engine.
+globals-driven API (:9-37, :40-148) and return the [2][5] ellipse array like
+the reference; `reachable_points` returns the RF_max / RF_min lists.
 """
 import numpy as np
 import torch
@@ -76,16 +78,58 @@ def reachable_domain(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14, dev
     return mx[0][keep], mn[0][keep]
 
 
-def Reachable_Domain(device="cuda"):
-    """RD_single_pulse.Reachable_Domain on the module `params`; returns the
-    (RF_max, RF_min) numpy point lists instead of the fitted ellipse."""
+ELL_STALE_THETA, ELL_TOO_MANY, ELL_TOO_FEW = -1, -2, -3
+
+
+def ellipse_fit(rf_max, rf_min, status, stream=None, intermediates=False):
+    """curve_fitting.Curve_fitting on dense grids from reachable_domain_grid:
+    returns (ellipse [nsets][2][5] f64 = (xc, yc, a, b, theta) of the RF_max
+    and RF_min envelopes, info [nsets][2] i32: > 0 least-squares function
+    evaluations, < 0 no fit (ELL_*; parameters NaN)).  intermediates=True
+    also returns the fitted point sets [nsets][2][128][2] (NaN-padded) and
+    the EllipticEnvelope centers [nsets][2][2]."""
+    nsets, ndir = status.shape
+    _lib.require_cuda(status, torch.uint8, (nsets, ndir), "status")
+    _lib.require_cuda(rf_max, torch.float64, (nsets, ndir, 3), "rf_max")
+    _lib.require_cuda(rf_min, torch.float64, (nsets, ndir, 3), "rf_min")
+    out = torch.empty((nsets, 2, 5), dtype=torch.float64, device=status.device)
+    info = torch.empty((nsets, 2), dtype=torch.int32, device=status.device)
+    fit = cen = None
+    if intermediates:
+        fit = torch.empty((nsets, 2, 128, 2), dtype=torch.float64, device=status.device)
+        cen = torch.empty((nsets, 2, 2), dtype=torch.float64, device=status.device)
+    check(_lib.lib().satenv_ellipse_fit(nsets, ndir, ptr(rf_max), ptr(rf_min), ptr(status), ptr(out), ptr(info),
+                                        ptr(fit) if fit is not None else None, ptr(cen) if cen is not None else None,
+                                        stream_ptr(stream)), "satenv_ellipse_fit")
+    return (out, info, fit, cen) if intermediates else (out, info)
+
+
+def reachable_ellipses(orbits, n1=1, n2=200, n3=200, stream=None):
+    """Grid + fit for every orbit: (ellipse [nsets][2][5], info [nsets][2])."""
+    return ellipse_fit(*reachable_domain_grid(orbits, n1, n2, n3, stream), stream=stream)
+
+
+def reachable_points(device="cuda"):
+    """The (RF_max, RF_min) numpy lists Reachable_Domain builds from `params` (:138-139)."""
     p = params
     mx, mn = reachable_domain(p["a"], p["e0"], p["f"], p["delta_max"], p["N1"], p["N2"], p["N3"], p["u"], device)
     return mx.cpu().numpy(), mn.cpu().numpy()
+
+
+def Reachable_Domain(device="cuda"):
+    """RD_single_pulse.Reachable_Domain (:40-148) on the module `params`:
+    the [2][5] ellipse array of Curve_fitting (:140)."""
+    p = params
+    orbits = orbits_tensor(p["a"], p["e0"], p["f"], p["delta_max"], p["u"], device)
+    ell, info = reachable_ellipses(orbits, p["N1"], p["N2"], p["N3"])
+    info = info.cpu().numpy()
+    if (info < 0).any():
+        raise ValueError(f"reachable-domain ellipse fit failed (info {info.tolist()}, see satenv_ellipse_fit)")
+    return ell[0].cpu().numpy()
 
 
 def Incoming_parameters(data, delta_max, device="cuda"):
     """RD_single_pulse.py:22-37: orbit elements data = [a, e, i, ., ., f]."""
     params["a"], params["i"], params["e0"], params["f"] = data[0], data[2], data[1], data[5]
     params["delta_max"] = delta_max
-    return Reachable_Domain(device)
+    return np.array(Reachable_Domain(device))

@@ -12,7 +12,11 @@ is, and with glibc arccos/arctan/tan (numpy's are SVML; see
 capture_golden.py), which pins the C oracle bit-exactly.
 
 Fixture rd_grid.npz: for case k, prm_k = [a, e0, f, delta_max, u, N1, N2, N3],
-rfmax_k / rfmin_k [m][3] (as is) and rfmax_glibc_k / rfmin_glibc_k.
+rfmax_k / rfmin_k [m][3] (as is), rfmax_glibc_k / rfmin_glibc_k, and ell_k
+[2][5] = the real Curve_fitting(rfmax_k, rfmin_k) (sklearn 1.7.2, scipy 1.15.3).
+Plus the reference's own golden pairs (data files, not code):
+pairs_in [r][5] = all_input.csv rows (a, e, i, f, fuel), pairs_out [r][10] =
+output_data.csv rows, pairs_rows = the row numbers.
 
 Run:  python tests/golden/capture_rd.py     (about a minute)
 """
@@ -69,6 +73,7 @@ def main():
         got["min"] = np.array(RF_min, dtype=np.float64).reshape(-1, 3)
         return np.zeros((2, 5))
 
+    real_fit = rd.cf.Curve_fitting
     rd.cf.Curve_fitting = recorder
     out = {}
     for k, (a, e0, f, dmax, n1, n2, n3) in enumerate(CASES):
@@ -78,8 +83,18 @@ def main():
         with glibc_libm(rd):
             rd.Reachable_Domain()
         out[f"rfmax_glibc_{k}"], out[f"rfmin_glibc_{k}"] = got["max"], got["min"]
+        out[f"ell_{k}"] = real_fit(out[f"rfmax_{k}"], out[f"rfmin_{k}"])
         out[f"prm_{k}"] = np.array([a, e0, f, dmax, rd.params["u"], n1, n2, n3], dtype=np.float64)
         print(k, out[f"rfmax_{k}"].shape, out[f"rfmax_glibc_{k}"].shape)
+    import csv
+    d = os.path.join(REF, "single_pluse_model")
+    with open(os.path.join(d, "all_input.csv")) as fi, open(os.path.join(d, "output_data.csv")) as fo:
+        rin = [list(map(float, r)) for r in list(csv.reader(fi))[1:]]
+        rout = [list(map(float, r)) for r in list(csv.reader(fo))[1:]]
+    rows = sorted({0, 1, 100, 400, 800} | set(np.random.default_rng(0).choice(len(rin), 7, replace=False).tolist()))
+    out["pairs_rows"] = np.array(rows)
+    out["pairs_in"] = np.array([rin[r] for r in rows])
+    out["pairs_out"] = np.array([rout[r] for r in rows])
     np.savez_compressed(os.path.join(OUT, "rd_grid.npz"), ncases=np.array(len(CASES)), **out)
 
 

@@ -96,3 +96,183 @@ def test_rd_theta_branch_gap_reported(rd, oracle):
     assert np.array_equal(st[0].cpu().numpy(), ost)
     with pytest.raises(ValueError):
         rd.reachable_domain(1e7, 0.2, 0.0, 500.0, 1, 40, 40, device="cuda:0")
+
+
+# --- Curve_fitting on the GPU (satenv_ellipse_fit) --------------------------------
+# Parity bar.  Fits are compared through the implicit ellipse function on the
+# fitted points ("gap"; theta alone is meaningless when a ~ b).
+#  - phases A-D (points, center, angular filter) vs the restatement on the
+#    GPU's own grid: centers 1e-12, fitted points 1e-12;
+#  - phase E (scipy's trf) vs scipy's least_squares on the GPU's own fitted
+#    points: gap < 1e-4 where the instance is well posed for scipy itself
+#    (scipy, the numpy trf restatement and scipy on 1e-15-perturbed points
+#    agree to 1e-4); on ill-posed instances (near-circular envelopes, where
+#    x_scale 1 lets theta random-walk) the GPU fit's cost is within 5% of
+#    scipy's;
+#  - end to end vs the reference's stored ellipses wherever the reference is
+#    itself reproducible: the same instance run with glibc instead of SVML
+#    libm (or the oracle grid for the CSV pairs) gives the same ellipse.  The
+#    reference is not reproducible on some instances: one exact duplicate
+#    more or less in np.unique moves its MCD center by up to 10%.
+def _resid(p, fp):
+    import ellipse_oracle as E
+    return E.residuals(p, fp[:, 0], fp[:, 1])
+
+
+def _gap(p, q, fp):
+    return np.abs(_resid(p, fp) - _resid(q, fp)).max()
+
+
+def _cost(p, fp):
+    return 0.5 * float(np.sum(_resid(p, fp) ** 2))
+
+
+def _points(fit, s, j):
+    p = fit[s, j].cpu().numpy()
+    return p[~np.isnan(p[:, 0])]
+
+
+def _solver_probes(fp, n=10):
+    """scipy's least_squares on the points and on n copies with 1e-16
+    relative noise, plus the numpy trf restatement: the outcomes the
+    reference's own solver produces at its rounding level."""
+    import ellipse_oracle as E
+    rng = np.random.default_rng(0)
+    out = [E.fit_ellipse(fp), E.trf_restated(fp)[0]]
+    for _ in range(n):
+        out.append(E.fit_ellipse(fp * (1 + 1e-16 * rng.standard_normal(fp.shape))))
+    return out
+
+
+def _check_solver(ell, fp, what, tol=1e-4):
+    """phase E vs scipy on the same points; returns True if well posed."""
+    probes = _solver_probes(fp)
+    sc = probes[0]
+    if all(_gap(p, sc, fp) < tol for p in probes):
+        assert _gap(ell, sc, fp) < tol, (what, ell, sc)
+        return True
+    # ill posed: the GPU lands on one of the reference's own outcomes, or no worse than the worst of them
+    near = min(_gap(ell, p, fp) for p in probes)
+    assert near < 10 * tol or _cost(ell, fp) <= 1.001 * max(_cost(p, fp) for p in probes), (what, near)
+    return False
+
+
+def test_ellipse_intermediates_vs_oracle(rd):
+    """Phases A-D of the kernel (gather, np.unique order, EllipticEnvelope
+    center, angular-bin filtering) on the GPU's own grid vs the restatement
+    on the same points: centers to 1e-12; fitted point sequences equal up to
+    the pick between near-duplicate points (gama = 0 vs 2 pi, +-alpha pairs),
+    which an ulp of the center decides."""
+    import ellipse_oracle as E
+    g = golden("rd_grid")
+    for k in range(int(g["ncases"])):
+        a, e0, f, dm, u, n1, n2, n3 = g[f"prm_{k}"]
+        orbits = rd.orbits_tensor(a, e0, f, dm, u, device="cuda:0")
+        mx, mn, st = rd.reachable_domain_grid(orbits, int(n1), int(n2), int(n3))
+        _, info, fit, cen = rd.ellipse_fit(mx, mn, st, intermediates=True)
+        assert (info > 0).all()
+        keep = (st[0] == 1).cpu().numpy()
+        for j, data in enumerate((mx[0].cpu().numpy()[keep], mn[0].cpu().numpy()[keep])):
+            pts = E.unique_points(data)
+            c = E.mcd_center(pts)
+            np.testing.assert_allclose(cen[0, j].cpu().numpy(), c, rtol=1e-12, atol=0)
+            fp = E.filter_points(pts, c, j == 0)
+            got = _points(fit, 0, j)
+            assert got.shape == fp.shape, (k, j)
+            np.testing.assert_allclose(got, fp, rtol=0, atol=1e-12 * np.abs(fp).max())
+
+
+def _grid_points(grid, s):
+    mx, mn, st = grid
+    keep = (st[s] == 1).cpu().numpy()
+    return mx[s].cpu().numpy()[keep], mn[s].cpu().numpy()[keep]
+
+
+def test_ellipse_fit_vs_reference_curve_fitting(rd):
+    """GPU grid + GPU fit vs the reference's Curve_fitting on its own point
+    lists (rd_grid.npz ell_k), wherever the reference's pipeline itself
+    reproduces that ellipse from the GPU's grid (its np.unique / MCD / bin
+    steps are discontinuous in the last ulp of the grid)."""
+    import ellipse_oracle as E
+    g = golden("rd_grid")
+    checked = 0
+    for k in range(int(g["ncases"])):
+        a, e0, f, dm, u, n1, n2, n3 = g[f"prm_{k}"]
+        orbits = rd.orbits_tensor(a, e0, f, dm, u, device="cuda:0")
+        grid = rd.reachable_domain_grid(orbits, int(n1), int(n2), int(n3))
+        ell, info, fit, _ = rd.ellipse_fit(*grid, intermediates=True)
+        assert (info > 0).all(), (k, info)
+        alt = E.curve_fitting(*_grid_points(grid, 0))
+        for j in range(2):
+            fp = _points(fit, 0, j)
+            e = ell[0, j].cpu().numpy()
+            _check_solver(e, fp, (k, j))
+            ref = g[f"ell_{k}"][j]
+            if _gap(alt[j], ref, fp) < 1e-4:
+                assert _gap(e, ref, fp) < 1e-4, (k, j, e, ref)
+                checked += 1
+    assert checked >= 4
+
+
+def test_ellipse_fit_golden_pairs(rd):
+    """all_input.csv -> output_data.csv rows (the reference's golden pairs)
+    in one batched launch pair, to the pairs' own reproducibility (1e-3),
+    wherever the reference's pipeline reproduces the pair from the GPU grid."""
+    import ellipse_oracle as E
+    g = golden("rd_grid")
+    inp = g["pairs_in"]
+    orbits = rd.orbits_tensor(inp[:, 0], inp[:, 1], inp[:, 3], inp[:, 4], device="cuda:0")
+    grid = rd.reachable_domain_grid(orbits)
+    ell, info, fit, _ = rd.ellipse_fit(*grid, intermediates=True)
+    assert (info > 0).all(), info
+    checked = 0
+    for s, (row, out) in enumerate(zip(g["pairs_rows"], g["pairs_out"])):
+        ref = out.reshape(2, 5)
+        alt = E.curve_fitting(*_grid_points(grid, s))
+        for j in range(2):
+            fp = _points(fit, s, j)
+            e = ell[s, j].cpu().numpy()
+            _check_solver(e, fp, (row, j))
+            if _gap(alt[j], ref[j], fp) < 1e-3:
+                assert _gap(e, ref[j], fp) < 1e-3, (row, j, e, ref[j])
+                checked += 1
+    assert checked >= len(inp)
+
+
+def test_ellipse_fit_random_orbits_vs_oracle(rd, oracle):
+    """64 random orbits in one launch: every fit the restatement says is
+    possible is made, results are deterministic, phase E matches scipy."""
+    import ellipse_oracle as E
+    rng = np.random.default_rng(3)
+    n = 64
+    a = rng.uniform(7e6, 5e7, n)
+    e0 = rng.uniform(0.0, 0.6, n)
+    f = rng.uniform(0.05, 2 * np.pi - 0.05, n)
+    dm = rng.uniform(100.0, 800.0, n)
+    orbits = rd.orbits_tensor(a, e0, f, dm, device="cuda:0")
+    grid = rd.reachable_domain_grid(orbits, 1, 120, 160)
+    ell, info, fit, _ = rd.ellipse_fit(*grid, intermediates=True)
+    ell2, info2 = rd.ellipse_fit(*grid)
+    assert torch.equal(ell.nan_to_num(), ell2.nan_to_num()) and torch.equal(info, info2)   # deterministic
+    ell, info = ell.cpu().numpy(), info.cpu().numpy()
+    fitted = posed = 0
+    for s in range(n):
+        mx, mn = oracle.reachable_domain(a[s], e0[s], f[s], dm[s], 1, 120, 160)
+        for j, data in enumerate((mx, mn)):
+            pts = E.unique_points(data)
+            if len(pts) < 2 or len(set(np.digitize(np.arctan2(*(pts - E.mcd_center(pts)).T[::-1]),
+                                                   E.bin_edges()))) < 5:
+                assert info[s, j] == rd.ELL_TOO_FEW, (s, j)
+                continue
+            fitted += 1
+            assert info[s, j] > 0, (s, j, info[s, j])
+            posed += _check_solver(ell[s, j], _points(fit, s, j), (s, j))
+    assert fitted >= n and posed >= fitted - 8
+
+
+def test_ellipse_fit_reports_stale_theta(rd):
+    orbits = rd.orbits_tensor([1e7, 1e7], [0.2, 0.2], [0.0, 1.0], [500.0, 500.0], device="cuda:0")
+    ell, info = rd.reachable_ellipses(orbits, 1, 40, 40)
+    info = info.cpu().numpy()
+    assert (info[0] == rd.ELL_STALE_THETA).all() and (info[1] > 0).all(), info
+    assert torch.isnan(ell[0]).all()
