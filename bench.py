@@ -26,6 +26,8 @@ sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
 METRIC = "env-steps/sec + PPO updates/sec at N_envs=16384, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3     # MI355X_MICROARCH.md: FP32 matrix 157.3 TF spec
+BF16_MFMA_PEAK_TFS = 2500.0    # MI355X_MICROARCH.md: dense BF16 matrix ~2.5 PF
+SURROGATE_FLOP_PER_ENV = 2 * (5 * 256 + 256 * 128 + 128 * 64 + 64 * 10)   # ImprovedNN forward, algorithmic
 ENV_BYTES_PER_STEP = 381       # DESIGN.md "Roofline": state 16 f64 + 3 i32 planes r/w, actions, obs, reward, done
 
 
@@ -43,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
+    ap.add_argument("--surrogate", action="store_true",
+                    help="config 5: ImprovedNN surrogate (bf16) evaluated on every env step of the rollout")
     return ap.parse_args()
 
 
@@ -103,7 +107,11 @@ def workload_name(a, world):
     """Which BASELINE.json config this run is (configs[1..3]), or a plain description."""
     desc = (f"num_envs={a.num_envs}/GPU x {world} GPU, hidden={a.hidden}, horizon={a.horizon}, GAE lambda=0.95, "
             f"minibatch={a.minibatch}, {a.epochs} PPO epochs")
+    if a.surrogate:
+        desc += ", ImprovedNN surrogate bf16 per env-step"
     if a.horizon == 2048 and a.minibatch == 4096 and a.epochs == 10:
+        if world == 1 and a.num_envs == 16384 and a.hidden == 256 and a.surrogate:
+            return "BASELINE.json configs[4]: " + desc
         if world == 1 and a.num_envs == 16384 and a.hidden == 256:
             return "BASELINE.json configs[2]: " + desc
         if world == 1 and a.num_envs == 4096 and a.hidden == 64:
@@ -131,7 +139,7 @@ def main():
     from satrl.trainer import VecTrainer, args_param
     args = args_param(batch_size=a.num_envs * a.horizon, mini_batch_size=a.minibatch, hidden_width=a.hidden,
                       K_epochs=a.epochs, max_episode_steps=1000, num_envs=a.num_envs, horizon=a.horizon, seed=0,
-                      max_train_steps=int(3e6), chkpt_dir="/tmp")
+                      max_train_steps=int(3e6), chkpt_dir="/tmp", surrogate=a.surrogate)
     tr = VecTrainer(args, flag=0, d_capture=a.d_capture, pg=pg, env_offset=rank * a.num_envs)
 
     def barrier():
@@ -255,6 +263,21 @@ def main():
     ell_ok = int((ell_info > 0).sum())
     del rd_out, ell, ell_info
 
+    # ---- config 5 kernel: ImprovedNN surrogate (bf16 MFMA) on every env's current orbit
+    from satrl.surrogate import Surrogate
+    sur = tr.surrogate if tr.surrogate is not None else Surrogate(device="cuda", seed=0)
+    sur_out = torch.empty((a.num_envs, 10), dtype=torch.float32, device="cuda")
+    for _ in range(10):
+        sur.env_forward(env, out=sur_out)
+    e0.record()
+    for _ in range(a.kernel_iters):
+        sur.env_forward(env, out=sur_out)
+    e1.record()
+    torch.cuda.synchronize()
+    sur_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+    sur_flop = a.num_envs * SURROGATE_FLOP_PER_ENV
+    sur_tfs = sur_flop / (sur_us * 1e-6) / 1e12
+
     rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
     update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
     gae_ms = sum(timers["gae_ms"]) / len(timers["gae_ms"])
@@ -301,6 +324,13 @@ def main():
                             "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
                             "env_rk4_cw_avg_launch_us": env_rk_us,
                             "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6)},
+            "surrogate": {"kernel": "satenv_surrogate (ImprovedNN 5-256-128-64-10, bf16 MFMA 16x16x32, f32 acc)",
+                          "in_rollout": bool(a.surrogate), "avg_launch_us": sur_us,
+                          "env_steps_per_s": a.num_envs / (sur_us * 1e-6), "bound": "mfma",
+                          "achieved": sur_tfs, "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": sur_tfs / BF16_MFMA_PEAK_TFS, "flop_per_env": SURROGATE_FLOP_PER_ENV,
+                          "note": "latency bound: 91 KB of packed weights staged into LDS per workgroup; "
+                                  "FP64 orbital elements per env"},
             "reachable_domain": {"grids_per_s": rd_sets / (rd_ms * 1e-3), "ms_per_launch": rd_ms,
                                  "sample": f"{rd_sets} random orbits x 201 x 201 directions (RD_single_pulse "
                                            "defaults N1=1, N2=N3=200), one launch incl. output zero-fill",

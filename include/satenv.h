@@ -172,6 +172,24 @@ int satenv_ellipse_fit(int64_t nsets, int32_t ndir, const double* rf_max, const 
                        double* ellipse_out, int32_t* info_out, double* fit_points_out, double* center_out,
                        void* stream);
 
+/* config 5: the ImprovedNN surrogate (single_pluse_model/model.py:7-24,
+ * 5 -> 256 -> 128 -> 64 -> 10, ReLU, inference: no dropout) in bf16 with f32
+ * accumulation, as network_method_process (real_time_data_process.py:112-125)
+ * evaluates it on [a, e, i, f, fuel_c] of the pursuer's absolute orbit (the
+ * reference's call site environment.py:158 is commented out; the output is
+ * the env's ellipse_params and feeds no reward).
+ * blob: device buffer of satenv_surrogate_blob_bytes() bytes, filled by
+ * satenv_surrogate_pack from the torch Linear parameters (f32 device
+ * arrays, weight [out][in] row-major: w1 [256][5], w2 [128][256], w3 [64][128],
+ * w4 [10][64]).  satenv_surrogate: out f32 [N][10] from the handle's current
+ * state (NaN rows where the orbit has no 6-element set).
+ * satenv_surrogate_mlp: the same network on given features x f32 [n][5].   */
+int satenv_surrogate_blob_bytes(void);
+int satenv_surrogate_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                          const float* b3, const float* w4, const float* b4, void* blob, void* stream);
+int satenv_surrogate(satenv_env* h, const void* blob, float* out, void* stream);
+int satenv_surrogate_mlp(int64_t n, const float* x, const void* blob, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

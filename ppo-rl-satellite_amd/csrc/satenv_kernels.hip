@@ -18,6 +18,7 @@
 #include "satenv.h"
 #include "satenv_device.h"
 #include "ellipse_device.h"
+#include "surrogate_device.h"
 
 using namespace satenv;
 
@@ -432,6 +433,82 @@ __global__ void __launch_bounds__(kRdBlock) rd_kernel(const satenv_rd_orbit* __r
   }
 }
 
+// ---------------------------------------------------------------------------
+// config 5: ImprovedNN surrogate (bf16 MFMA) on the pursuer's current orbit,
+// network_method_process real_time_data_process.py:112-125.  x == nullptr:
+// features from the env state (relative_state_to_absolute_state
+// environment.py:334-343 -> calculate_orbital_elements :11-105 -> [a, e, i, f,
+// fuel_c] as float32); else x [n][5] f32 directly.  Envs whose orbit has no
+// 6-element set (e == 0 / parabolic: the reference builds a 4-feature input
+// and crashes) get NaN outputs.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(surrogate::kThreads) surrogate_kernel(const Params prm, int64_t n,
+                                                                        const double* __restrict__ f64,
+                                                                        const float* __restrict__ x,
+                                                                        const uint8_t* __restrict__ blob,
+                                                                        float* __restrict__ out) {
+  using namespace surrogate;
+  __shared__ __align__(16) uint8_t lds[kBlobBytes];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(blob);
+    uint4* dst = reinterpret_cast<uint4*>(lds);
+    for (int i = threadIdx.x; i < kBlobBytes / 16; i += kThreads) dst[i] = src[i];
+  }
+  __syncthreads();
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(lds);
+  const float* Bs = reinterpret_cast<const float*>(lds + kBiasOffBytes);
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile * 16 < n; tile += (int64_t)gridDim.x * 4) {
+    const int64_t env = tile * 16 + c;
+    const bool valid = env < n;
+    frag_ab in1[1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) in1[0][k] = 0;
+    int ok = 0;
+    if (g == 0 && valid) {
+      float fv[kIn];
+      if (x) {
+#pragma unroll
+        for (int k = 0; k < kIn; ++k) fv[k] = x[env * kIn + k];
+        ok = 1;
+      } else {
+        Elements E;
+        const int rc = orbital_elements(3.986e14, prm.R_cw[0] + f64[0 * n + env], prm.R_cw[1] + f64[1 * n + env],
+                                        prm.R_cw[2] + f64[2 * n + env], prm.V_cw[0] + f64[3 * n + env],
+                                        prm.V_cw[1] + f64[4 * n + env], prm.V_cw[2] + f64[5 * n + env], E);
+        ok = rc == 0;
+        fv[0] = (float)E.a; fv[1] = (float)E.e; fv[2] = (float)E.i; fv[3] = (float)E.f;
+        fv[4] = (float)f64[12 * n + env];
+      }
+#pragma unroll
+      for (int k = 0; k < kIn; ++k) in1[0][k] = (short)f2bf(fv[k]);
+    }
+    ok = __shfl(ok, c, 64);
+    frag_ab h1[8], h2[4], h3[2];
+    layer<16, 1, kW1Row>(W + kW1Off, Bs, in1, h1);
+    layer<8, 8, kW2Row>(W + kW2Off, Bs + kH1, h1, h2);
+    layer<4, 4, kW3Row>(W + kW3Off, Bs + kH1 + kH2, h2, h3);
+    frag_cd acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const unsigned short* row = W + kW4Off + c * kW4Row + 8 * g;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_frag(row + 32 * s2), h3[s2], acc, 0, 0, 0);
+    if (valid) {
+      const float* b4 = Bs + kH1 + kH2 + kH3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 4 * g + i;
+        if (o < kOut) out[env * kOut + o] = ok ? acc[i] + b4[o] : __uint_as_float(0x7fc00000u);
+      }
+    }
+  }
+}
+
+int surrogate_grid(int64_t n) {
+  const int64_t tiles = (n + 63) / 64;
+  return (int)(tiles < 1024 ? tiles : 1024);
+}
+
 }  // namespace
 
 struct satenv_env {
@@ -655,6 +732,36 @@ int satenv_ellipse_fit(int64_t nsets, int32_t ndir, const double* rf_max, const 
   hipLaunchKernelGGL(ellipse::ellipse_kernel, dim3((unsigned)(2 * nsets)), dim3(ellipse::kThreads), 0,
                      (hipStream_t)stream, ndir, rf_max, rf_min, status, ellipse_out, info_out, fit_points_out,
                      center_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_surrogate_blob_bytes(void) { return surrogate::kBlobBytes; }
+
+int satenv_surrogate_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                          const float* b3, const float* w4, const float* b4, void* blob, void* stream) {
+  if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !w4 || !b4 || !blob)
+    return fail(SATENV_ERR_ARG, "satenv_surrogate_pack: null pointer");
+  hipLaunchKernelGGL(surrogate::pack_kernel, dim3(64), dim3(256), 0, (hipStream_t)stream, w1, b1, w2, b2, w3, b3, w4,
+                     b4, (uint8_t*)blob);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_surrogate(satenv_env* h, const void* blob, float* out, void* stream) {
+  if (!h || !blob || !out) return fail(SATENV_ERR_ARG, "satenv_surrogate: null pointer");
+  hipLaunchKernelGGL(surrogate_kernel, dim3(surrogate_grid(h->n)), dim3(surrogate::kThreads), 0, (hipStream_t)stream,
+                     h->prm, h->n, h->f64, nullptr, (const uint8_t*)blob, out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_surrogate_mlp(int64_t n, const float* x, const void* blob, float* out, void* stream) {
+  if (n <= 0 || !x || !blob || !out) return fail(SATENV_ERR_ARG, "satenv_surrogate_mlp: bad args");
+  satenv_params prm;
+  std::memset(&prm, 0, sizeof(prm));
+  hipLaunchKernelGGL(surrogate_kernel, dim3(surrogate_grid(n)), dim3(surrogate::kThreads), 0, (hipStream_t)stream, prm,
+                     n, nullptr, x, (const uint8_t*)blob, out);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

@@ -74,6 +74,10 @@ _SIGS = {
     "satenv_solve_alpha": ([_i64, _vp, _vp, _vp], C.c_int),
     "satenv_rk4_j2": ([_i64, _vp, C.c_double, _i32, _vp, _vp], C.c_int),
     "satenv_reachable_domain": ([_i64, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_surrogate_blob_bytes": ([], C.c_int),
+    "satenv_surrogate_pack": ([_vp] * 10, C.c_int),
+    "satenv_surrogate": ([_vp, _vp, _vp, _vp], C.c_int),
+    "satenv_surrogate_mlp": ([_i64, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_ellipse_fit": ([_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_gae": ([_i64, _i64, _vp, _vp, _vp, C.c_float, C.c_float, _vp, _vp, _vp], C.c_int),
     "satrl_gaussian_sample": ([_i64, _vp, _vp, C.c_float, C.c_uint64, C.c_uint32, _i64, C.c_uint64, _vp, _vp, _vp,

@@ -35,7 +35,8 @@ class args_param:  # noqa: N801
                  use_state_norm=True, use_reward_norm=False, use_reward_scaling=True, entropy_coef=0.01,
                  use_lr_decay=True, use_grad_clip=True, use_orthogonal_init=True, set_adam_eps=True, use_tanh=True,
                  chkpt_dir="/mnt/datab/home/yuanwenzheng/PICTURE1",
-                 num_envs=1, horizon=None, seed=0, rollout_graph_chunk=64, update_graph_group=16, device=None):
+                 num_envs=1, horizon=None, seed=0, rollout_graph_chunk=64, update_graph_group=16, device=None,
+                 surrogate=False):
         self.max_train_steps = max_train_steps
         self.evaluate_freq = evaluate_freq
         self.save_freq = save_freq
@@ -69,6 +70,9 @@ class args_param:  # noqa: N801
         self.rollout_graph_chunk = rollout_graph_chunk
         self.update_graph_group = update_graph_group
         self.device = device
+        # config 5: evaluate the ImprovedNN surrogate (bf16) on every env step into
+        # VecTrainer.ellipse_params (environment.py:158); a path or state_dict loads weights
+        self.surrogate = surrogate
         # set by the train_* functions from the env (CPPO_main.py:99-101)
         self.state_dim = 18
         self.action_dim = 3
@@ -212,6 +216,13 @@ class VecTrainer:
         self.iteration_count = 0
         self.rollout_steps = 0
         self.episodes = 0.0
+        self.surrogate = None
+        self.ellipse_params = None
+        if getattr(args, "surrogate", False):
+            from .surrogate import Surrogate
+            sd = args.surrogate if isinstance(args.surrogate, (str, dict)) else None
+            self.surrogate = Surrogate(device=self.device, seed=self.seed, state_dict=sd)
+            self.ellipse_params = torch.zeros((self.N, 10), dtype=torch.float32, device=self.device)
         self.env.reset(self.flag, obs_out=self.buf.obs[0])
 
     def _broadcast_params(self):
@@ -233,6 +244,8 @@ class VecTrainer:
         policy_act(self.pursuer.H, obs_t, self.pursuer.P, self.evader.P, 1.6, self.seed, self.env_offset, t,
                    pa, plp, ea, elp, step_base=self.step_base)
         self.env.step_autoreset(pa, ea, obs_out=buf.obs[t + 1], reward_out=buf.rew[t], done_out=buf.done[t])
+        if self.surrogate is not None:            # env.ellipse_params of the state the policy sees next
+            self.surrogate.env_forward(self.env, out=self.ellipse_params)
 
     def set_flag(self, flag):
         """Switch the learning agent (Flag 0: pursuer, CPPO_main.py:94-161;

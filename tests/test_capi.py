@@ -76,3 +76,20 @@ def test_reference_module_name_shims():
     assert rb.ReplayBuffer is satrl.buffer.ReplayBuffer
     assert main.args_param is satrl.trainer.args_param
     assert main.train_pursuer_network is satrl.trainer.train_pursuer_network
+
+
+def test_improvednn_matches_reference_state_dict():
+    """satrl.surrogate.ImprovedNN has the reference's parameter names/shapes:
+    MLPNet2.pth (single_pluse_model/) loads with weights_only=True.  Runs only
+    where the reference checkout exists (the build container)."""
+    import os
+    import torch
+    path = "/root/reference/single_pluse_model/MLPNet2.pth"
+    if not os.path.exists(path):
+        pytest.skip("reference checkout not present")
+    from satrl.surrogate import ImprovedNN
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    net = ImprovedNN()
+    net.load_state_dict(sd)
+    out = net(torch.zeros(1, 5))
+    assert out.shape == (1, 10) and torch.isfinite(out).all()
