@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="init the nccl process group even at world size 1 (rehearses the DP update path)")
     ap.add_argument("--surrogate", action="store_true",
                     help="config 5: ImprovedNN surrogate (bf16) evaluated on every env step of the rollout")
     return ap.parse_args()
@@ -131,8 +133,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     pg = None
-    if world > 1:
+    if world > 1 or a.force_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         pg = dist.group.WORLD
 

@@ -62,6 +62,14 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
 int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, const float* p1, const float* pt,
                      float* G, double* nsq, double* steps, void* stream);
 
+/* Data parallelism, after the all-reduce (SUM) of G over `world` ranks:
+ * G /= world (IEEE division, = torch's div_ of the gradient average), then
+ * satrl_ppo_reduce mode 2 on it.  One launch, so mode 1 | ncclAllReduce |
+ * this | satrl_ppo_adam is a single-stream chain a hipGraph captures whole.
+ * Replaces the per-minibatch gradient of PPO_continuous.update
+ * (ppo_continuous.py:227-239) for a minibatch spread over the ranks.       */
+int satrl_ppo_reduce_dp(int H, int mb, int net, int world, float* G, double* nsq, double* steps, void* stream);
+
 /* clip_grad_norm_(max_norm) per net (use_clip) + torch Adam (lerp form) per
  * net: lr [2] f32 device; bct f64 [bct_len][2] = {1 - beta1**k, sqrt(1 -
  * beta2**k)} for step k computed on the host with python-float math (as

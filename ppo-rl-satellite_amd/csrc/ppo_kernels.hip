@@ -640,6 +640,10 @@ constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
+// IEEE division per component, as torch's G.div_(world) after the all-reduce
+__device__ __forceinline__ float4 f4div(float4 a, float d) {
+  return make_float4(a.x / d, a.y / d, a.z / d, a.w / d);
+}
 __device__ __forceinline__ double sq4(float4 v) {
   return (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
 }
@@ -680,7 +684,7 @@ __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
 __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode, const float* __restrict__ p2,
                                                      const float* __restrict__ p1, const float* __restrict__ pt,
                                                      float* __restrict__ G, double* __restrict__ nsq,
-                                                     double* __restrict__ steps) {
+                                                     double* __restrict__ steps, int world) {
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float4 red[256];
@@ -701,6 +705,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
       if (lead && valid) G4[col] = v;
     } else if (lead && valid) {
       v = G4[col];
+      if (world > 1) { v = f4div(v, (float)world); G4[col] = v; }
     }
     if (lead && valid) {
       if (net) sc += sq4(v); else sa += sq4(v);
@@ -716,6 +721,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
       if (lead && valid) G4[L.W1 / 4 + col] = v;
     } else if (lead && valid) {
       v = G4[L.W1 / 4 + col];
+      if (world > 1) { v = f4div(v, (float)world); G4[L.W1 / 4 + col] = v; }
     }
     if (lead && valid) {
       if (col * 4 >= (int64_t)H * 20) sc += sq4(v); else sa += sq4(v);
@@ -731,6 +737,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
       if (lead && valid) G4[L.b2 / 4 + col] = v;
     } else if (lead && valid) {
       v = G4[L.b2 / 4 + col];
+      if (world > 1) { v = f4div(v, (float)world); G4[L.b2 / 4 + col] = v; }
     }
     if (lead && valid) {
       if (net_of(L, L.b2 + col * 4, H)) sc += sq4(v); else sa += sq4(v);
@@ -945,7 +952,16 @@ int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, c
   if ((mode & 2) && (!nsq || !steps)) return -1;
   const RedGeom g = geom(H, mb, S, net);
   hipLaunchKernelGGL(reduce_kernel, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1, pt, G,
-                     nsq, steps);
+                     nsq, steps, 1);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_ppo_reduce_dp(int H, int mb, int net, int world, float* G, double* nsq, double* steps, void* stream) {
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || world < 1 || !G || !nsq || !steps) return -1;
+  const RedGeom g = geom(H, mb, 1, net);
+  hipLaunchKernelGGL(reduce_kernel, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, 2, nullptr, nullptr,
+                     nullptr, G, nsq, steps, world);
   LAUNCH_CHECK();
   return 0;
 }

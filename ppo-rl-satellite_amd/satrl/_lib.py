@@ -90,6 +90,7 @@ _SIGS = {
     "satrl_ppo_dw2_splits": ([C.c_int, C.c_int], C.c_int),
     "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
                         C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp,

@@ -5,6 +5,9 @@ per update, one all-reduce of the flat gradient per minibatch (both nets,
 one bucket, before clipping so every rank clips identically), and the
 episode-statistics sum.  Plain torch.distributed calls on whatever device
 the tensors live on: RCCL over xGMI on the GPUs, gloo in the CPU tests.
+(On the GPUs the per-minibatch gradient all-reduce goes through
+satrl.rccl instead, on the compute stream, so that it is captured in the
+update's hipGraphs.)
 ``pg=None`` means a single process (every function is then local)."""
 from __future__ import annotations
 
@@ -60,6 +63,15 @@ def average_(flat: torch.Tensor, pg) -> torch.Tensor:
         import torch.distributed as dist
         dist.all_reduce(flat, group=pg)
         flat.div_(world_size(pg))
+    return flat
+
+
+def sum_inplace_(flat: torch.Tensor, pg) -> torch.Tensor:
+    """Per minibatch, c10d form: SUM of every rank's gradient in place (the
+    division by the world size happens in satrl_ppo_reduce_dp)."""
+    if pg is not None:
+        import torch.distributed as dist
+        dist.all_reduce(flat, group=pg)
     return flat
 
 

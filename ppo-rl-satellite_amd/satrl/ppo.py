@@ -26,6 +26,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import dist as _dist
+from . import rccl as _rccl
 from ._lib import check, ptr, stream_ptr
 
 LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
@@ -281,9 +282,13 @@ class FusedMinibatch:
         else:
             check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        None, None, sp), "satrl_ppo_reduce")
-            _dist.average_(L.G, L.pg)                                         # one bucket, both nets
-            check(lib.satrl_ppo_reduce(H, mb, net, S, 2, None, None, None, ptr(L.G), ptr(nsq), ptr(L.steps), sp),
-                  "satrl_ppo_reduce")
+            # one bucket, both nets: SUM over the ranks, then G /= world and the norms in one launch
+            if L.comm is not None:
+                L.comm.all_reduce_sum_(L.G)                                   # RCCL on this stream (capturable)
+            else:
+                _dist.sum_inplace_(L.G, L.pg)                                 # c10d (gloo in the CPU tests)
+            check(lib.satrl_ppo_reduce_dp(H, mb, net, _dist.world_size(L.pg), ptr(L.G), ptr(nsq), ptr(L.steps), sp),
+                  "satrl_ppo_reduce_dp")
         check(lib.satrl_ppo_adam(H, mb, net, ptr(nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
                                  float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
                                  ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
@@ -324,6 +329,8 @@ class FusedMinibatch:
                 with torch.cuda.stream(self.side if net == 1 else torch.cuda.current_stream()):
                     self._dw2(self.H1, self.dZ2, self.mb, self.S, net)
             torch.cuda.synchronize()
+        if self.L.comm is not None:
+            self.L.comm.warm(self.L.G)        # RCCL connects lazily: never inside the capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.current_stream().wait_stream(s)
@@ -337,7 +344,7 @@ class FusedMinibatch:
         B = perm.numel()
         mb, G = self.mb, self.group
         nfull = B // mb
-        graphable = self.use_graph and self.L.pg is None and torch.cuda.is_available()
+        graphable = self.use_graph and torch.cuda.is_available() and (self.L.pg is None or self.L.comm is not None)
         k = 0
         while k < nfull:
             ng = min(G, nfull - k)
@@ -402,6 +409,9 @@ class PPOLearner:
         self.beta1, self.beta2 = 0.9, 0.999                  # torch.optim.Adam defaults
         self.adam_eps = 1e-5 if args.set_adam_eps else 1e-8  # ppo_continuous.py:161-166
         self.pg = pg
+        # RCCL communicator for the in-graph gradient all-reduce (None without a
+        # process group, or on gloo: the c10d all-reduce then runs eagerly)
+        self.comm = _rccl.for_group(pg, self.device) if pg is not None and self.device.type == "cuda" else None
         self.graph_group = graph_group
         self.use_graph = use_graph
         # CPU init with the reference's RNG consumption order (actor, then critic)

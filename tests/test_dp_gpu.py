@@ -126,3 +126,59 @@ def test_rollout_is_sharding_invariant():
         assert np.array_equal(o, obs[:, 32 * r:32 * (r + 1)])
         assert np.array_equal(rw, rew[:, 32 * r:32 * (r + 1)])
         assert np.array_equal(a, act[:, 32 * r:32 * (r + 1)])
+
+
+def _nccl_update_rank(port, q):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        q.put(_graphed_update(dist.group.WORLD))
+    finally:
+        dist.destroy_process_group()
+
+
+def _graphed_update(pg):
+    """Two epochs of 16 minibatches (4 graph groups of 4) through
+    PPOLearner.update_packed, with the update's hipGraphs on."""
+    sys.path.insert(0, PKG_DIR)
+    from satrl.ppo import PPOLearner
+    from satrl.trainer import args_param
+    torch.manual_seed(5)
+    args = args_param(hidden_width=H, mini_batch_size=MB, batch_size=B, K_epochs=2, chkpt_dir="/tmp")
+    args.state_dim, args.action_dim, args.max_action = 18, 3, 1.6
+    L = PPOLearner(args, "pursuer", device="cuda:0", pg=pg, graph_group=4, use_graph=True)
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    src = torch.zeros((B, 32), device="cuda:0")
+    src[:, 0:18] = torch.randn((B, 18), device="cuda:0", generator=g)
+    src[:, 18:21] = torch.rand((B, 3), device="cuda:0", generator=g) * 3.2 - 1.6
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda:0", generator=g)
+    src[:, 24] = torch.randn(B, device="cuda:0", generator=g)
+    src[:, 25] = torch.randn(B, device="cuda:0", generator=g) * 5
+    perms = [torch.randperm(B, device="cuda:0", generator=g) for _ in range(2)]
+    L.update_packed(src, 100, perms=perms)
+    torch.cuda.synchronize()
+    used = L.comm is not None and L.stepper(MB).graph is not None
+    return used, L.P.cpu().numpy(), L.W2T.cpu().numpy()
+
+
+def test_rccl_graphed_dp_update_world1():
+    """The data-parallel update on an nccl (RCCL) group: the gradient
+    all-reduce is issued by satrl.rccl on the compute stream and captured in
+    the update's hipGraphs with the kernels.  At world size 1 it must equal
+    the single-process update bitwise (mode 1 | all-reduce | reduce_dp ==
+    mode 3 when nothing is added or divided)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = ctx.Process(target=_nccl_update_rank, args=(port, q))
+    p.start()
+    used, pd, wd = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert used, "the DP update did not run from a graph with the RCCL communicator"
+    _, ps, ws = _graphed_update(None)
+    assert (pd == ps).all() and (wd == ws).all()
