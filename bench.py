@@ -216,9 +216,43 @@ def main():
     torch.cuda.synchronize()
     env_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
     env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
+    env_traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", "r1_env_pmc.json")
+    if os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            pmc = json.load(f)
+        if pmc.get("num_envs") == a.num_envs:
+            env_traffic = pmc["hbm_bytes_per_launch"]
+
+    # ---- north-star sweep: the env kernel alone at num_envs 4k / 16k / 64k on this GPU
+    # (autoreset, U(-1.6,1.6) f32 actions cycled from 64 pre-drawn sets, 256 untimed
+    # steps first so episodes are mid-flight and the danger-zone solves are in their
+    # steady mix, then kernel_iters timed launches)
+    from satrl.env import VecSatellites
+    env_sweep = {}
+    gs = torch.Generator(device="cuda").manual_seed(7)
+    for n_sw in (4096, 16384, 65536):
+        e_sw = VecSatellites(n_sw, d_capture=a.d_capture, max_episode_steps=1000)
+        e_sw.reset(0)
+        acts = (torch.rand((64, 2, n_sw, 3), device="cuda", generator=gs) * 3.2 - 1.6).contiguous()
+        o_sw = torch.empty((n_sw, 18), dtype=torch.float32, device="cuda")
+        r_sw = torch.empty(n_sw, dtype=torch.float32, device="cuda")
+        d_sw = torch.empty(n_sw, dtype=torch.uint8, device="cuda")
+        for k in range(256):
+            e_sw.step_autoreset(acts[k % 64, 0], acts[k % 64, 1], o_sw, r_sw, d_sw)
+        e0.record()
+        for k in range(a.kernel_iters):
+            e_sw.step_autoreset(acts[k % 64, 0], acts[k % 64, 1], o_sw, r_sw, d_sw)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+        gbs = n_sw * ENV_BYTES_PER_STEP / (us * 1e-6) / 1e9
+        env_sweep[str(n_sw)] = {"avg_launch_us": us, "env_steps_per_s": n_sw / (us * 1e-6), "achieved_GBs": gbs,
+                                "hbm_frac": gbs / HBM_PEAK_GBS}
+        del e_sw, acts
 
     # ---- §8f propagators: RK4 two-body + J2 batch kernel, and the env step in RK4-CW mode
-    from satrl.env import VecSatellites, rk4_j2
+    from satrl.env import rk4_j2
     g = torch.Generator(device="cuda").manual_seed(3)
     rv = torch.empty((a.num_envs, 6), dtype=torch.float64, device="cuda")
     rv[:, :3] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 7000.0
@@ -321,7 +355,11 @@ def main():
             "roofline_env": {"kernel": "satenv step_kernel<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
                              "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
-                             "note": "algorithmic bytes; the kernel is FP64 latency bound (DESIGN.md)"},
+                             "traffic": env_traffic,
+                             "traffic_source": "profiles/r1_env_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, bytes/launch, "
+                                               "16384 envs mid-episode)",
+                             "note": "algorithmic bytes; the kernel is FP64 latency bound (DESIGN.md)",
+                             "sweep_num_envs": env_sweep},
             "roofline_update": {"bound": "mfma", "achieved": upd_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                                 "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
                                 "flop_per_transition_epoch": flop_per_transition_epoch},

@@ -37,7 +37,16 @@ __device__ unsigned long long g_probe[4096][16][2][2];
 #define PHASE_PROBE(k) do {} while (0)
 #endif
 
-constexpr int kRows = 32;          // minibatch rows per rowpass workgroup (and per partial slab)
+#ifndef SATRL_RP_ROWS
+#define SATRL_RP_ROWS 32
+#endif
+#ifndef SATRL_RP_NW256
+#define SATRL_RP_NW256 16
+#endif
+constexpr int kRows = SATRL_RP_ROWS;   // minibatch rows per rowpass workgroup (and per partial slab)
+constexpr int kNW256 = SATRL_RP_NW256; // waves per rowpass workgroup at H = 256
+// rowpass workgroups resident per CU the register allocation must allow
+constexpr int kRpWgPerCU = kRows == 16 ? 2 : 1;
 
 constexpr float kLogSqrt2Pi = 0.9189385332046727f;   // math.log(math.sqrt(2*math.pi))
 
@@ -313,7 +322,7 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
 }
 
 template <int H, int NW>
-__global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* __restrict__ src,
+__global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const float* __restrict__ W2T, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
@@ -325,7 +334,6 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
   __shared__ float ax[R][8];
   __shared__ float dz3s[R][4];
-  __shared__ float lsp[R][4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
   // net_sel < 0: both nets, blockIdx = (row block, net); else that net only
   const int net = net_sel < 0 ? (int)(blockIdx.x & 1) : net_sel;
@@ -333,6 +341,12 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
   const int r0 = rb * R;
   auto& S = sm.S;
   PHASE_PROBE(0);
+  // the head's output-layer bias / log_std (uniform: scalar loads issued now,
+  // long landed when the head runs)
+  float hb3[3], hls[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) { hb3[d] = P[L.b3a + d]; hls[d] = P[L.ls + d]; }
+  const float hb3c = P[L.b3c];
 
   f4 acc[RT][CT];
   float h1[RT][CT][4];
@@ -356,9 +370,9 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanhf(out_sum<NW, kRows>(sm.osum, r, d) + P[L.b3a + d]);
+          th[d] = tanhf(out_sum<NW, kRows>(sm.osum, r, d) + hb3[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
-          const float sd = expf(P[L.ls + d]);
+          const float sd = expf(hls[d]);
           var[d] = sd * sd;
           dv[d] = ax[r][d] - mu[d];
           logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - logf(sd)) - kLogSqrt2Pi;
@@ -383,12 +397,34 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
           dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        const float vc = out_sum<NW, kRows>(sm.osum, r, 0) + P[L.b3c];
+        const float vc = out_sum<NW, kRows>(sm.osum, r, 0) + hb3c;
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { dz3s[r][q] = dz[q]; lsp[r][q] = dls[q]; }
+    for (int q = 0; q < 4; ++q) dz3s[r][q] = dz[q];
+    // the block's b3a / log_std / b3c partials: sums over its R rows, reduced
+    // across these R lanes of wave 0 by a fixed xor tree (deterministic)
+    float* tp = ptail + (int64_t)rb * L.tail;
+    float red[7] = {dz[0], dz[1], dz[2], dls[0], dls[1], dls[2], dz[3]};
+#pragma unroll
+    for (int off = 1; off < R; off <<= 1)
+#pragma unroll
+      for (int q = 0; q < 7; ++q) red[q] += __shfl_xor(red[q], off, 64);
+    if (r == 0) {
+      if (net == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          tp[5 * H + q] = red[q];          // b3a
+          tp[5 * H + 4 + q] = red[3 + q];  // log_std
+        }
+        tp[5 * H + 3] = 0.0f;
+        tp[5 * H + 7] = 0.0f;
+      } else {
+        tp[6 * H + 8] = red[6];            // b3c
+        tp[6 * H + 9] = 0.0f; tp[6 * H + 10] = 0.0f; tp[6 * H + 11] = 0.0f;
+      }
+    }
   }
   __syncthreads();
   PHASE_PROBE(4);
@@ -423,20 +459,6 @@ __global__ void __launch_bounds__(NW * 64) rowpass_kernel(int mb, const float* _
       tp[net * H + n] = cb2;                                       // db2
       if (net == 0) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
       else tp[5 * H + 8 + n] = cw[0];                              // dW3c
-    }
-  }
-  if (tid < 4) {
-    float sb = 0.f, sl = 0.f, sc = 0.f;
-    for (int r = 0; r < R; ++r) {
-      sb += tid < 3 ? dz3s[r][tid] : 0.0f;
-      sl += tid < 3 ? lsp[r][tid] : 0.0f;
-      sc += tid == 0 ? dz3s[r][3] : 0.0f;
-    }
-    if (net == 0) {
-      tp[5 * H + tid] = sb;          // b3a
-      tp[5 * H + 4 + tid] = sl;      // log_std
-    } else {
-      tp[6 * H + 8 + tid] = sc;      // b3c
     }
   }
   __syncthreads();
@@ -914,7 +936,7 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
   else
-    hipLaunchKernelGGL((rowpass_kernel<256, 16>), g, dim3(1024), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
+    hipLaunchKernelGGL((rowpass_kernel<256, kNW256>), g, dim3(kNW256 * 64), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
   LAUNCH_CHECK();
   return 0;

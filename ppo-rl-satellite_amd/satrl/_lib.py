@@ -20,6 +20,8 @@ import torch  # noqa: F401  (must be loaded before libsatrl.so, see module doc)
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libsatrl.so")
+# development A/B builds only (tools/_probe variants); the shipped path is LIB_PATH
+LIB_PATH = os.environ.get("SATRL_LIB_PATH", LIB_PATH)
 
 SATENV_F64_PLANES = 15
 SATENV_I32_PLANES = 3

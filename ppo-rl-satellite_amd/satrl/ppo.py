@@ -199,6 +199,8 @@ class FusedMinibatch:
         # library GEMM (torch.bmm -> hipBLASLt, split-K 4) measured 13 us vs
         # 15 us for satrl_ppo_dw2, so it stays a plain library GEMM
         self.lib_gemm = learner.H >= 256
+        if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob
+            self.lib_gemm = os.environ["SATRL_DW2_LIB"] == "1"
         self.S = self.splits(learner.H, self.mb)
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
@@ -249,7 +251,8 @@ class FusedMinibatch:
     def splits(self, H, mb):
         """split-K ways of the dW2 product for a minibatch of mb rows."""
         if self.lib_gemm:
-            return 4 if mb % 4 == 0 else 1
+            S = int(os.environ.get("SATRL_DW2_SPLITS", "4"))          # dev A/B knob; 4 measured best
+            return S if mb % S == 0 else 1
         S = _lib.lib().satrl_ppo_dw2_splits(int(H), int(mb))
         if S < 1:
             raise _lib.NativeError(f"satrl_ppo_dw2_splits({H}, {mb}) failed")

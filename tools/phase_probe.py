@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Development tool (not shipped, not a test): per-phase cycle costs of
+satrl_ppo_rowpass<256,16> from the SATRL_PHASE_PROBE build
+(make -C ppo-rl-satellite_amd/csrc probe -> tools/_probe/libsatrl_probe.so),
+and event timings of the four launches of one minibatch step at the bench
+configuration (H 256, mb 4096, contiguous staged rows).
+
+Stamps (ppo_kernels.hip PHASE_PROBE): 0 start, 8 gather issued, 9 S ready,
+10 fc1 MFMA, 11 tanh(fc1) stored, 1 barrier, 2 fc2 MFMA (B), 3 output-layer
+sums (C fwd), 4 loss head, 5 dZ2 + tail partials, 6 dH1 MFMA (D), 7 end (E).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
+import satrl._lib as _L  # noqa: E402
+
+probe = len(sys.argv) > 1 and sys.argv[1] == "probe"
+if probe:
+    _L.LIB_PATH = os.path.join(ROOT, "tools", "_probe", "libsatrl_probe.so")
+elif len(sys.argv) > 1 and sys.argv[1].endswith(".so"):
+    _L.LIB_PATH = os.path.abspath(sys.argv[1])                # an A/B variant build
+print("library:", _L.LIB_PATH)
+from satrl.ppo import PPOLearner  # noqa: E402
+from satrl.trainer import args_param  # noqa: E402
+
+H, mb = 256, 4096
+a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=16 * mb, chkpt_dir="/tmp")
+L = PPOLearner(a, "pursuer", use_graph=False)
+L.sync_w2t()
+g = torch.Generator(device="cuda").manual_seed(0)
+src = torch.randn((16 * mb, 32), device="cuda", generator=g)
+src[:, 21:24] = -1.0 - torch.rand((16 * mb, 3), device="cuda", generator=g)
+st = L.stepper(mb)
+for _ in range(5):
+    st.rowpass(src, None)
+torch.cuda.synchronize()
+
+if probe:
+    lib = _L.lib()
+    buf = np.zeros((4096, 16, 2, 2), dtype=np.uint64)
+    lib.satrl_probe_read.argtypes = [C.c_void_p]
+    assert lib.satrl_probe_read(buf.ctypes.data) == 0
+    nwg = 2 * (mb // 32)
+    b = buf[:nwg].astype(np.int64)
+    order = [0, 8, 9, 10, 11, 1, 2, 3, 4, 5, 6, 7]
+    names = ["gather issue", "S ready+w3", "fc1 mfma", "tanh h1 store", "barrier", "B fc2", "C fwd",
+             "C head", "C tail", "D dH1", "E dW1"]
+    for w in (0, 1):
+        print(f"wave {'0' if w == 0 else 'NW/2'}: phase cycles (median over workgroups, actor | critic)")
+        for k in range(len(order) - 1):
+            d = b[:, order[k + 1], w, 1] - b[:, order[k], w, 1]
+            print(f"  {names[k]:>14}: {int(np.median(d[0::2])):7d} | {int(np.median(d[1::2])):7d}")
+        tot = b[:, 7, w, 1] - b[:, 0, w, 1]
+        print(f"  {'total':>14}: {int(np.median(tot[0::2])):7d} | {int(np.median(tot[1::2])):7d}")
+    rt = b[:, 0, 0, 0]
+    print("start spread (realtime ticks, 100 MHz):", int(rt.max() - rt.min()),
+          " end spread:", int(b[:, 7, 0, 0].max() - b[:, 7, 0, 0].min()),
+          " kernel span:", int(b[:, 7, 0, 0].max() - rt.min()))
+
+# event timings of each launch of one minibatch step
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+lib = _L.lib()
+sp = _L.stream_ptr()
+S = st.S
+H1, dZ2 = st.rowpass(src, None)
+
+
+def t(fn, n=200):
+    for _ in range(5):
+        fn()
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / n
+
+
+nsq = st.nsq[0]
+res = {
+    "rowpass": t(lambda: st.rowpass(src, None)),
+    "dw2": t(lambda: st._dw2(H1, dZ2, mb, S, -1)),
+    "reduce": t(lambda: lib.satrl_ppo_reduce(H, mb, -1, S, 3, _L.ptr(st.p2), _L.ptr(st.pw1), _L.ptr(st.ptail),
+                                             _L.ptr(L.G), _L.ptr(nsq), _L.ptr(L.steps), sp)),
+    "adam": t(lambda: lib.satrl_ppo_adam(H, mb, -1, _L.ptr(nsq), _L.ptr(L.steps), _L.ptr(L.bct), L.bct.shape[0],
+                                         _L.ptr(L.lr), 0.9, 0.999, 1e-5, 0.5, 1, _L.ptr(L.G), _L.ptr(L.P),
+                                         _L.ptr(L.M), _L.ptr(L.V), _L.ptr(L.W2T), sp)),
+    "step (4 launches)": t(lambda: st.step(src, None)),
+}
+perm = torch.randperm(16 * mb, device="cuda", generator=g)
+st.run(src, perm)
+torch.cuda.synchronize()
+res["graph group of 16 / 16"] = t(lambda: st.run(src, perm), n=20) / 16
+for k, v in res.items():
+    print(f"{k:>24}: {v:8.2f} us")

@@ -15,6 +15,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fe
     python3 "$ROOT/tools/rowpass_workload.py" 40 > /dev/null 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
     python3 "$ROOT/tools/rowpass_workload.py" 40 > /dev/null 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_env_fetch" -o run -- \
+    python3 "$ROOT/tools/env_workload.py" 40 > /dev/null 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_env_write" -o run -- \
+    python3 "$ROOT/tools/env_workload.py" 40 > /dev/null 2>&1
 python3 "$ROOT/tools/summarize_profiles.py" "$OUT" "$TAG" "$ROOT/profiles"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o run -- \
     python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"

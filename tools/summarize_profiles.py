@@ -21,12 +21,16 @@ def kernel_stats(path, out):
     return rows
 
 
-def pmc_per_dispatch(path, kernel_sub, counter):
+def pmc_per_dispatch(path, kernel_sub, counter, last=None):
     per = {}
     for r in csv.DictReader(open(path)):
         if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    vals = sorted(per.values())
+            k = int(r["Dispatch_Id"])
+            per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
+    keys = sorted(per)
+    if last is not None:
+        keys = keys[-last:]
+    vals = sorted(per[k] for k in keys)
     return vals[len(vals) // 2] if vals else None, len(vals)
 
 
@@ -49,6 +53,24 @@ def main():
                "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
                "workload": "tools/rowpass_workload.py"}
         with open(os.path.join(prof, f"{tag}_rowpass_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
+    fetch = os.path.join(d, "pmc_env_fetch", "run_counter_collection.csv")
+    write = os.path.join(d, "pmc_env_write", "run_counter_collection.csv")
+    if os.path.exists(fetch) and os.path.exists(write):
+        # the last 40 dispatches are the profiled mid-episode steps (256 warm-up steps first)
+        f_kb, nf = pmc_per_dispatch(fetch, "step_kernel", "FETCH_SIZE", last=40)
+        w_kb, nw = pmc_per_dispatch(write, "step_kernel", "WRITE_SIZE", last=40)
+        n = 16384
+        res = {"kernel": "satenv step_kernel<true>", "num_envs": n, "dispatches": [nf, nw],
+               "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
+               "fetch_bytes_per_env_raw": f_kb * 1024.0 / n, "write_bytes_per_env": w_kb * 1024.0 / n,
+               "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
+               "correction": "FETCH_SIZE x2 as for 16-B/lane reads (the kernel's f64 plane loads are 8 B/lane, "
+                             "uncalibrated per MI355X_MICROARCH.md; raw per-env fetch bytes kept beside), "
+                             "WRITE_SIZE x1; kB = 1024 B",
+               "workload": "tools/env_workload.py"}
+        with open(os.path.join(prof, f"{tag}_env_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res))
 
