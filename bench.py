@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--minibatch", type=int, default=4096)
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--d-capture", type=float, default=15000.0)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--force-dist", action="store_true",
@@ -52,26 +52,49 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
-    """Oracle (oracle/satenv_oracle.c, the CPU restatement) on host cores:
-    a bounded sample of the same env workload -- 16384 envs stepped from the
-    reference reset state with autoreset (Flag 0, uniform f32 actions), in
-    chunks of 256 steps until about `seconds` of CPU time, OpenMP over envs."""
+def cpu_baseline(seconds, n, T, H, mb, epochs):
+    """The same PPO iteration on host cores, from bounded samples of each
+    part, scaled to one iteration (N envs x T steps, K epochs of mb-row
+    minibatches) -> whole-iteration env-steps/s, the unit of ``value``:
+      env step   oracle/satenv_oracle.c (the C restatement), n envs from the
+                 reference reset state with autoreset (Flag 0, U(-1.6,1.6)
+                 f32 actions), chunks of 64 steps until ~`seconds`, OpenMP
+                 over envs;
+      policy     both agents' choose_action on n states and the critic values
+                 (oracle/ppo_cpu.py, torch-CPU f32 as ppo_continuous.py);
+      GAE        the reference's python reverse loop (oracle.gae_flat) on 2
+                 envs x T, scaled to n envs and divided by the thread count
+                 (envs are independent: perfect parallel assumed);
+      update     oracle/ppo_cpu.py minibatch steps (mb rows, H hidden),
+                 x (n*T/mb)*epochs."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    import ppo_cpu
     threads = max(1, min(16, os.cpu_count() or 1))
-    n, chunk = 16384, 256
+    chunk = 64
     rng = np.random.default_rng(0)
     pa = rng.uniform(-1.6, 1.6, (chunk, n, 3)).astype(np.float32)
     ea = rng.uniform(-1.6, 1.6, (chunk, n, 3)).astype(np.float32)
     ro = O.Rollout(n, d_capture=15000.0, max_episode_steps=1000)
     steps, dt = 0, 0.0
-    while dt < seconds and steps < 64 * chunk:
+    while dt < seconds and steps < 256 * chunk:
         t0 = time.perf_counter()
         ro.run(pa, ea, nthreads=threads)
         dt += time.perf_counter() - t0
         steps += chunk
+    t_env = dt / steps
+    t_pol, t_val, t_mb = ppo_cpu.time_learning_side(n, H, mb, threads)
+    g = np.random.default_rng(1)
+    r = g.standard_normal(T).astype(np.float32)
+    vs = g.standard_normal(T).astype(np.float32)
+    dn = (g.random(T) < 0.01).astype(np.float32)
+    t0 = time.perf_counter()
+    for _ in range(2):
+        O.gae_flat(r, vs, vs, dn, dn)
+    t_gae_env = (time.perf_counter() - t0) / 2
+    t_iter = (T * (t_env + t_pol) + (T + 1) * t_val + n * t_gae_env / threads
+              + epochs * (n * T // mb) * t_mb)
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -80,10 +103,17 @@ def cpu_baseline(seconds):
                 break
     except OSError:
         pass
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle C restatement, {n} envs x {steps} consecutive steps from reset with autoreset "
-                      f"(Flag 0, U(-1.6,1.6) f32 actions, d_capture 15000, max_episode_steps 1000), OpenMP {threads} "
-                      f"threads on '{model}' (os.cpu_count()={os.cpu_count()})",
+    return {"value": n * T / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"one PPO iteration ({n} envs x {T} steps, H {H}, {epochs} epochs x mb {mb}) on "
+                      f"{threads} threads of '{model}' (os.cpu_count()={os.cpu_count()}), scaled from samples: "
+                      f"env step = oracle C restatement, {n} envs x {steps} steps with autoreset (Flag 0, "
+                      f"U(-1.6,1.6) actions, d_capture 15000, max_episode_steps 1000); policy/values/update = "
+                      f"oracle/ppo_cpu.py torch-CPU f32 (8 policy steps, 2 value passes, 24 minibatches); GAE = "
+                      f"the reference's python loop on 2 envs x {T}",
+            "iteration_s": t_iter,
+            "env_step_only_env_steps_per_s": n / t_env,
+            "s_per_env_step_batch": t_env, "s_per_policy_step_both_agents": t_pol,
+            "s_per_value_pass": t_val, "s_per_update_minibatch": t_mb, "s_gae_per_env_python": t_gae_env,
             "seconds": dt}
 
 
@@ -327,7 +357,8 @@ def main():
     n_minibatches = a.epochs * ((a.num_envs * a.horizon) // a.minibatch)
 
     if rank == 0:
-        cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_baseline_seconds)
+        cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_baseline_seconds, a.num_envs, a.horizon, a.hidden,
+                                                            a.minibatch, a.epochs)
         rd_cpu_ms = None if a.no_cpu_baseline else rd_cpu_baseline()
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
