@@ -122,6 +122,14 @@ int satenv_danger_zone(int64_t n, const double* states, const double* fuel, cons
  * independent inputs: in f64 [n][6], alpha_out f64 [n].                    */
 int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* stream);
 
+/* Self-test of the env step's f64 sincos (no reference counterpart): the
+ * straight-line transcription of OCML's small-argument sincos the fsolve
+ * residual uses (use_library = 0), or the library sincos() itself (1), on n
+ * arguments x f64 [n] -> s_out, c_out f64 [n].  The two must agree bitwise
+ * (tests/test_env_gpu.py), so the hybrd restatement's arithmetic is the
+ * library's.                                                              */
+int satenv_sincos(int64_t n, const double* x, double* s_out, double* c_out, int32_t use_library, void* stream);
+
 /* synchronises the handle's device; *status = first sticky device error (0 = none) */
 int satenv_check(satenv_env* h, int32_t* status);
 

@@ -94,9 +94,82 @@ __device__ __forceinline__ int orbital_elements(double mu, double R0, double R1,
 // with A = (2u(1-cos t))/(h v1y) - v1x sin t / v1y hoisted (bit-neutral).
 // Bounded: every path increments nfev and stops at 400.
 // ---------------------------------------------------------------------------
+// OCML's __ocml_sincos_f64 for |x| < 2^30 as straight-line code: the
+// trigredsmall Cody-Waite reduction by pi/2 and the sincosred2 polynomials,
+// transcribed operation for operation from the device library's bitcode
+// (ROCm 7.2 ocml.bc), so results are bit-identical to sincos() there.
+// Straight-line (no per-call branch on the argument size), several calls
+// interleave -- sincos() itself branches to the large-argument reduction,
+// which serialises independent calls.  |x| >= 2^30 and inf/NaN go to
+// sincos() (see sincos_fast).
+__device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_out) {
+  const double ax = fabs(x);
+  // __ocmlpriv_trigredsmall_f64
+  const double q = rint(ax * 0x1.45f306dc9c883p-1);                 // 2/pi
+  const double r4 = fma(q, -0x1.921fb54442d18p+0, ax);
+  const double r5 = fma(q, -0x1.1a62633145c00p-54, r4);
+  const double p6 = q * 0x1.1a62633145c00p-54;
+  const double r8 = fma(q, 0x1.1a62633145c00p-54, -p6);
+  const double r9 = r4 - p6;
+  const double r10 = r4 - r9;
+  const double r11 = r10 - p6;
+  const double r12 = r9 - r5;
+  const double r13 = r12 + r11;
+  const double r14 = r13 - r8;
+  const double r15 = fma(q, -0x1.b839a252049c0p-104, r14);
+  const double hi = r5 + r15;
+  const double r17 = hi - r5;
+  const double lo = r15 - r17;
+  const int quad = ((int)q) & 3;
+  // __ocmlpriv_sincosred2_f64(hi, lo)
+  const double x2 = hi * hi;
+  const double h4 = x2 * 0.5;
+  const double c5 = 1.0 - h4;
+  const double c6 = 1.0 - c5;
+  const double c7 = c6 - h4;
+  const double x4 = x2 * x2;
+  double pc = fma(x2, -0x1.907db46cc5e42p-37, 0x1.1eeb69037ab78p-29);
+  pc = fma(x2, pc, -0x1.27e4fa17f65f6p-22);
+  pc = fma(x2, pc, 0x1.a01a019f4ec90p-16);
+  pc = fma(x2, pc, -0x1.6c16c16c16967p-10);
+  pc = fma(x2, pc, 0x1.5555555555555p-5);
+  const double c15 = fma(hi, -lo, c7);
+  const double c16 = fma(x4, pc, c15);
+  const double cr = c5 + c16;
+  double ps = fma(x2, 0x1.5e0b2f9a43bb8p-33, -0x1.ae600b42fdfa7p-26);
+  ps = fma(x2, ps, 0x1.71de3796cde01p-19);
+  ps = fma(x2, ps, -0x1.a01a019e83e5cp-13);
+  ps = fma(x2, ps, 0x1.1111111110bb3p-7);
+  const double m23 = hi * (-x2);
+  const double s25 = fma(m23, ps, lo * 0.5);
+  const double s26 = fma(x2, s25, -lo);
+  const double s27 = fma(m23, -0x1.5555555555555p-3, s26);
+  const double sr = hi - s27;
+  // quadrant and sign (__ocml_sincos_f64)
+  const unsigned flip = quad > 1 ? 0x80000000u : 0u;
+  const bool even = (quad & 1) == 0;
+  const double sv = even ? sr : cr;
+  const double cv = even ? cr : -sr;
+  const unsigned xs = (unsigned)(__double_as_longlong(x) >> 32) & 0x80000000u;
+  const long long sb = __double_as_longlong(sv), cb = __double_as_longlong(cv);
+  s_out = __longlong_as_double(sb ^ ((long long)(xs ^ flip) << 32));
+  c_out = __longlong_as_double(cb ^ ((long long)flip << 32));
+}
+
+// sincos() with the straight-line body for |x| < 2^30 (every argument of
+// the env step in practice); the rare rest takes the library call
+__device__ __forceinline__ void sincos_fast(double x, double& s, double& c) {
+  sincos_small(x, s, c);
+  if (!(fabs(x) < 0x1.0p+30)) sincos(x, &s, &c);
+}
+
 __device__ __forceinline__ double resid(double A, double st, double dvm, double a) {
   double s, c;
+#ifdef SATENV_RESID_LIBSINCOS
   sincos(a, &s, &c);
+#else
+  sincos_fast(a, s, c);
+#endif
   return A * (dvm * c) + st * (-dvm * s);
 }
 
@@ -217,36 +290,52 @@ __device__ __noinline__ double hybrd1(double A, double st, double dvm, double x)
 // ---------------------------------------------------------------------------
 struct Pursuer { double u, dv2, e, f0, p, r, sf0, X, sq; };
 
-__device__ __forceinline__ void rf_extreme(const Pursuer& P, double f_c, double& rmax, double& rmin) {
+// the two fsolve problems of one rf_extreme_point call (guesses +pi/2 and
+// -pi/2, :516 / :534), set up before any solve so that the danger-zone
+// count can advance all four of an env's solves in one hybrdN<4>
+struct RfSolve { bool ok; double vx0, vy0, dvm, st, ct; double A[2], ag[2]; };
+
+__device__ __forceinline__ void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
   const double d = f_c - P.f0;
   const double sd = sin(d);
   const double temp1 = (sd * sd) / (P.u * (P.X * P.X) / (P.p * P.dv2) - 1.0);    // :466
-  if (!(0.0 <= temp1)) { rmax = 0.0; rmin = 0.0; return; }                       // :477
+  q.ok = (0.0 <= temp1);                                                         // else (0, 0), :477
+  q.vx0 = q.vy0 = q.dvm = q.st = q.ct = 0.0;
+  q.A[0] = q.A[1] = 0.0;
+  q.ag[0] = kPi / 2;
+  q.ag[1] = -kPi / 2;
+  if (!q.ok) return;
   const double beta = atan(0.0 / sd);                                            // tan(fai)=0, :469
   const double sb = sin(beta), cb = cos(beta);
-  const double dvm = sqrt(P.dv2 - P.u * (P.X * P.X) * (sb * sb) / P.p);          // :470
+  q.dvm = sqrt(P.dv2 - P.u * (P.X * P.X) * (sb * sb) / P.p);                     // :470
   double theta = 0.0;
   if ((-kTwoPi <= d && d < -kPi) || (0.0 <= d && d < kPi)) theta = acos(cos(d) * 1.0);          // :473
   else if ((-kPi <= d && d < 0.0) || (kPi <= d && d < kTwoPi)) theta = kTwoPi - acos(cos(d) * 1.0);
-  double st, ct;
-  sincos(theta, &st, &ct);
-  const double vx0 = P.sq * P.e * P.sf0;                                         // :518
-  const double vy0 = P.sq * P.X * cb;                                            // :519
+  sincos(theta, &q.st, &q.ct);
+  q.vx0 = P.sq * P.e * P.sf0;                                                    // :518
+  q.vy0 = P.sq * P.X * cb;                                                       // :519
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    double sg, cg;
+    sincos(q.ag[k], &sg, &cg);
+    const double v1x = q.vx0 + q.dvm * cg, v1y = q.vy0 + q.dvm * sg;
+    const double h = P.r * v1y;
+    q.A[k] = (2.0 * P.u * (1.0 - q.ct)) / (h * v1y) - v1x * q.st / v1y;          // :560
+  }
+}
+
+// rf from the two solutions, abs and sort (:525-530, :549-556)
+__device__ __forceinline__ void rf_finish(const Pursuer& P, const RfSolve& q, double al0, double al1, double& rmax,
+                                          double& rmin) {
+  if (!q.ok) { rmax = 0.0; rmin = 0.0; return; }
   double rf[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const double ag = k == 0 ? kPi / 2 : -kPi / 2;                               // :516, :534
-    double sg, cg;
-    sincos(ag, &sg, &cg);
-    const double v1x = vx0 + dvm * cg, v1y = vy0 + dvm * sg;
-    const double h = P.r * v1y;
-    const double A = (2.0 * P.u * (1.0 - ct)) / (h * v1y) - v1x * st / v1y;      // :560
-    const double al = hybrd1(A, st, dvm, ag);
     double sa, ca;
-    sincos(al, &sa, &ca);
-    const double vx = vx0 + dvm * ca, vy = vy0 + dvm * sa;                       // :525-528
+    sincos(k == 0 ? al0 : al1, &sa, &ca);
+    const double vx = q.vx0 + q.dvm * ca, vy = q.vy0 + q.dvm * sa;               // :525-528
     const double hm = P.r * vy;
-    rf[k] = (hm * hm) / (P.u * (1.0 - ct) + hm * vy * ct - hm * vx * st);        // :530
+    rf[k] = (hm * hm) / (P.u * (1.0 - q.ct) + hm * vy * q.ct - hm * vx * q.st);  // :530
   }
   rmax = fabs(rf[0]);
   rmin = fabs(rf[1]);
@@ -259,10 +348,17 @@ __device__ __forceinline__ double fuel_sq(double fuel, int mode) {
   return fuel * fuel;
 }
 
-// environment.py:317-332 + satellite_function.py:18-99,317-373.  Returns 0 or <0.
-__device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
-                                           double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
-                                           double Ev1, double Ev2, double fuel, int fmode, int& count) {
+// environment.py:317-332 + satellite_function.py:18-99,317-373, cut at its
+// fsolve calls: dz_setup computes both element sets, the latitudinal angles,
+// the two rf_extreme_point set-ups (up to four fsolve problems, z.q[c].A[k]
+// with guess z.q[c].ag[k], live when z.q[c].ok) and the target radii;
+// dz_finish takes the four solutions and returns the count.  Returns 0 or
+// <0 (a non-6-element orbit branch).
+struct DzCtx { Pursuer P; RfSolve q[2]; double r_ft1, r_ft2; };
+
+__device__ __forceinline__ int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
+                                        double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
+                                        double Ev1, double Ev2, double fuel, int fmode, DzCtx& z) {
   const double u = 3.986e14;                                // Time_window_of_danger_zone default u
   Elements C, T;
   int rc = orbital_elements(u, prm.R_cw[0] + Pp0, prm.R_cw[1] + Pp1, prm.R_cw[2] + Pp2, prm.V_cw[0] + Pv0,
@@ -271,7 +367,7 @@ __device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double
   rc = orbital_elements(u, prm.R_cw[0] + Ep0, prm.R_cw[1] + Ep1, prm.R_cw[2] + Ep2, prm.V_cw[0] + Ev0,
                         prm.V_cw[1] + Ev1, prm.V_cw[2] + Ev2, T);
   if (rc) return rc;
-  Pursuer P;
+  Pursuer& P = z.P;
   P.u = u;
   P.dv2 = fuel_sq(fuel, fmode);
   P.e = C.e;
@@ -294,14 +390,37 @@ __device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double
   if (temp1 != temp1 || temp2 != temp2) { temp1 = 1.0; temp2 = 1.0; }         // :331-332
   const double u_c1 = atan(temp1), u_c2 = kPi + u_c1;
   const double u_t1 = atan(temp2), u_t2 = u_t1 + kPi;
-  double mx1, mn1, mx2, mn2;
-  rf_extreme(P, u_c1 - C.omega, mx1, mn1);
-  rf_extreme(P, u_c2 - C.omega, mx2, mn2);
+  rf_setup(P, u_c1 - C.omega, z.q[0]);                                           // rf_extreme_point('orbit_c1')
+  rf_setup(P, u_c2 - C.omega, z.q[1]);                                           // ('orbit_c2')
   const double pt = T.a * (1.0 - T.e * T.e);
-  const double r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                  // :363 (cross-wired f_t2)
-  const double r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                  // :365
-  const bool in1 = (mn1 <= r_ft1 && r_ft1 <= mx1), in2 = (mn2 <= r_ft2 && r_ft2 <= mx2);
-  count = (in1 && in2) ? 2 : ((in1 || in2) ? 1 : 0);
+  z.r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                             // :363 (cross-wired f_t2)
+  z.r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                             // :365
+  return 0;
+}
+
+// al[2c + k] = the fsolve solution of problem (c, k)
+__device__ __forceinline__ int dz_finish(const DzCtx& z, const double (&al)[4]) {
+  double mx1, mn1, mx2, mn2;
+  rf_finish(z.P, z.q[0], al[0], al[1], mx1, mn1);
+  rf_finish(z.P, z.q[1], al[2], al[3], mx2, mn2);
+  const bool in1 = (mn1 <= z.r_ft1 && z.r_ft1 <= mx1), in2 = (mn2 <= z.r_ft2 && z.r_ft2 <= mx2);
+  return (in1 && in2) ? 2 : ((in1 || in2) ? 1 : 0);
+}
+
+// the whole count in one lane (the four solves one after another)
+__device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
+                                           double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
+                                           double Ev1, double Ev2, double fuel, int fmode, int& count) {
+  DzCtx z;
+  const int rc = dz_setup(prm, Pp0, Pp1, Pp2, Pv0, Pv1, Pv2, Ep0, Ep1, Ep2, Ev0, Ev1, Ev2, fuel, fmode, z);
+  if (rc) return rc;
+  double al[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const RfSolve& q = z.q[k >> 1];
+    al[k] = q.ok ? hybrd1(q.A[k & 1], q.st, q.dvm, q.ag[k & 1]) : q.ag[k & 1];
+  }
+  count = dz_finish(z, al);
   return 0;
 }
 

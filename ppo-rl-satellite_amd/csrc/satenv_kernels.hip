@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -108,140 +109,248 @@ __device__ __forceinline__ void wave_stats(double* stats, double fin, double fin
 }
 
 // ---------------------------------------------------------------------------
-// One environment step (environment.py:81-255), one lane per env.
+// One environment step (environment.py:81-255), one lane per env, in two
+// halves around the danger-zone count: step_begin (actions, fuel, STM,
+// terminal tests, the count's set-up) and step_end (count, reward, outputs,
+// autoreset, state write-back).
 // ---------------------------------------------------------------------------
+struct Lane {
+  double k[12];
+  double fuel_c, fuel_t, dis, dis_prev;
+  int dz, count, flag, fcm, ftm;
+  bool p_zero;
+  float pa[3];
+  bool terminal;          // capture or timeout: reward/done set, no count (:139-147 return first)
+  double reward;
+  bool done;
+  double cap;
+};
+
+__device__ __forceinline__ void step_begin(const Params& prm, int64_t n, const double* __restrict__ f64,
+                                           const int32_t* __restrict__ i32, const StepIO& io, int64_t i,
+                                           bool autoreset, Lane& L) {
+  double* k = L.k;
+#pragma unroll
+  for (int c = 0; c < 12; ++c) k[c] = f64[c * n + i];
+  L.fuel_c = f64[12 * n + i];
+  L.fuel_t = f64[13 * n + i];
+  L.dis = f64[14 * n + i];
+  L.dz = i32[kPlaneDz * n + i];
+  const int bits = i32[kPlaneBits * n + i];
+  if (autoreset || io.ext_count == nullptr) L.count = i32[kPlaneCount * n + i] + 1;
+  else L.count = io.ext_count[i];
+  L.flag = env_flag(bits);
+  const int vi = vel_int(bits);
+  L.fcm = fc_mode(bits);
+  L.ftm = ft_mode(bits);
+  float ea[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    L.pa[c] = clip16(io.pa[i * 3 + c]);                                  // :86-87
+    ea[c] = clip16(io.ea[i * 3 + c]);
+  }
+  L.dis_prev = norm3(k[0] - k[6], k[1] - k[7], k[2] - k[8]);             // :89
+  bool p_zero = false, e_zero = false, move_p = true, move_e = true;
+  if (L.flag == 0) {
+    if (L.dis < prm.d_range && L.dz != 0) { move_p = false; p_zero = true; }   // :91-97
+  } else {
+    if (L.dz == 0) { move_e = false; e_zero = true; }                         // :194-198
+  }
+  L.p_zero = p_zero;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {                                           // Vector[i] += action[i]
+    if (move_p) { const double t = k[3 + c] + (double)L.pa[c]; k[3 + c] = vi ? trunc(t) : t; }
+    if (move_e) { const double t = k[9 + c] + (double)ea[c]; k[9 + c] = vi ? trunc(t) : t; }
+  }
+  fuel_sub(L.fuel_c, L.fcm, p_zero, (fabsf(L.pa[0]) + fabsf(L.pa[1])) + fabsf(L.pa[2]));   // :106
+  fuel_sub(L.fuel_t, L.ftm, e_zero, (fabsf(ea[0]) + fabsf(ea[1])) + fabsf(ea[2]));         // :107
+
+  if (prm.propagator == 1) {                                              // optional: RK4 on the CW ODE
+#pragma unroll
+    for (int craft = 0; craft < 2; ++craft) {
+      double x[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) x[c] = k[6 * craft + c];
+      cw_rk4(x, prm.cw_omega, 100.0, prm.rk4_substeps);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) k[6 * craft + c] = x[c];
+    }
+  } else {
+    // Clohessy-Wiltshire STM (satellite_function.py:776-779), OpenBLAS dgemv_t order
+    double y[12];
+#pragma unroll
+    for (int craft = 0; craft < 2; ++craft) {
+      const double* x = k + 6 * craft;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const double* M = prm.stm + 6 * r;
+        const double p0 = M[0] * x[0], p1 = M[1] * x[1], p2 = M[2] * x[2];
+        const double p3 = M[3] * x[3], p4 = M[4] * x[4], p5 = M[5] * x[5];
+        y[6 * craft + r] = (((p0 + p2) + (p1 + p3)) + p4) + p5;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 12; ++c) k[c] = y[c];
+  }
+  L.dis = norm3(k[0] - k[6], k[1] - k[7], k[2] - k[8]);                   // :132
+  L.cap = 0.0;
+  L.terminal = true;
+  L.done = true;
+  if (L.dis <= prm.d_capture) {                                           // :139-142, :221-225
+    L.reward = L.flag == 0 ? prm.win_reward : -150.0;
+    L.cap = 1.0;
+  } else if (L.count >= prm.max_episode_steps) {                         // :144-147, :227-231
+    L.reward = L.flag == 0 ? prm.burn_reward : prm.win_reward;
+  } else {
+    L.terminal = false;
+    L.done = false;
+  }
+}
+
+// non-terminal reward with the new danger-zone count (:150, :161-175, :251)
+__device__ __forceinline__ void step_reward(const Params& prm, Lane& L, int cnt) {
+  const double* k = L.k;
+  const double r0 = k[0] - k[6], r1 = k[1] - k[7], r2 = k[2] - k[8];
+  L.dz = cnt;
+  double r = (L.dis < L.dis_prev) ? 1.0 : -1.0;                          // :161-164
+  r += (prm.d_capture <= L.dis && L.dis <= 4 * prm.d_capture) ? -1.0 : -2.0;
+  r += (L.dz == 0) ? -1.0 : L.dz * 0.5;
+  const double pv1 = cos_sim(k[0], k[1], k[2], k[6], k[7], k[8]);       // reward_of_action3
+  const double pv2 = cos_sim(k[3], k[4], k[5], k[9], k[10], k[11]);     // reward_of_action1
+  const double pv3 = cos_sim(r0, r1, r2, k[3], k[4], k[5]);             // reward_of_action2
+  double pv4 = 0.0;                                                      // reward_of_action4, :388
+  const float* pa = L.pa;
+  if (!L.p_zero && pa[0] != 0.0f && pa[1] != 0.0f && pa[2] != 0.0f) {
+    const double nr = norm3(r0, r1, r2);
+    const float na = norm3f(pa[0], pa[1], pa[2]);
+    pv4 = -dot3(r0 / nr, r1 / nr, r2 / nr, (double)(pa[0] / na), (double)(pa[1] / na), (double)(pa[2] / na));
+  }
+  r += 1 * pv1;
+  r += 0.6 * pv2;
+  r += 0.2 * pv3;
+  r += 2 * pv4;
+  L.reward = L.flag == 0 ? r : -r;                                        // :251
+}
+
+__device__ __forceinline__ void step_end(const Params& prm, int64_t n, double* __restrict__ f64,
+                                         int32_t* __restrict__ i32, const StepIO& io, int64_t i, bool autoreset,
+                                         Lane& L, double& fin, double& fin_ret, double& rew_acc) {
+  if (io.rew64) io.rew64[i] = L.reward;
+  if (io.rew32) io.rew32[i] = (float)L.reward;
+  if (io.done) io.done[i] = L.done ? 1 : 0;
+  double ret = f64[kPlaneRet * n + i] + L.reward;
+  rew_acc = L.reward;
+  int vi_out = 0;
+  if (autoreset && L.done) {                                              // CPPO_main.py:149-153 -> reset(Flag)
+    fin = 1.0;
+    fin_ret = ret;
+    ret = 0.0;
+    reset_kin(prm, L.k);
+    vi_out = 1;
+    L.count = 0;
+  }
+  write_obs(io.obs, io.obs64, i, L.k);
+#pragma unroll
+  for (int c = 0; c < 12; ++c) f64[c * n + i] = L.k[c];
+  f64[12 * n + i] = L.fuel_c;
+  f64[13 * n + i] = L.fuel_t;
+  f64[14 * n + i] = L.dis;
+  f64[kPlaneRet * n + i] = ret;
+  i32[kPlaneDz * n + i] = L.dz;
+  i32[kPlaneCount * n + i] = L.count;
+  i32[kPlaneBits * n + i] = make_bits(L.fcm, L.ftm, vi_out, L.flag);
+}
+
+__device__ __forceinline__ int lane_setup(const Params& prm, const Lane& L, DzCtx& z) {
+  const double* k = L.k;
+  return dz_setup(prm, k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9], k[10], k[11], L.fuel_c, L.fcm,
+                  z);
+}
+
+// one lane per env, the count's four solves one after another (64-lane blocks)
 template <bool AUTORESET>
-__global__ void __launch_bounds__(256) step_kernel(const Params prm, int64_t n, double* __restrict__ f64,
-                                                   int32_t* __restrict__ i32, StepIO io) {
+__global__ void __launch_bounds__(64) step_kernel(const Params prm, int64_t n, double* __restrict__ f64,
+                                                  int32_t* __restrict__ i32, StepIO io) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < n;
   double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0, cap = 0.0;
-  if (live) {
-    double k[12];
-#pragma unroll
-    for (int c = 0; c < 12; ++c) k[c] = f64[c * n + i];
-    double fuel_c = f64[12 * n + i], fuel_t = f64[13 * n + i], dis = f64[14 * n + i];
-    int dz = i32[kPlaneDz * n + i];
-    int bits = i32[kPlaneBits * n + i];
-    int count;
-    if (AUTORESET || io.ext_count == nullptr) count = i32[kPlaneCount * n + i] + 1;
-    else count = io.ext_count[i];
-    const int flag = env_flag(bits);
-    const int vi = vel_int(bits);
-    int fcm = fc_mode(bits), ftm = ft_mode(bits);
-
-    float pa[3], ea[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      pa[c] = clip16(io.pa[i * 3 + c]);                                  // :86-87
-      ea[c] = clip16(io.ea[i * 3 + c]);
-    }
-    const double dis_prev = norm3(k[0] - k[6], k[1] - k[7], k[2] - k[8]);    // :89
-    bool p_zero = false, e_zero = false, move_p = true, move_e = true;
-    if (flag == 0) {
-      if (dis < prm.d_range && dz != 0) { move_p = false; p_zero = true; }  // :91-97
-    } else {
-      if (dz == 0) { move_e = false; e_zero = true; }                        // :194-198
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {                                            // Vector[i] += action[i]
-      if (move_p) { const double t = k[3 + c] + (double)pa[c]; k[3 + c] = vi ? trunc(t) : t; }
-      if (move_e) { const double t = k[9 + c] + (double)ea[c]; k[9 + c] = vi ? trunc(t) : t; }
-    }
-    fuel_sub(fuel_c, fcm, p_zero, (fabsf(pa[0]) + fabsf(pa[1])) + fabsf(pa[2]));   // :106
-    fuel_sub(fuel_t, ftm, e_zero, (fabsf(ea[0]) + fabsf(ea[1])) + fabsf(ea[2]));   // :107
-
-    if (prm.propagator == 1) {                                              // optional: RK4 on the CW ODE
-#pragma unroll
-      for (int craft = 0; craft < 2; ++craft) {
-        double x[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) x[c] = k[6 * craft + c];
-        cw_rk4(x, prm.cw_omega, 100.0, prm.rk4_substeps);
-#pragma unroll
-        for (int c = 0; c < 6; ++c) k[6 * craft + c] = x[c];
-      }
-    } else {
-      // Clohessy-Wiltshire STM (satellite_function.py:776-779), OpenBLAS dgemv_t order
-      double y[12];
-#pragma unroll
-      for (int craft = 0; craft < 2; ++craft) {
-        const double* x = k + 6 * craft;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          const double* M = prm.stm + 6 * r;
-          const double p0 = M[0] * x[0], p1 = M[1] * x[1], p2 = M[2] * x[2];
-          const double p3 = M[3] * x[3], p4 = M[4] * x[4], p5 = M[5] * x[5];
-          y[6 * craft + r] = (((p0 + p2) + (p1 + p3)) + p4) + p5;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 12; ++c) k[c] = y[c];
-    }
-    const double r0 = k[0] - k[6], r1 = k[1] - k[7], r2 = k[2] - k[8];
-    dis = norm3(r0, r1, r2);                                                // :132
-
-    double reward;
-    bool done;
-    if (dis <= prm.d_capture) {                                             // :139-142, :221-225
-      reward = flag == 0 ? prm.win_reward : -150.0;
-      done = true;
-      cap = 1.0;
-    } else if (count >= prm.max_episode_steps) {                           // :144-147, :227-231
-      reward = flag == 0 ? prm.burn_reward : prm.win_reward;
-      done = true;
-    } else {
+  if (i < n) {
+    Lane L;
+    step_begin(prm, n, f64, i32, io, i, AUTORESET, L);
+    cap = L.cap;
+    if (!L.terminal) {
       int cnt = 0;
-      const int rc = danger_zone(prm, k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], k[8], k[9], k[10], k[11],
-                                 fuel_c, fcm, cnt);                         // :150, :317-332
+      const int rc = danger_zone(prm, L.k[0], L.k[1], L.k[2], L.k[3], L.k[4], L.k[5], L.k[6], L.k[7], L.k[8],
+                                 L.k[9], L.k[10], L.k[11], L.fuel_c, L.fcm, cnt);   // :150, :317-332
       if (rc) atomicCAS(io.err, 0, rc);
-      dz = cnt;
-      double r = (dis < dis_prev) ? 1.0 : -1.0;                            // :161-164
-      r += (prm.d_capture <= dis && dis <= 4 * prm.d_capture) ? -1.0 : -2.0;
-      r += (dz == 0) ? -1.0 : dz * 0.5;
-      const double pv1 = cos_sim(k[0], k[1], k[2], k[6], k[7], k[8]);     // reward_of_action3
-      const double pv2 = cos_sim(k[3], k[4], k[5], k[9], k[10], k[11]);   // reward_of_action1
-      const double pv3 = cos_sim(r0, r1, r2, k[3], k[4], k[5]);           // reward_of_action2
-      double pv4 = 0.0;                                                    // reward_of_action4, :388
-      if (!p_zero && pa[0] != 0.0f && pa[1] != 0.0f && pa[2] != 0.0f) {
-        const double nr = norm3(r0, r1, r2);
-        const float na = norm3f(pa[0], pa[1], pa[2]);
-        pv4 = -dot3(r0 / nr, r1 / nr, r2 / nr, (double)(pa[0] / na), (double)(pa[1] / na), (double)(pa[2] / na));
-      }
-      r += 1 * pv1;
-      r += 0.6 * pv2;
-      r += 0.2 * pv3;
-      r += 2 * pv4;
-      reward = flag == 0 ? r : -r;                                          // :251
-      done = false;
+      step_reward(prm, L, cnt);
     }
-
-    if (io.rew64) io.rew64[i] = reward;
-    if (io.rew32) io.rew32[i] = (float)reward;
-    if (io.done) io.done[i] = done ? 1 : 0;
-    double ret = f64[kPlaneRet * n + i] + reward;
-    rew_acc = reward;
-    int vi_out = 0;
-    if (AUTORESET && done) {                                                // CPPO_main.py:149-153 -> reset(Flag)
-      fin = 1.0;
-      fin_ret = ret;
-      ret = 0.0;
-      reset_kin(prm, k);
-      vi_out = 1;
-      count = 0;
-    }
-    write_obs(io.obs, io.obs64, i, k);
-#pragma unroll
-    for (int c = 0; c < 12; ++c) f64[c * n + i] = k[c];
-    f64[12 * n + i] = fuel_c;
-    f64[13 * n + i] = fuel_t;
-    f64[14 * n + i] = dis;
-    f64[kPlaneRet * n + i] = ret;
-    i32[kPlaneDz * n + i] = dz;
-    i32[kPlaneCount * n + i] = count;
-    i32[kPlaneBits * n + i] = make_bits(fcm, ftm, vi_out, flag);
+    step_end(prm, n, f64, i32, io, i, AUTORESET, L, fin, fin_ret, rew_acc);
   }
   if (io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
+}
+
+// 64 envs per 4-wave workgroup: wave 0 runs the env lanes (step_begin, the
+// count's set-up, then its finish and step_end), and between two barriers
+// wave w solves fsolve problem w of every env of the block (the c-th
+// rf_extreme_point's k-th guess, w = 2c + k) -- so the four dependent
+// hybrd loops of an env run side by side on four SIMDs instead of one
+// after another on one, and a launch has 4x the waves (the step is FP64
+// latency bound: 16384 envs are only 256 waves).  Bit-identical to
+// step_kernel: every problem runs the same hybrd1.
+constexpr int kSplitEnvs = 64;
+template <bool AUTORESET>
+__global__ void __launch_bounds__(256) step_kernel_split(const Params prm, int64_t n, double* __restrict__ f64,
+                                                         int32_t* __restrict__ i32, StepIO io) {
+  __shared__ double sA[4][kSplitEnvs], sSt[4][kSplitEnvs], sDvm[4][kSplitEnvs], sX[4][kSplitEnvs];
+  __shared__ int sOn[4][kSplitEnvs];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + lane;
+  const bool live = w == 0 && i < n;
+  Lane L;
+  DzCtx z;
+  int rc = 0;
+  double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0, cap = 0.0;
+  if (w == 0) {
+    bool on[2] = {false, false};
+    if (live) {
+      step_begin(prm, n, f64, i32, io, i, AUTORESET, L);
+      cap = L.cap;
+      if (!L.terminal) {
+        rc = lane_setup(prm, L, z);                                      // :150, :317-332
+        if (rc == 0) { on[0] = z.q[0].ok; on[1] = z.q[1].ok; }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = q >> 1, kk = q & 1;
+      sOn[q][lane] = on[c] ? 1 : 0;
+      if (on[c]) {
+        sA[q][lane] = z.q[c].A[kk];
+        sSt[q][lane] = z.q[c].st;
+        sDvm[q][lane] = z.q[c].dvm;
+        sX[q][lane] = z.q[c].ag[kk];
+      }
+    }
+  }
+  __syncthreads();
+  if (sOn[w][lane]) sX[w][lane] = hybrd1(sA[w][lane], sSt[w][lane], sDvm[w][lane], sX[w][lane]);
+  __syncthreads();
+  if (live) {
+    if (!L.terminal) {
+      int cnt = 0;
+      if (rc) {
+        atomicCAS(io.err, 0, rc);
+      } else {
+        double al[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) al[q] = sOn[q][lane] ? sX[q][lane] : z.q[q >> 1].ag[q & 1];
+        cnt = dz_finish(z, al);
+      }
+      step_reward(prm, L, cnt);
+    }
+    step_end(prm, n, f64, i32, io, i, AUTORESET, L, fin, fin_ret, rew_acc);
+  }
+  if (w == 0 && io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
 }
 
 __global__ void __launch_bounds__(256) reset_kernel(const Params prm, int64_t n, double* __restrict__ f64,
@@ -302,6 +411,17 @@ __global__ void __launch_bounds__(256) solve_alpha_kernel(int64_t n, const doubl
   const double u = 3.986e14, dvm = x[0], theta = x[1], v1x = x[2], v1y = x[3], h = x[4];
   const double A = (2.0 * u * (1.0 - cos(theta))) / (h * v1y) - v1x * sin(theta) / v1y;
   out[i] = hybrd1(A, sin(theta), dvm, x[5]);
+}
+
+__global__ void __launch_bounds__(256) sincos_kernel(int64_t n, const double* __restrict__ x, double* __restrict__ so,
+                                                     double* __restrict__ co, int32_t use_library) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s, c;
+  if (use_library) sincos(x[i], &s, &c);
+  else sincos_fast(x[i], s, c);
+  so[i] = s;
+  co[i] = c;
 }
 
 // batched RK4 two-body + J2 propagation (轨道外推-龙格库塔算法.py), SoA [6][n]
@@ -518,19 +638,19 @@ struct satenv_env {
   double* f64 = nullptr;
   int32_t* i32 = nullptr;
   int32_t* err = nullptr;
-  int block = 64;
+  int split = 1;   // step_kernel_split (1) or the one-lane step_kernel (0)
 };
 
 namespace {
 
 int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
-// env-step launch geometry: N = 16384 envs is only 256 waves, so 64-lane
-// workgroups spread them over all 256 CUs instead of packing 4 per CU.
-int pick_block(int64_t n) {
-  if (n <= 256 * 64) return 64;
-  if (n <= 256 * 128) return 128;
-  return 256;
+// env-step kernel choice (SATENV_STEP_SPLIT=0 forces the one-lane kernel: dev A/B)
+int pick_split(int64_t n) {
+  (void)n;
+  const char* e = std::getenv("SATENV_STEP_SPLIT");
+  if (e && e[0] == '0') return 0;
+  return 1;
 }
 
 }  // namespace
@@ -589,7 +709,7 @@ int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, in
   h->n = num_envs;
   h->device = device;
   h->prm = *p;
-  h->block = pick_block(num_envs);
+  h->split = pick_split(num_envs);
   hipError_t e = hipMalloc(&h->f64, sizeof(double) * kF64Planes * num_envs);
   if (e == hipSuccess) e = hipMalloc(&h->i32, sizeof(int32_t) * kI32Planes * num_envs);
   if (e == hipSuccess) e = hipMalloc(&h->err, sizeof(int32_t));
@@ -647,8 +767,12 @@ int satenv_step(satenv_env* h, const float* pa, const float* ea, const int32_t* 
                 double* obs64_out, double* reward_out, uint8_t* done_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step: null argument");
   StepIO io{pa, ea, episode_count, obs_out, obs64_out, reward_out, nullptr, done_out, nullptr, h->err};
-  hipLaunchKernelGGL(step_kernel<false>, dim3(grid_for(h->n, h->block)), dim3(h->block), 0, (hipStream_t)stream,
-                     h->prm, h->n, h->f64, h->i32, io);
+  if (h->split)
+    hipLaunchKernelGGL(step_kernel_split<false>, dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0, (hipStream_t)stream,
+                       h->prm, h->n, h->f64, h->i32, io);
+  else
+    hipLaunchKernelGGL(step_kernel<false>, dim3(grid_for(h->n, 64)), dim3(64), 0, (hipStream_t)stream, h->prm, h->n,
+                       h->f64, h->i32, io);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }
@@ -657,8 +781,12 @@ int satenv_step_autoreset(satenv_env* h, const float* pa, const float* ea, float
                           uint8_t* done_out, double* stats_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step_autoreset: null argument");
   StepIO io{pa, ea, nullptr, obs_out, nullptr, nullptr, reward_out, done_out, stats_out, h->err};
-  hipLaunchKernelGGL(step_kernel<true>, dim3(grid_for(h->n, h->block)), dim3(h->block), 0, (hipStream_t)stream,
-                     h->prm, h->n, h->f64, h->i32, io);
+  if (h->split)
+    hipLaunchKernelGGL(step_kernel_split<true>, dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0, (hipStream_t)stream,
+                       h->prm, h->n, h->f64, h->i32, io);
+  else
+    hipLaunchKernelGGL(step_kernel<true>, dim3(grid_for(h->n, 64)), dim3(64), 0, (hipStream_t)stream, h->prm, h->n,
+                       h->f64, h->i32, io);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }
@@ -697,6 +825,14 @@ int satenv_danger_zone(int64_t n, const double* states, const double* fuel, cons
 int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* stream) {
   if (n <= 0 || !in || !alpha_out) return fail(SATENV_ERR_ARG, "satenv_solve_alpha: bad args");
   hipLaunchKernelGGL(solve_alpha_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, in, alpha_out);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_sincos(int64_t n, const double* x, double* s_out, double* c_out, int32_t use_library, void* stream) {
+  if (n <= 0 || !x || !s_out || !c_out) return fail(SATENV_ERR_ARG, "satenv_sincos: bad args");
+  hipLaunchKernelGGL(sincos_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, x, s_out, c_out,
+                     use_library);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

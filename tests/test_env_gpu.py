@@ -51,6 +51,32 @@ def test_solve_alpha_matches_fsolve(satrl_env):
     assert exact > 0.5
 
 
+def test_straight_line_sincos_is_the_library_sincos(satrl_env):
+    """The fsolve residual's sincos (satenv_device.h sincos_small, a
+    transcription of OCML's small-argument path) == the device library's
+    sincos(), bitwise, over the argument ranges the env step meets (solver
+    iterates near +-pi/2, angles in [-4pi, 4pi]), wide random magnitudes up
+    to and past the 2^30 switch, signed zeros, subnormals, inf and NaN."""
+    from satrl import _lib
+    g = np.random.default_rng(3)
+    parts = [np.pi / 2 + g.normal(0, 1e-3, 200000), -np.pi / 2 + g.normal(0, 1e-3, 200000),
+             g.uniform(-4 * np.pi, 4 * np.pi, 400000),
+             np.sign(g.normal(size=200000)) * 10.0 ** g.uniform(-300, 12, 200000),
+             np.array([0.0, -0.0, 5e-324, -5e-324, 2.0 ** 30, -(2.0 ** 30), np.nextafter(2.0 ** 30, 0),
+                       np.inf, -np.inf, np.nan, np.pi, -np.pi, np.pi / 4, 1e-8])]
+    x = torch.tensor(np.concatenate(parts), dtype=torch.float64, device="cuda")
+    n = x.numel()
+    res = []
+    for lib_flag in (0, 1):
+        s = torch.empty(n, dtype=torch.float64, device="cuda")
+        c = torch.empty(n, dtype=torch.float64, device="cuda")
+        _lib.check(_lib.lib().satenv_sincos(n, _lib.ptr(x), _lib.ptr(s), _lib.ptr(c), lib_flag, _lib.stream_ptr()),
+                   "satenv_sincos")
+        res.append((s.cpu().numpy().view(np.int64), c.cpu().numpy().view(np.int64)))
+    (s0, c0), (s1, c1) = res
+    assert np.array_equal(s0, s1) and np.array_equal(c0, c1)
+
+
 def test_danger_zone_counts(satrl_env):
     from satrl import _lib
     d = golden("dz_cases")
