@@ -248,6 +248,16 @@ def _typed(v, mode):
     return [int(v), np.int64(v), np.float32(v), np.float64(v)][mode]
 
 
+class _EllipseFittingNet:
+    """The part of real_time_data_process.network_method_train (:127-139) the
+    env step can observe: ``net`` = an ImprovedNN built on the CPU (its
+    forward is commented out in the step, environment.py:158)."""
+
+    def __init__(self):
+        from .surrogate import ImprovedNN
+        self.net = ImprovedNN()
+
+
 class satellites:  # noqa: N801  (reference class name)
     """Drop-in for ``environment.satellites`` (environment.py:8), Flag 0/1.
 
@@ -271,6 +281,11 @@ class satellites:  # noqa: N801  (reference class name)
         self.win_reward = 100
         self.ellipse_params = []
         self.observation_space, self.action_space, self.action_space_beta = _spaces()
+        # environment.py:49 builds the ellipse-fitting trainer, whose ImprovedNN()
+        # (real_time_data_process.py:129) draws its default init from torch's
+        # global CPU generator: draw the same numbers, so agents constructed
+        # after a seeded env get the reference's weights
+        self.trian_elliptical_fitting = _EllipseFittingNet()
         dev = self._v.device
         self._pa = torch.empty((1, ACT_DIM), dtype=torch.float32, device=dev)
         self._ea = torch.empty((1, ACT_DIM), dtype=torch.float32, device=dev)

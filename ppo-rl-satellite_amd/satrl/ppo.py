@@ -254,6 +254,8 @@ class FusedMinibatch:
             S = int(os.environ.get("SATRL_DW2_SPLITS", "4"))          # dev A/B knob; 4 measured best
             return S if mb % S == 0 else 1
         S = _lib.lib().satrl_ppo_dw2_splits(int(H), int(mb))
+        if os.environ.get("SATRL_DW2_S"):                               # dev A/B knob
+            S = int(os.environ["SATRL_DW2_S"])
         if S < 1:
             raise _lib.NativeError(f"satrl_ppo_dw2_splits({H}, {mb}) failed")
         return S

@@ -1,0 +1,172 @@
+"""The reference's own evaluation loop through the drop-in classes.
+
+CPPO_main.test_network (CPPO_main.py:233-282) with the one_layer pursuer
+checkpoint and a randomly initialised evader, torch/np seed 0, as
+tests/golden/capture_golden.py ran it on the reference (test_network.npz,
+64- and 1000-step episodes).  The env constructor, both PPO_continuous
+agents and every choose_action draw from torch's global CPU generator in the
+reference's order, so agent weights and sampled noise are the reference's.
+
+The closed loop is discontinuous (the danger-zone count is an integer that
+gates the pursuer and moves the reward by 0.5), so an ulp of GEMM-order
+difference in the GPU f32 forward eventually flips a count and the episodes
+part.  Each half is therefore pinned with the other half forced to the
+reference's recorded values:
+  * agents forced through the reference env's outputs: every choose_action
+    (pursuer and evader) matches the recorded one -- seeding, RNG order and
+    the f32 forward.  The observations are raw positions (~2e5 m), so fc1's
+    pre-activations are sums of terms ~1e4 that cancel to O(1): a different
+    f32 summation order (the GPU GEMM vs the reference's CPU one) moves the
+    mean by up to ~1e-3.  The bar is therefore the a-priori f32 forward
+    error bound of that very input (Higham's gamma_n per dot product,
+    propagated through tanh's local slope and the next layers' |W|), per step in
+    f64: |ours - reference| <= 2 x bound (both within the bound of the exact
+    value); log-probs move by |a - mu| / sigma^2 times that, plus 1e-5;
+  * env forced with the recorded actions: the drop-in satellites (HIP f64
+    step) reproduces every recorded reward and done flag, and the return;
+    bars: done exact, rewards 1e-9 absolute, return 1e-12 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_one_layer_checkpoint(d):
+    """agent_pursuer_{actor_Gaussian,critic} state_dict files from the
+    reference's one_layer checkpoint values kept in policy_one_layer.npz."""
+    g = golden("policy_one_layer")
+    for net, fname in (("actor", "agent_pursuer_actor_Gaussian"), ("critic", "agent_pursuer_critic")):
+        sd = {k[len(net) + 1:]: torch.tensor(g[k]) for k in g.files if k.startswith(net + ".")}
+        torch.save(sd, os.path.join(d, fname))
+
+
+U32 = 2.0 ** -24
+
+
+def _gamma(n):
+    return n * U32 / (1 - n * U32)
+
+
+def _mean_error_bound(sd, obs, max_action=1.6):
+    """First-order bound on |f32 forward - exact| of max_action*tanh(mean_layer(
+    tanh(fc2(tanh(fc1(s)))))) for each row of obs (f32-rounded inputs, as
+    both implementations round them identically); sd: the actor state_dict
+    as float64 arrays."""
+    s = obs.astype(np.float32).astype(np.float64)
+    bound_in, act = np.zeros_like(s), s
+    for w, b in (("fc1.weight", "fc1.bias"), ("fc2.weight", "fc2.bias"), ("mean_layer.weight", "mean_layer.bias")):
+        W, bb = sd[w], sd[b]
+        z = act @ W.T + bb
+        mag = np.abs(act) @ np.abs(W).T + np.abs(bb)
+        err = bound_in @ np.abs(W).T + _gamma(W.shape[1] + 1) * mag
+        act = np.tanh(z)
+        lip = 1.0 - np.tanh(np.maximum(np.abs(z) - err, 0.0)) ** 2   # max of tanh' over [z - err, z + err]
+        bound_in = lip * err + 2 * U32 * np.abs(act) + 2 * U32     # + tanh's own rounding
+    return max_action * bound_in + 2 * U32 * max_action
+
+
+def _run_test_network(tmp_path, max_ep, force_env, force_agents):
+    """satrl.trainer.test_network on the drop-in classes, seeded as the
+    fixture; logs what the agents chose and what the env returned."""
+    from satrl import ppo as P
+    from satrl.env import satellites
+    from satrl.trainer import args_param, test_network
+    g = golden("test_network")
+    obs_g, pa_g, ea_g = g[f"obs_in_{max_ep}"], g[f"pa_{max_ep}"], g[f"ea_{max_ep}"]
+    r_g, done_g = g[f"r_{max_ep}"], g[f"done_{max_ep}"]
+    _write_one_layer_checkpoint(str(tmp_path))
+    log = {"pa": [], "ea": [], "plogp": [], "pmean": [], "r": [], "done": [], "obs_in": []}
+    orig_choose, orig_init, orig_step = P.PPO_continuous.choose_action, P.PPO_continuous.__init__, satellites.step
+
+    def init(self, args_, idx, *a, **k):
+        orig_init(self, args_, idx, *a, **k)
+        if idx == "pursuer":
+            log["_pursuer"] = self
+        log["_agent_" + idx] = self
+
+    def choose(self, s):
+        a, lp = orig_choose(self, s)                 # draws the noise either way (RNG order)
+        t = len(log["r"])
+        if self is log.get("_pursuer"):
+            log["obs_in"].append(np.asarray(s, np.float64))
+            log["pa"].append(a)
+            log["plogp"].append(lp)
+            log["pmean"].append(self.evaluate(s))
+            if force_agents:
+                a = pa_g[t].copy()
+        else:
+            log["ea"].append(a)
+            if force_agents:
+                a = ea_g[t].copy()
+        return a, lp
+
+    def step(self, pa, ea, c):
+        t = len(log["r"])
+        if force_env:
+            s_ = obs_g[t + 1] if t + 1 < len(obs_g) else obs_g[t]
+            r, d = r_g[t], bool(done_g[t])
+        else:
+            s_, r, d = orig_step(self, pa, ea, c)
+        log["r"].append(float(r))
+        log["done"].append(int(d))
+        return s_, r, d
+
+    P.PPO_continuous.__init__, P.PPO_continuous.choose_action, satellites.step = init, choose, step
+    try:
+        torch.manual_seed(0)
+        np.random.seed(0)
+        a2 = args_param(max_episode_steps=max_ep, batch_size=64, max_train_steps=5000, K_epochs=3,
+                        chkpt_dir=str(tmp_path))
+        env = satellites(Pursuer_position=np.array([2000000, 2000000, 1000000]),
+                         Pursuer_vector=np.array([1710, 1140, 1300]),
+                         Escaper_position=np.array([1850000, 2000000, 1000000]),
+                         Escaper_vector=np.array([1710, 1140, 1300]), d_capture=50000, args=a2)
+        ret = test_network(a2, env, show_pictures=False, d_capture=20000)
+    finally:
+        P.PPO_continuous.__init__, P.PPO_continuous.choose_action, satellites.step = orig_init, orig_choose, orig_step
+    return g, log, ret
+
+
+@pytest.mark.parametrize("max_ep", [64, 1000])
+def test_agents_match_reference_choices(tmp_path, max_ep):
+    g, log, _ = _run_test_network(tmp_path, max_ep, force_env=True, force_agents=False)
+    n = len(g[f"r_{max_ep}"])
+    assert len(log["pa"]) == n and len(log["ea"]) == n
+    obs = g[f"obs_in_{max_ep}"]
+    np.testing.assert_array_equal(np.asarray(log["obs_in"]), obs)          # the forced inputs
+    bounds = {}
+    for who in ("pursuer", "evader"):
+        sd = {k: v.detach().cpu().double().numpy() for k, v in log["_agent_" + who].actor.state_dict().items()}
+        bounds[who] = _mean_error_bound(sd, obs)
+    # the pursuer's mean and action (the evader's mean is not recorded: its action carries it)
+    pm, pa, ea = (np.asarray(log[k], np.float64) for k in ("pmean", "pa", "ea"))
+    assert np.all(np.abs(pm - g[f"pmean_{max_ep}"]) <= 2 * bounds["pursuer"])
+    assert np.all(np.abs(pa - g[f"pa_{max_ep}"]) <= 2 * bounds["pursuer"] + 2 * U32 * 1.6)
+    assert np.all(np.abs(ea - g[f"ea_{max_ep}"]) <= 2 * bounds["evader"] + 2 * U32 * 1.6)
+    sig2 = np.exp(2 * g["actor.log_std"] if "actor.log_std" in g.files else
+                  2 * golden("policy_one_layer")["actor.log_std"])
+    slope = np.abs(pa - pm) / sig2
+    assert np.all(np.abs(np.asarray(log["plogp"], np.float64) - g[f"plogp_{max_ep}"])
+                  <= slope * 4 * bounds["pursuer"] + 1e-5)
+    # the bound is not vacuous: it is far below the actions' scale on most steps
+    print(max_ep, "median / max bound", float(np.median(bounds["pursuer"])), float(bounds["pursuer"].max()),
+          "max |dmean|", float(np.max(np.abs(pm - g[f"pmean_{max_ep}"]))))
+    assert np.median(bounds["pursuer"]) < 1e-2
+
+
+@pytest.mark.parametrize("max_ep", [64, 1000])
+def test_env_matches_reference_episode(tmp_path, max_ep):
+    g, log, ret = _run_test_network(tmp_path, max_ep, force_env=False, force_agents=True)
+    n = len(g[f"r_{max_ep}"])
+    assert len(log["r"]) == n
+    np.testing.assert_array_equal(np.asarray(log["done"]), g[f"done_{max_ep}"])
+    np.testing.assert_allclose(np.asarray(log["obs_in"]), g[f"obs_in_{max_ep}"], rtol=1e-12, atol=0)
+    assert float(np.max(np.abs(np.asarray(log["r"]) - g[f"r_{max_ep}"]))) <= 1e-9
+    gr = float(g[f"return_{max_ep}"])
+    assert abs(ret - gr) <= 1e-12 * max(1.0, abs(gr)), (ret, gr)

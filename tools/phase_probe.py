@@ -27,6 +27,9 @@ elif len(sys.argv) > 1 and sys.argv[1].endswith(".so"):
     _L.LIB_PATH = os.path.abspath(sys.argv[1])                # an A/B variant build
 print("library:", _L.LIB_PATH)
 from satrl.ppo import PPOLearner  # noqa: E402
+if os.environ.get("SATRL_BLAS"):                       # dev A/B: torch's BLAS backend for the dW2 bmm
+    torch.backends.cuda.preferred_blas_library(os.environ["SATRL_BLAS"])
+    print("blas:", torch.backends.cuda.preferred_blas_library())
 from satrl.trainer import args_param  # noqa: E402
 
 H, mb = 256, 4096
