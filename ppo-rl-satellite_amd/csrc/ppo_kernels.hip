@@ -809,30 +809,6 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   __shared__ float cst[2][3];                                      // coef, step_size, bc2_sqrt per net
   __shared__ float tile[32][33];
   const int t = threadIdx.x;
-  const int ntc = H / 32, nbw = (net_sel < 0 ? 2 : 1) * ntc * ntc;
-  const float4* G4 = reinterpret_cast<const float4*>(G);
-  float4* P4 = reinterpret_cast<float4*>(P);
-  float4* M4 = reinterpret_cast<float4*>(M);
-  float4* V4 = reinterpret_cast<float4*>(V);
-  // this thread's element (float4) and net, and its operand loads issued
-  // before the norm fold so the two latency rounds overlap
-  int64_t e4;
-  int net;
-  bool live = true;
-  if ((int)blockIdx.x < nbw) {
-    const int tb = blockIdx.x % (ntc * ntc);
-    net = net_sel < 0 ? (int)(blockIdx.x / (ntc * ntc)) : net_sel;
-    const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
-    e4 = ((int64_t)net * H * H + (int64_t)n * H + k) / 4;
-  } else {
-    e4 = L.W1 / 4 + (int64_t)(blockIdx.x - nbw) * 256 + t;
-    net = e4 < L.total / 4 ? net_of(L, e4 * 4, H) : 0;
-    live = e4 < L.total / 4 && (net_sel < 0 || net == net_sel);
-  }
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4 g = live ? G4[e4] : z4;
-  float4 m = live ? M4[e4] : z4, v = live ? V4[e4] : z4;
-  const float4 p = live ? P4[e4] : z4;
   double a = 0.0, c = 0.0;
   for (int k = t; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
   block_sum2(a, c, sh);
@@ -851,7 +827,27 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   __syncthreads();
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
-  if (!live) return;                                               // (no barrier follows in this branch)
+  const int ntc = H / 32, nbw = (net_sel < 0 ? 2 : 1) * ntc * ntc;
+  const float4* G4 = reinterpret_cast<const float4*>(G);
+  float4* P4 = reinterpret_cast<float4*>(P);
+  float4* M4 = reinterpret_cast<float4*>(M);
+  float4* V4 = reinterpret_cast<float4*>(V);
+  int64_t e4;
+  int net;
+  if ((int)blockIdx.x < nbw) {
+    const int tb = blockIdx.x % (ntc * ntc);
+    net = net_sel < 0 ? (int)(blockIdx.x / (ntc * ntc)) : net_sel;
+    const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
+    e4 = ((int64_t)net * H * H + (int64_t)n * H + k) / 4;
+  } else {
+    e4 = L.W1 / 4 + (int64_t)(blockIdx.x - nbw) * 256 + t;
+    if (e4 >= L.total / 4) return;                                 // (no barrier follows in this branch)
+    net = net_of(L, e4 * 4, H);
+    if (net_sel >= 0 && net != net_sel) return;
+  }
+  const float4 g = G4[e4];
+  float4 m = M4[e4], v = V4[e4];
+  const float4 p = P4[e4];
   const float coef = cst[net][0], ss = cst[net][1], b2s = cst[net][2];
   float4 pn;
   pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
