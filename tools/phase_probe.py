@@ -20,9 +20,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
 import satrl._lib as _L  # noqa: E402
 
-probe = len(sys.argv) > 1 and sys.argv[1] == "probe"
+probe = len(sys.argv) > 1 and sys.argv[1].startswith("probe")
 if probe:
-    _L.LIB_PATH = os.path.join(ROOT, "tools", "_probe", "libsatrl_probe.so")
+    _L.LIB_PATH = (os.path.abspath(sys.argv[1][len("probe:"):]) if sys.argv[1].startswith("probe:")
+                   else os.path.join(ROOT, "tools", "_probe", "libsatrl_probe.so"))
 elif len(sys.argv) > 1 and sys.argv[1].endswith(".so"):
     _L.LIB_PATH = os.path.abspath(sys.argv[1])                # an A/B variant build
 print("library:", _L.LIB_PATH)
@@ -61,6 +62,9 @@ if probe:
             print(f"  {names[k]:>14}: {int(np.median(d[0::2])):7d} | {int(np.median(d[1::2])):7d}")
         tot = b[:, 7, w, 1] - b[:, 0, w, 1]
         print(f"  {'total':>14}: {int(np.median(tot[0::2])):7d} | {int(np.median(tot[1::2])):7d}")
+    cyc = (b[:, 7, 0, 1] - b[:, 0, 0, 1]).astype(np.float64)
+    wall = (b[:, 7, 0, 0] - b[:, 0, 0, 0]).astype(np.float64) / 100e6
+    print("shader clock over a workgroup's span (median GHz):", round(float(np.median(cyc / wall)) / 1e9, 3))
     rt = b[:, 0, 0, 0]
     print("start spread (realtime ticks, 100 MHz):", int(rt.max() - rt.min()),
           " end spread:", int(b[:, 7, 0, 0].max() - b[:, 7, 0, 0].min()),
