@@ -170,3 +170,115 @@ def test_env_matches_reference_episode(tmp_path, max_ep):
     assert float(np.max(np.abs(np.asarray(log["r"]) - g[f"r_{max_ep}"]))) <= 1e-9
     gr = float(g[f"return_{max_ep}"])
     assert abs(ret - gr) <= 1e-12 * max(1.0, abs(gr)), (ret, gr)
+
+
+def test_train_loop_matches_reference(tmp_path):
+    """CPPO_main.train_pursuer_network as the reference's __main__ runs it
+    (Sign == 0: pre-trained one_layer pursuer, batch 64, K_epochs 3,
+    d_capture 15000), seed 0, 3 episodes with an update at the end of each
+    (train_loop.npz, tests/golden/capture_train.py).  The reference's
+    observations, rewards, dones and executed actions are forced (the loop is
+    discontinuous, see the module docstring), so the replay buffer each
+    update sees is the reference's.  Checked:
+      * the global RNG stays aligned across choose_action draws and the
+        updates' BatchSampler permutations: every unclamped sample's noise
+        (a - mu) / sigma equals the reference's within 1e-5, for both agents
+        and all 192 steps (episodes 2 and 3 draw after an update);
+      * the evader (never updated) and the pursuer before its first update:
+        means/actions within 2x the per-step f32 forward error bound;
+      * the pursuer's parameters after each update: the bar of
+        test_update_matches_reference (rtol 1e-3, atol 1 % of the Adam
+        travel bound lr * steps).
+    """
+    from satrl import ppo as P
+    from satrl.env import satellites
+    from satrl.trainer import args_param, train_pursuer_network
+    g = golden("train_loop")
+    n = len(g["r"])
+    _write_one_layer_checkpoint(str(tmp_path))
+    rec = {"pursuer": {"a": [], "mu": [], "sig": []}, "evader": {"a": [], "mu": [], "sig": []}}
+    after = []
+    orig_choose, orig_init, orig_step, orig_update = (P.PPO_continuous.choose_action, P.PPO_continuous.__init__,
+                                                      satellites.step, P.PPO_continuous.update)
+    agents = {}
+
+    def init(self, args_, idx, *a, **k):
+        orig_init(self, args_, idx, *a, **k)
+        agents[idx] = self
+        self._who = idx
+
+    def choose(self, s):
+        mu = self.evaluate(s)
+        a, lp = orig_choose(self, s)
+        r = rec[self._who]
+        t = len(r["a"])
+        r["a"].append(a)
+        r["mu"].append(mu)
+        r["sig"].append(np.exp(self.actor.log_std.detach().cpu().numpy().ravel()))
+        if self._who == "pursuer":
+            return g["pa"][t].copy(), g["plogp"][t].copy()
+        return g["ea"][t].copy(), lp
+
+    def step(self, pa, ea, c):
+        t = len(rec["evader"]["a"]) - 1
+        s_ = g["obs_in"][t + 1] if t + 1 < n else g["obs_in"][t]
+        return s_, g["r"][t], bool(g["done"][t])
+
+    def update(self, rb, total_steps):
+        orig_update(self, rb, total_steps)
+        after.append({f"{net}.{k}": v.detach().cpu().numpy().copy()
+                      for net in ("actor", "critic") for k, v in getattr(self, net).state_dict().items()})
+
+    P.PPO_continuous.choose_action, P.PPO_continuous.__init__, P.PPO_continuous.update = choose, init, update
+    satellites.step = step
+    try:
+        torch.manual_seed(0)
+        np.random.seed(0)
+        args = args_param(max_episode_steps=64, batch_size=64, max_train_steps=3, K_epochs=3, chkpt_dir=str(tmp_path))
+        env = satellites(Pursuer_position=np.array([2000000, 2000000, 1000000]),
+                         Pursuer_vector=np.array([1710, 1140, 1300]),
+                         Escaper_position=np.array([1850000, 2000000, 1000000]),
+                         Escaper_vector=np.array([1710, 1140, 1300]), d_capture=50000, args=args)
+        train_pursuer_network(args, env, show_picture=False, pre_train=True, d_capture=15000, max_episodes=3)
+    finally:
+        P.PPO_continuous.choose_action, P.PPO_continuous.__init__, P.PPO_continuous.update = (orig_choose, orig_init,
+                                                                                             orig_update)
+        satellites.step = orig_step
+    assert len(rec["pursuer"]["a"]) == n and len(rec["evader"]["a"]) == n
+    assert len(after) == int(g["n_updates"])
+    # RNG alignment: the standard-normal draw behind every unclamped sample
+    ups = [0] + [int(u) for u in g["update_step"]]
+    for who, key in (("pursuer", "p"), ("evader", "e")):
+        a, mu, sig = (np.asarray(rec[who][k], np.float64) for k in ("a", "mu", "sig"))
+        ga, gmu = g[key + "a"].astype(np.float64), g[key + "mean"].astype(np.float64)
+        gsig = sig.copy()                  # the evader's log_std stays 0 (never updated): sigma 1 on both sides
+        if who == "pursuer":               # the reference's sigma per segment between updates
+            for k in range(len(ups) - 1):
+                ls = golden("policy_one_layer")["actor.log_std"] if k == 0 else g[f"after{k - 1}.actor.log_std"]
+                gsig[ups[k]:ups[k + 1]] = np.exp(ls.astype(np.float64)).ravel()
+        free = (np.abs(a) < 1.6) & (np.abs(ga) < 1.6)
+        eps, geps = (a - mu) / sig, (ga - gmu) / gsig
+        assert free.mean() > 0.3
+        d = np.abs(eps - geps)[free]
+        print(who, "noise draws matched:", int(free.sum()), "max |d eps|", float(d.max()))
+        assert d.max() <= 1e-5, (who, float(d.max()))
+    # forward bounds: the evader throughout, the pursuer before its first update
+    obs = g["obs_in"]
+    sd_e = {k: v.detach().cpu().double().numpy() for k, v in agents["evader"].actor.state_dict().items()}
+    be = _mean_error_bound(sd_e, obs)
+    assert np.all(np.abs(np.asarray(rec["evader"]["mu"]) - g["emean"]) <= 2 * be)
+    sd_p = {k[len("actor."):]: torch.tensor(v).double().numpy() for k, v in
+            ((k, golden("policy_one_layer")[k]) for k in golden("policy_one_layer").files if k.startswith("actor."))}
+    u0 = ups[1]
+    bp = _mean_error_bound(sd_p, obs[:u0])
+    assert np.all(np.abs(np.asarray(rec["pursuer"]["mu"][:u0]) - g["pmean"][:u0]) <= 2 * bp)
+    # parameters after each update
+    lr = float(args.lr_a)
+    print("worst param diff per update:",
+          [max(float(np.abs(v - g[f"after{k}.{nm}"]).max()) for nm, v in got.items()) for k, got in enumerate(after)])
+    for k, got in enumerate(after):
+        steps = 3 * (k + 1)
+        for name, v in got.items():
+            ref = g[f"after{k}.{name}"]
+            assert np.allclose(v, ref, rtol=1e-3, atol=2 * lr * steps * 0.01 + 1e-6), (k, name,
+                                                                                      float(np.abs(v - ref).max()))
