@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=6.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
+    ap.add_argument("--graph-group", type=int, default=64, help="minibatches per replayed update hipGraph")
     ap.add_argument("--force-dist", action="store_true",
                     help="init the nccl process group even at world size 1 (rehearses the DP update path)")
     ap.add_argument("--surrogate", action="store_true",
@@ -174,7 +175,8 @@ def main():
     from satrl.trainer import VecTrainer, args_param
     args = args_param(batch_size=a.num_envs * a.horizon, mini_batch_size=a.minibatch, hidden_width=a.hidden,
                       K_epochs=a.epochs, max_episode_steps=1000, num_envs=a.num_envs, horizon=a.horizon, seed=0,
-                      max_train_steps=int(3e6), chkpt_dir="/tmp", surrogate=a.surrogate)
+                      max_train_steps=int(3e6), chkpt_dir="/tmp", surrogate=a.surrogate,
+                      update_graph_group=a.graph_group)
     tr = VecTrainer(args, flag=0, d_capture=a.d_capture, pg=pg, env_offset=rank * a.num_envs)
 
     def barrier():

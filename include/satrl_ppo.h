@@ -108,6 +108,16 @@ int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const 
  * ppo_continuous.py:200-201                                               */
 int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float* v_out, void* stream);
 
+/* Minibatch staging for a graph-replayed group of minibatches
+ * (BatchSampler(SubsetRandomSampler) order, ppo_continuous.py:217): rows
+ * [0, rows) of stage f32 [rows][32] = src[perm[group[0] * rows + r]] (packed
+ * transition rows, 32 f32 each), with group a device i64 counter, so the
+ * replayed graph walks the epoch's permutation without a host copy.
+ * satrl_ppo_group_advance: group[0] += 1 (the last node of such a graph).  */
+int satrl_ppo_stage(int64_t rows, const float* src, const int64_t* perm, const int64_t* group, float* stage,
+                    void* stream);
+int satrl_ppo_group_advance(int64_t* group, void* stream);
+
 const char* satrl_ppo_last_error(void);
 
 #ifdef __cplusplus

@@ -869,6 +869,21 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   }
 }
 
+// ---------------------------------------------------------------------------
+// stage: the rows of a group of minibatches gathered contiguously, at the
+// permutation offset a device counter holds (8 lanes x float4 per 128-B row)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) stage_kernel(int64_t rows, const float4* __restrict__ src,
+                                                    const int64_t* __restrict__ perm,
+                                                    const int64_t* __restrict__ group, float4* __restrict__ stage) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, r = t >> 3;
+  if (r >= rows) return;
+  const int64_t row = perm[group[0] * rows + r];
+  stage[t] = src[row * 8 + (t & 7)];
+}
+
+__global__ void group_advance_kernel(int64_t* group) { group[0] += 1; }
+
 int n_head_wg(int mb) { return (mb + kRows - 1) / kRows; }
 int n_w1_wg(int mb) { return n_head_wg(mb); }
 RedGeom geom(int H, int mb, int S, int net = -1) {
@@ -1000,6 +1015,22 @@ int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* step
   const int nblk = n_blocks(geom(H, mb, 1, net));
   hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq,
                      steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T, net);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_ppo_stage(int64_t rows, const float* src, const int64_t* perm, const int64_t* group, float* stage,
+                    void* stream) {
+  if (rows <= 0 || !src || !perm || !group || !stage) return -1;
+  hipLaunchKernelGGL(stage_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, rows,
+                     reinterpret_cast<const float4*>(src), perm, group, reinterpret_cast<float4*>(stage));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_ppo_group_advance(int64_t* group, void* stream) {
+  if (!group) return -1;
+  hipLaunchKernelGGL(group_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, group);
   LAUNCH_CHECK();
   return 0;
 }

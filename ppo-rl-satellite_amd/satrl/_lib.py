@@ -101,6 +101,8 @@ _SIGS = {
     "satrl_policy_act": ([C.c_int, _i64, _vp, _vp, _vp, C.c_float, C.c_uint64, _i64, C.c_uint64, _vp, _vp, _vp, _vp,
                           _vp, _vp], C.c_int),
     "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_stage": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_group_advance": ([_vp, _vp], C.c_int),
     "satrl_ppo_last_error": ([], C.c_char_p),
 }
 

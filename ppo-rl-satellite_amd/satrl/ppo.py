@@ -223,6 +223,11 @@ class FusedMinibatch:
         self.side = torch.cuda.Stream(device=dev) if self.split and torch.cuda.is_available() else None
         self.graph = None
         self._src_ptr = None
+        # graph replays walk the epoch's permutation through a device group
+        # counter (satrl_ppo_stage / satrl_ppo_group_advance): no host copy
+        # or host round trip between groups
+        self.perm_buf = None
+        self.grp = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def rowpass(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass alone (a pure function of src, idx and the
@@ -326,6 +331,19 @@ class FusedMinibatch:
                 self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
         self._chains(chain)
 
+    def _group_dev(self, src):
+        """One graph group: stage the rows of the next `group` minibatches of
+        self.perm_buf (offset grp[0]), step them, advance grp."""
+        mb, G = self.mb, self.group
+        check(_lib.lib().satrl_ppo_stage(G * mb, ptr(src), ptr(self.perm_buf), ptr(self.grp), ptr(self.stage),
+                                         stream_ptr()), "satrl_ppo_stage")
+
+        def chain(net):
+            for k in range(G):
+                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
+        self._chains(chain)
+        check(_lib.lib().satrl_ppo_group_advance(ptr(self.grp), stream_ptr()), "satrl_ppo_group_advance")
+
     def _capture(self, src):
         if self.lib_gemm:
             # hipBLASLt sets up a GEMM shape on its first call per stream, which is
@@ -341,7 +359,7 @@ class FusedMinibatch:
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self._group(src, self.group)
+            self._group_dev(src)
         self._src_ptr = src.data_ptr()
 
     def run(self, src, perm):
@@ -351,15 +369,22 @@ class FusedMinibatch:
         nfull = B // mb
         graphable = self.use_graph and torch.cuda.is_available() and (self.L.pg is None or self.L.comm is not None)
         k = 0
-        while k < nfull:
+        if graphable and nfull >= G:
+            if self.perm_buf is None or self.perm_buf.numel() < B:
+                self.perm_buf = torch.empty(B, dtype=torch.int64, device=perm.device)
+                self.graph = None
+            if perm.data_ptr() != self.perm_buf.data_ptr():
+                self.perm_buf[:B].copy_(perm)
+            if self.graph is None or self._src_ptr != src.data_ptr():
+                self._capture(src)
+            self.grp.zero_()
+            for _ in range(nfull // G):
+                self.graph.replay()
+            k = (nfull // G) * G
+        while k < nfull:                      # the rest of the full minibatches, eagerly
             ng = min(G, nfull - k)
             self.idx[:ng].copy_(perm[k * mb:(k + ng) * mb].view(ng, mb))
-            if graphable and ng == G:
-                if self.graph is None or self._src_ptr != src.data_ptr():
-                    self._capture(src)
-                self.graph.replay()
-            else:
-                self._group(src, ng)
+            self._group(src, ng)
             k += ng
         if B % mb:
             tail = perm[nfull * mb:].contiguous()

@@ -35,7 +35,7 @@ class args_param:  # noqa: N801
                  use_state_norm=True, use_reward_norm=False, use_reward_scaling=True, entropy_coef=0.01,
                  use_lr_decay=True, use_grad_clip=True, use_orthogonal_init=True, set_adam_eps=True, use_tanh=True,
                  chkpt_dir="/mnt/datab/home/yuanwenzheng/PICTURE1",
-                 num_envs=1, horizon=None, seed=0, rollout_graph_chunk=64, update_graph_group=16, device=None,
+                 num_envs=1, horizon=None, seed=0, rollout_graph_chunk=64, update_graph_group=64, device=None,
                  surrogate=False):
         self.max_train_steps = max_train_steps
         self.evaluate_freq = evaluate_freq

@@ -235,6 +235,36 @@ def test_rowpass_contiguous_rows_match_gather():
         assert torch.equal(a, b)
 
 
+def test_update_graph_groups_equal_eager():
+    """FusedMinibatch.run: graph replays that walk the permutation through the
+    device group counter (satrl_ppo_stage / satrl_ppo_group_advance), then
+    the eager remainder groups and the ragged tail minibatch == the same epoch
+    stepped eagerly, bitwise (parameters, Adam moments, step counters), over
+    two epochs (the counter restarts per epoch)."""
+    from satrl.ppo import PPOLearner
+    mb, G = 256, 4
+    B = (2 * G + 3) * mb + 17                      # 2 graph groups, 3 eager minibatches, a 17-row tail
+    res = []
+    for use_graph in (True, False):
+        torch.manual_seed(11)
+        args = _args(hidden_width=64, mini_batch_size=mb, batch_size=B)
+        L = PPOLearner(args, "pursuer", graph_group=G, use_graph=use_graph)
+        g = torch.Generator(device="cuda").manual_seed(2)
+        src = torch.randn((B, 32), device="cuda", generator=g)
+        src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+        perms = [torch.randperm(B, device="cuda", generator=g) for _ in range(2)]
+        L.sync_w2t()
+        st = L.stepper(mb)
+        for p in perms:
+            st.run(src, p)
+        torch.cuda.synchronize()
+        if use_graph:
+            assert st.graph is not None and int(st.grp.item()) == 2
+        res.append((L.P.clone(), L.M.clone(), L.V.clone(), L.steps.clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_policy_act_and_value_kernels():
     """satrl_policy_act / satrl_policy_value vs the torch modules + satrl_gaussian_sample
     (same Philox draw); every row independent of N and of its position (bitwise)."""
