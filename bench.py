@@ -283,6 +283,25 @@ def main():
                                 "hbm_frac": gbs / HBM_PEAK_GBS}
         del e_sw, acts
 
+    # ---- north-star sweep, end to end: the rollout (both agents' policy kernel ->
+    # Philox sampling -> env step, hipGraph chunks) at num_envs 4k / 16k / 64k, a
+    # 256-step horizon after one untimed collect (graphs captured, episodes mid-flight)
+    rollout_sweep = {}
+    for n_sw in (4096, 16384, 65536):
+        a_sw = args_param(batch_size=n_sw * 256, mini_batch_size=a.minibatch, hidden_width=a.hidden, K_epochs=1,
+                          max_episode_steps=1000, num_envs=n_sw, horizon=256, seed=0, max_train_steps=int(3e6),
+                          chkpt_dir="/tmp")
+        tr_sw = VecTrainer(a_sw, flag=0, d_capture=a.d_capture)
+        tr_sw.collect()
+        torch.cuda.synchronize()
+        e0.record()
+        tr_sw.collect()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        rollout_sweep[str(n_sw)] = {"ms_per_256_steps": ms, "env_steps_per_s": n_sw * 256 / (ms * 1e-3)}
+        del tr_sw
+
     # ---- §8f propagators: RK4 two-body + J2 batch kernel, and the env step in RK4-CW mode
     from satrl.env import rk4_j2
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -373,6 +392,7 @@ def main():
                        "d_capture": a.d_capture, "parallelism": f"dp{world}"},
             "ppo_updates_per_s": a.steps / elapsed,
             "rollout_env_steps_per_s": n_total * a.horizon / (rollout_ms * 1e-3),
+            "rollout_sweep_num_envs": rollout_sweep,
             "rollout_ms": rollout_ms, "gae_ms": gae_ms, "update_ms": update_ms,
             "env_kernel_env_steps_per_s": a.num_envs / (env_us * 1e-6),
             "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
