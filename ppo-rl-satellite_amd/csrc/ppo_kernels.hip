@@ -512,7 +512,14 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
 // rows per policy/value workgroup (64-row tiles measured 62 vs 58.5 us per
 // rollout step at 16k envs: fewer, larger workgroups lose more to the tail
 // than the halved weight ingest saves)
-constexpr int kPolRows = 32;
+#ifndef SATRL_POL_ROWS
+#define SATRL_POL_ROWS 32
+#endif
+#ifndef SATRL_POL_NW256
+#define SATRL_POL_NW256 16
+#endif
+constexpr int kPolRows = SATRL_POL_ROWS;   // rows per policy workgroup
+constexpr int kPolNW = SATRL_POL_NW256;    // waves per policy workgroup at H = 256
 
 template <int H, int NW, int MODE>
 __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float* __restrict__ obs,
@@ -1053,7 +1060,7 @@ int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const 
     hipLaunchKernelGGL((policy_kernel<128, 8, 0>), g, dim3(512), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
                        k10, k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
   else
-    hipLaunchKernelGGL((policy_kernel<256, 16, 0>), g, dim3(1024), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
+    hipLaunchKernelGGL((policy_kernel<256, kPolNW, 0>), g, dim3(kPolNW * 64), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
                        k10, k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
   LAUNCH_CHECK();
   return 0;
@@ -1070,7 +1077,7 @@ int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float
     hipLaunchKernelGGL((policy_kernel<128, 8, 1>), g, dim3(512), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
                        (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
   else
-    hipLaunchKernelGGL((policy_kernel<256, 16, 1>), g, dim3(1024), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
+    hipLaunchKernelGGL((policy_kernel<256, kPolNW, 1>), g, dim3(kPolNW * 64), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
                        (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
   LAUNCH_CHECK();
   return 0;
