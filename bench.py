@@ -378,9 +378,10 @@ def main():
     n_minibatches = a.epochs * ((a.num_envs * a.horizon) // a.minibatch)
 
     if rank == 0:
-        cpu = None if a.no_cpu_baseline else cpu_baseline(a.cpu_baseline_seconds, a.num_envs, a.horizon, a.hidden,
-                                                            a.minibatch, a.epochs)
-        rd_cpu_ms = None if a.no_cpu_baseline else rd_cpu_baseline()
+        host_baseline = not a.no_cpu_baseline and world == 1          # rank 0 at N = 1 only
+        cpu = cpu_baseline(a.cpu_baseline_seconds, a.num_envs, a.horizon, a.hidden, a.minibatch,
+                           a.epochs) if host_baseline else None
+        rd_cpu_ms = rd_cpu_baseline() if host_baseline else None
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
