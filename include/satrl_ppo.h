@@ -118,6 +118,11 @@ int satrl_ppo_stage(int64_t rows, const float* src, const int64_t* perm, const i
                     void* stream);
 int satrl_ppo_group_advance(int64_t* group, void* stream);
 
+/* y[i] = tanh(x[i]) f32 [n], with the activation every MLP kernel above uses
+ * for torch.tanh in Actor_Gaussian / Critic.forward (ppo_continuous.py:61-134):
+ * the hook of its exhaustive accuracy test.                               */
+int satrl_ppo_tanh(int64_t n, const float* x, float* y, void* stream);
+
 const char* satrl_ppo_last_error(void);
 
 #ifdef __cplusplus

@@ -121,6 +121,31 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// tanh of the MLP activations (fc1, fc2, mean layer).  The split of Cephes
+// tanhf: |x| < 0.625 an odd minimax polynomial, else 1 - 2/(e^{2|x|} + 1) on
+// the hardware v_exp_f32 / v_rcp_f32; both arms straight-line, then a select.
+// Within 2 ulp of the correctly rounded tanh over every f32 (GPU test
+// test_tanh_f32_ulp, exhaustive), in ~15 VALU ops where the library tanhf's
+// accurate exp and IEEE division take ~3x that.  Every MLP kernel (rollout
+// policy/value, update rowpass) calls this one function, so logp_old from the
+// rollout still equals the update's recomputation bit for bit.
+// SATRL_LIB_TANH (development A/B only) switches back to the library tanhf.
+__device__ __forceinline__ float tanh_f32(float x) {
+#ifdef SATRL_LIB_TANH
+  return tanhf(x);
+#else
+  const float y = fabsf(x), z = x * x;
+  float p = fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f);
+  p = fmaf(p, z, -5.37397155531e-2f);
+  p = fmaf(p, z, 1.33314422036e-1f);
+  p = fmaf(p, z, -3.33332819422e-1f);
+  const float small = fmaf(p * z, x, x);
+  const float e = __builtin_amdgcn_exp2f(y * 2.8853900817779268f);        // e^{2|x|}; inf -> rcp 0 -> 1
+  const float big = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+  return y < 0.625f ? small : copysignf(big, x);                          // NaN -> big arm -> NaN
+#endif
+}
+
 template <int CT>
 __device__ __forceinline__ void b_chunk(const float* __restrict__ bp, int LDB, float4 (&b)[CT][2]) {
 #pragma unroll
@@ -262,7 +287,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 16 * rt + 4 * lg + j;
-        const float h = tanhf(acc[rt][t][j]);                      // fc1 + tanh
+        const float h = tanh_f32(acc[rt][t][j]);                   // fc1 + tanh
         h1[rt][t][j] = h;
         sm.h1s[r][n] = h;
         if (h1out != nullptr && r < nvalid) h1out[(int64_t)r * H + n] = h;
@@ -292,7 +317,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
     for (int t = 0; t < CT; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float h = tanhf(acc[rt][t][j] + b2v[t]);              // fc2 + tanh
+        const float h = tanh_f32(acc[rt][t][j] + b2v[t]);           // fc2 + tanh
         acc[rt][t][j] = h;
 #pragma unroll
         for (int q = 0; q < 3; ++q) p[q][rt][j] = fmaf(h, w3[t][q], p[q][rt][j]);
@@ -370,7 +395,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanhf(out_sum<NW, kRows>(sm.osum, r, d) + hb3[d]);
+          th[d] = tanh_f32(out_sum<NW, kRows>(sm.osum, r, d) + hb3[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           const float sd = expf(hls[d]);
           var[d] = sd * sd;
@@ -561,7 +586,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   float* logp = agent == 0 ? logp0 : logp1;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const float mu = max_action * tanhf(out_sum<NW, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
+    const float mu = max_action * tanh_f32(out_sum<NW, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
     gaussian_act(mu, P[L.ls + d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
   }
 }
@@ -891,6 +916,11 @@ __global__ void __launch_bounds__(256) stage_kernel(int64_t rows, const float4* 
 
 __global__ void group_advance_kernel(int64_t* group) { group[0] += 1; }
 
+__global__ void __launch_bounds__(256) tanh_kernel(int64_t n, const float* __restrict__ x, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = tanh_f32(x[i]);
+}
+
 int n_head_wg(int mb) { return (mb + kRows - 1) / kRows; }
 int n_w1_wg(int mb) { return n_head_wg(mb); }
 RedGeom geom(int H, int mb, int S, int net = -1) {
@@ -1079,6 +1109,13 @@ int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float
   else
     hipLaunchKernelGGL((policy_kernel<256, kPolNW, 1>), g, dim3(kPolNW * 64), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
                        (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_ppo_tanh(int64_t n, const float* x, float* y, void* stream) {
+  if (n <= 0 || n > (int64_t)256 * 0x7FFFFFFF || !x || !y) return -1;
+  hipLaunchKernelGGL(tanh_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, x, y);
   LAUNCH_CHECK();
   return 0;
 }

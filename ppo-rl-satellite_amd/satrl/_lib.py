@@ -103,6 +103,7 @@ _SIGS = {
     "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_stage": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_group_advance": ([_vp, _vp], C.c_int),
+    "satrl_ppo_tanh": ([_i64, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_last_error": ([], C.c_char_p),
 }
 

@@ -43,6 +43,45 @@ def test_gae_kernel_on_reference_buffer():
     assert np.array_equal(vt.cpu().numpy(), u["v_target"].reshape(-1))
 
 
+TANH_MAX_ULP = 2
+
+
+def test_tanh_f32_ulp():
+    """The MLP kernels' activation (ppo_kernels.hip tanh_f32, torch.tanh at
+    ppo_continuous.py:61-134) over EVERY non-negative f32 incl. +inf: within
+    TANH_MAX_ULP of tanh evaluated in f64 and rounded once to f32.  It is odd
+    by construction: negatives spot-checked bitwise, NaN propagates."""
+    import satrl._lib as _L
+    lib, sp = _L.lib(), _L.stream_ptr()
+    top = 0x7F800000                                                   # +inf
+    n = 1 << 27
+    y = torch.empty(n, device="cuda")
+    worst, worst_x = 0, 0.0
+    for c in range(0, top + 1, n):
+        bits = torch.arange(c, min(c + n, top + 1), dtype=torch.int32, device="cuda")
+        x = bits.view(torch.float32)
+        m = x.numel()
+        assert lib.satrl_ppo_tanh(m, _L.ptr(x), _L.ptr(y), sp) == 0
+        ref = torch.tanh(x.double()).float()
+        d = (y[:m].view(torch.int32) - ref.view(torch.int32)).abs()
+        k = int(d.argmax())
+        if int(d[k]) > worst:
+            worst, worst_x = int(d[k]), float(x[k])
+    print(f"tanh_f32: max {worst} ulp (at x = {worst_x!r})")
+    assert worst <= TANH_MAX_ULP, (worst, worst_x)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(1 << 20, device="cuda", generator=g) * 4
+    yp, yn = torch.empty_like(x), torch.empty_like(x)
+    assert lib.satrl_ppo_tanh(x.numel(), _L.ptr(x), _L.ptr(yp), sp) == 0
+    xn = -x
+    assert lib.satrl_ppo_tanh(x.numel(), _L.ptr(xn), _L.ptr(yn), sp) == 0
+    assert torch.equal(yn, -yp)
+    nan = torch.tensor([float("nan"), float("-inf")], device="cuda")
+    out = torch.empty_like(nan)
+    assert lib.satrl_ppo_tanh(2, _L.ptr(nan), _L.ptr(out), sp) == 0
+    assert torch.isnan(out[0]) and float(out[1]) == -1.0
+
+
 def test_gaussian_sample_logprob_and_stats():
     from satrl.ppo import gaussian_sample
     N = 200000
