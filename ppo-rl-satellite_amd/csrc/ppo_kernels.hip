@@ -177,11 +177,39 @@ __device__ __forceinline__ void mfma_chunk(const float* __restrict__ ap, const f
   }
 }
 
+// the LDS A operand of one 32-wide k chunk, and the chunk's MFMAs on operands
+// already in registers
+template <int LDA, int RT>
+__device__ __forceinline__ void a_chunk(const float* __restrict__ ap, float4 (&a)[RT][2]) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    a[rt][0] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA);
+    a[rt][1] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA + 4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int RT, int CT>
+__device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4 (&b)[CT][2], f4 (&acc)[RT][CT]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int t = 0; t < CT; ++t) acc[rt][t] = mfma4(a[rt][h][e], b[t][h][e], acc[rt][t]);
+}
+
 // acc[rt][t] += A[16rt.. +16][K] (LDS, row stride LDA) x B^T with B[n][k]
 // row-major (ld LDB) for columns n0 + 16t, in 32-wide k chunks.  Chunk pairs
 // with two register buffers in a rolled loop (prefetch distance one chunk);
 // loads unconditional and the last pair peeled, so every vmcnt wait is exact.
-template <int K, int LDA, int LDB, int RT, int CT>
+// APRE: the LDS A chunk is double-buffered the same way, so a chunk's MFMAs
+// do not start behind a fresh ds_read's latency (the rowpass: 34.7 -> 33.6
+// us).  It costs 16 VGPRs, which the policy kernel's occupancy does not
+// afford (59 -> 63 us per rollout step), so there it is off; the MFMA
+// sequence, hence every result bit, is the same either way.
+template <int K, int LDA, int LDB, int RT, int CT, bool APRE>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
                                           f4 (&acc)[RT][CT]) {
   constexpr int NC = K / 32;
@@ -190,17 +218,36 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   const float* ap = A + i * LDA + 8 * g;
   const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
   float4 x[CT][2], y[CT][2];
-  b_chunk<CT>(bp, LDB, x);
+  if constexpr (APRE) {
+    float4 ax[RT][2], ay[RT][2];
+    b_chunk<CT>(bp, LDB, x);
+    a_chunk<LDA, RT>(ap, ax);
 #pragma unroll 1
-  for (int c = 0; c < NC - 2; c += 2) {
-    b_chunk<CT>(bp + 32 * (c + 1), LDB, y);
-    mfma_chunk<LDA, RT, CT>(ap + 32 * c, x, acc);
-    b_chunk<CT>(bp + 32 * (c + 2), LDB, x);
-    mfma_chunk<LDA, RT, CT>(ap + 32 * (c + 1), y, acc);
+    for (int c = 0; c < NC - 2; c += 2) {
+      b_chunk<CT>(bp + 32 * (c + 1), LDB, y);
+      a_chunk<LDA, RT>(ap + 32 * (c + 1), ay);
+      mfma_regs<RT, CT>(ax, x, acc);
+      b_chunk<CT>(bp + 32 * (c + 2), LDB, x);
+      a_chunk<LDA, RT>(ap + 32 * (c + 2), ax);
+      mfma_regs<RT, CT>(ay, y, acc);
+    }
+    b_chunk<CT>(bp + 32 * (NC - 1), LDB, y);
+    a_chunk<LDA, RT>(ap + 32 * (NC - 1), ay);
+    mfma_regs<RT, CT>(ax, x, acc);
+    mfma_regs<RT, CT>(ay, y, acc);
+  } else {
+    b_chunk<CT>(bp, LDB, x);
+#pragma unroll 1
+    for (int c = 0; c < NC - 2; c += 2) {
+      b_chunk<CT>(bp + 32 * (c + 1), LDB, y);
+      mfma_chunk<LDA, RT, CT>(ap + 32 * c, x, acc);
+      b_chunk<CT>(bp + 32 * (c + 2), LDB, x);
+      mfma_chunk<LDA, RT, CT>(ap + 32 * (c + 1), y, acc);
+    }
+    b_chunk<CT>(bp + 32 * (NC - 1), LDB, y);
+    mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 2), x, acc);
+    mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 1), y, acc);
   }
-  b_chunk<CT>(bp + 32 * (NC - 1), LDB, y);
-  mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 2), x, acc);
-  mfma_chunk<LDA, RT, CT>(ap + 32 * (NC - 1), y, acc);
 }
 
 // Shared-memory block and forward pass (phases A, B and the output-layer dot
@@ -222,7 +269,7 @@ struct MlpSmem {
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
 // tanh(fc1) goes to h1out[r * H + n].
-template <int H, int NW, int R, class Gather>
+template <int H, int NW, int R, bool APRE, class Gather>
 __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P, int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
                                             f4 (&acc)[R / 16][H / 16 / NW],
@@ -299,7 +346,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  mfma_rows<H, LDA, H, RT, CT>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -383,7 +430,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
       if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
     }
   };
-  mlp_forward<H, NW, kRows>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  mlp_forward<H, NW, kRows, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -494,7 +541,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows<H, LDA, H, RT, CT>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc);
+  mfma_rows<H, LDA, H, RT, CT, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
@@ -571,7 +618,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW, R>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  mlp_forward<H, NW, R, false>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
