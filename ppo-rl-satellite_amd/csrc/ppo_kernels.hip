@@ -867,6 +867,9 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
 // float4 per thread, and the updated tile goes out transposed through LDS
 // into W2T (coalesced).  Blocks [nbw, ...): the rest of the layout, float4.
 // ---------------------------------------------------------------------------
+#ifndef SATRL_ADAM_EARLY
+#define SATRL_ADAM_EARLY 1
+#endif
 __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float step_size,
                                            float bc2s, float w1, float w2, float beta2, float eps, int use_clip) {
   if (use_clip) g = g * coef;                                      // grads.mul_(clip_coef_clamped)
@@ -888,8 +891,55 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   __shared__ float cst[2][3];                                      // coef, step_size, bc2_sqrt per net
   __shared__ float tile[32][33];
   const int t = threadIdx.x;
+  const int ntc = H / 32, nbw = (net_sel < 0 ? 2 : 1) * ntc * ntc;
+  // this thread's element (float4) and net, and whether it has one
+  int64_t e4;
+  int net;
+  bool live = true;
+  if ((int)blockIdx.x < nbw) {
+    const int tb = blockIdx.x % (ntc * ntc);
+    net = net_sel < 0 ? (int)(blockIdx.x / (ntc * ntc)) : net_sel;
+    const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
+    e4 = ((int64_t)net * H * H + (int64_t)n * H + k) / 4;
+  } else {
+    e4 = L.W1 / 4 + (int64_t)(blockIdx.x - nbw) * 256 + t;
+    live = e4 < L.total / 4;
+    net = live ? net_of(L, e4 * 4, H) : 0;
+    live = live && (net_sel < 0 || net == net_sel);
+  }
+#if SATRL_ADAM_EARLY
+  // the norm partials' loads go out first, this thread's G/M/V/P right
+  // behind them: the fold below waits only for the partials (vmcnt is in
+  // order), so the operand latency overlaps the fold
+  // (all loads unconditional on clamped indices, so none becomes a branch)
+  const double2* nsq2 = reinterpret_cast<const double2*>(nsq);
+  double2 pn2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pn2[i] = nsq2[min(t + 256 * i, nblk - 1)];
+  const float4* G4 = reinterpret_cast<const float4*>(G);
+  float4* P4 = reinterpret_cast<float4*>(P);
+  float4* M4 = reinterpret_cast<float4*>(M);
+  float4* V4 = reinterpret_cast<float4*>(V);
+  const int64_t el = live ? e4 : 0;
+  const float4 g = G4[el];
+  float4 m = M4[el], v = V4[el];
+  const float4 p = P4[el];
+  double a = 0.0, c = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {                                    // k = t, t+256, ... in order, as the loop
+    // x * 1.0 == x, x * 0.0 + a == a for these non-negative sums: bitwise the
+    // loop's skip, without a branch the compiler would sink the load into
+    const double in = t + 256 * i < nblk ? 1.0 : 0.0;
+    a += pn2[i].x * in;
+    c += pn2[i].y * in;
+  }
+  if (nblk > 1024) {                                               // (not at the sizes in use)
+    for (int k = t + 1024; k < nblk; k += 256) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
+  }
+#else
   double a = 0.0, c = 0.0;
   for (int k = t; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
+#endif
   block_sum2(a, c, sh);
   if (t < 2 && (net_sel < 0 || net_sel == t)) {
     const double nn = t == 0 ? a : c;
@@ -906,27 +956,16 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   __syncthreads();
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
-  const int ntc = H / 32, nbw = (net_sel < 0 ? 2 : 1) * ntc * ntc;
+  if (!live) return;                                               // (W1.. tail blocks only: no barrier follows)
+#if !SATRL_ADAM_EARLY
   const float4* G4 = reinterpret_cast<const float4*>(G);
   float4* P4 = reinterpret_cast<float4*>(P);
   float4* M4 = reinterpret_cast<float4*>(M);
   float4* V4 = reinterpret_cast<float4*>(V);
-  int64_t e4;
-  int net;
-  if ((int)blockIdx.x < nbw) {
-    const int tb = blockIdx.x % (ntc * ntc);
-    net = net_sel < 0 ? (int)(blockIdx.x / (ntc * ntc)) : net_sel;
-    const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
-    e4 = ((int64_t)net * H * H + (int64_t)n * H + k) / 4;
-  } else {
-    e4 = L.W1 / 4 + (int64_t)(blockIdx.x - nbw) * 256 + t;
-    if (e4 >= L.total / 4) return;                                 // (no barrier follows in this branch)
-    net = net_of(L, e4 * 4, H);
-    if (net_sel >= 0 && net != net_sel) return;
-  }
   const float4 g = G4[e4];
   float4 m = M4[e4], v = V4[e4];
   const float4 p = P4[e4];
+#endif
   const float coef = cst[net][0], ss = cst[net][1], b2s = cst[net][2];
   float4 pn;
   pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
