@@ -69,6 +69,15 @@ if probe:
     print("start spread (realtime ticks, 100 MHz):", int(rt.max() - rt.min()),
           " end spread:", int(b[:, 7, 0, 0].max() - b[:, 7, 0, 0].min()),
           " kernel span:", int(b[:, 7, 0, 0].max() - rt.min()))
+    # where the tail comes from: end times (ticks after the first start) by
+    # XCD (round-robin dispatch: blockIdx % 8; the actor on even ones) and
+    # the start of phase B / D (stamps 1 and 5) per XCD
+    end = b[:, 7, 0, 0] - rt.min()
+    for name, k in (("start B", 1), ("start D", 5), ("end", 7)):
+        v = b[:, k, 0, 0] - rt.min()
+        print(f"  {name:>8} by XCD (median / max ticks):",
+              " ".join(f"{int(np.median(v[x::8]))}/{int(v[x::8].max())}" for x in range(8)))
+    print("  slowest 8 workgroups:", [(int(i), int(end[i])) for i in np.argsort(end)[-8:]])
 
 # event timings of each launch of one minibatch step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
