@@ -45,6 +45,47 @@ def test_host_helpers_without_gpu():
     assert np.array_equal(E.stm(100.0), O.stm(100.0))
 
 
+def test_entry_points_reject_bad_arguments_before_any_device_call():
+    """Error behaviour of the boundary (include/*.h: 0 ok, negative codes):
+    shapes, widths and null pointers are checked on the host before any HIP
+    call, so these run without a GPU.  A non-null dummy pointer is never
+    dereferenced on these paths."""
+    import ctypes as C
+    import satrl._lib as L
+    from satrl import env as E
+    lib = L.lib()
+    fake = C.c_void_p(16)                       # never touched: every call below fails its host checks
+    # satenv_create: null out / null params / num_envs <= 0 / bad propagator -> SATENV_ERR_ARG (-1)
+    p = E.default_params()
+    h = C.c_void_p()
+    assert lib.satenv_create(None, 4, C.byref(p), 0) == -1
+    assert lib.satenv_create(C.byref(h), 4, None, 0) == -1
+    assert lib.satenv_create(C.byref(h), 0, C.byref(p), 0) == -1
+    assert b"bad arguments" in lib.satenv_last_error()
+    bad = E.default_params()
+    bad.propagator = 7
+    assert lib.satenv_create(C.byref(h), 4, C.byref(bad), 0) == -1
+    assert b"propagator" in lib.satenv_last_error()
+    # learner side: unsupported hidden width, empty minibatch, net out of range, null buffers
+    off = (C.c_int64 * 16)()
+    assert lib.satrl_ppo_layout(100, off) == -1 and lib.satrl_ppo_layout(256, off) == 0
+    assert lib.satrl_ppo_sizes(256, 0, None, None) == -1
+    args = [fake, None, fake, fake, 0.1, 0.01, 1.6, fake, fake, fake, fake, None]
+    assert lib.satrl_ppo_rowpass(100, 64, -1, *args) == -1                     # H not 64/128/256
+    assert lib.satrl_ppo_rowpass(256, 0, -1, *args) == -1                      # empty minibatch
+    assert lib.satrl_ppo_rowpass(256, 64, 2, *args) == -1                      # net not -1/0/1
+    assert lib.satrl_ppo_rowpass(256, 64, -1, None, *args[1:]) == -1           # null rows
+    assert lib.satrl_ppo_dw2(256, 4096, -1, 0, fake, fake, fake, None) == -1   # S < 1
+    assert lib.satrl_ppo_dw2(256, 64, -1, 64, fake, fake, fake, None) == -1    # an empty split
+    assert lib.satrl_ppo_reduce(256, 64, -1, 1, 4, fake, fake, fake, fake, fake, fake, None) == -1   # mode
+    assert lib.satrl_ppo_reduce(256, 64, -1, 1, 2, fake, fake, fake, fake, None, None, None) == -1   # no nsq
+    assert lib.satrl_gae(0, 4, fake, fake, fake, 0.99, 0.95, fake, fake, None) == -1
+    assert lib.satrl_gae(4, 4, fake, None, fake, 0.99, 0.95, fake, fake, None) == -1
+    assert lib.satrl_policy_act(256, 8, fake, fake, fake, 1.6, 0, 0, 0, None, fake, fake, None, None,
+                                None) == -1                                   # second agent without outputs
+    assert lib.satrl_ppo_tanh(0, fake, fake, None) == -1
+
+
 def test_product_has_no_cpu_fallback():
     import torch
     from satrl import env as E

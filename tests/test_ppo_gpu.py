@@ -179,19 +179,22 @@ def test_update_matches_reference():
     assert abs(la - u["lr_after"][0]) <= 1e-6 * u["lr_after"][0] and abs(lc - u["lr_after"][1]) <= 1e-6 * u["lr_after"][1]
 
 
-@pytest.mark.parametrize("H,split", [(64, False), (256, False), (256, True)])
-def test_fused_step_vs_torch_autograd(H, split):
+@pytest.mark.parametrize("H,split,mb", [(64, False, 512), (256, False, 512), (256, True, 512),
+                                         (256, False, 777), (64, False, 100)])
+def test_fused_step_vs_torch_autograd(H, split, mb):
     """satrl_ppo_rowpass (f32 MFMA) + hipBLASLt dW2 + reduce + Adam vs plain torch fp32 autograd +
-    clip_grad_norm_ + torch.optim.Adam on the same minibatch."""
+    clip_grad_norm_ + torch.optim.Adam on the same minibatch; mb 777 / 100 are
+    ragged (the last BatchSampler minibatch with drop_last=False, a partial
+    32-row block and split-K remainder)."""
     from satrl.ppo import PPOLearner
     from torch_reference import reference_step
     torch.manual_seed(11)
-    args = _args(hidden_width=H, mini_batch_size=512, batch_size=4096)
+    args = _args(hidden_width=H, mini_batch_size=mb, batch_size=4096)
     L = PPOLearner(args, "pursuer", use_graph=False)
     with torch.no_grad():                      # non-trivial weights (reference init has mean_layer gain 0.01)
         for p in list(L.actor.parameters()) + list(L.critic.parameters()):
             p.add_(torch.randn_like(p) * 0.05)
-    B, mb = 4096, 512
+    B = 4096
     g = torch.Generator(device="cuda").manual_seed(0)
     src = torch.zeros((B, 32), device="cuda")
     src[:, 0:18] = torch.randn((B, 18), device="cuda", generator=g)
