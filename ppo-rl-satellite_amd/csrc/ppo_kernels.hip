@@ -120,6 +120,21 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<0x140>(v);   // row_mirror
   return v;
 }
+// row16_sum of NV values stage by stage: NV independent DPP adds between
+// dependent ones, so no DPP read-after-write s_nop is needed (value-major
+// order left ~90 of them in phase C); every value's ops and order are the
+// same as row16_sum's, so the sums are bitwise identical
+template <int NV>
+__device__ __forceinline__ void row16_sum_n(float (&v)[NV]) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] += dpp_f<0xB1>(v[q]);
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] += dpp_f<0x4E>(v[q]);
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] += dpp_f<0x141>(v[q]);
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] += dpp_f<0x140>(v[q]);
+}
 
 // tanh of the MLP activations (fc1, fc2, mean layer).  The split of Cephes
 // tanhf: |x| < 0.625 an odd minimax polynomial, else 1 - 2/(e^{2|x|} + 1) on
@@ -250,6 +265,34 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   }
 }
 
+// rows r < nvalid of a 32-/16-row block's accumulator-layout values v[rt][t][j]
+// (row 16rt + 4lg + j, column n0 + 16t + li) to out[r * ld + column]: a
+// uniform branch keeps a full block's stores straight-line (a per-lane test
+// made every store its own exec-masked branch)
+template <int R, int CT>
+__device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int n0, int nvalid,
+                                           const float (&v)[R / 16][CT][4]) {
+  const int l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  if (nvalid >= R) {
+#pragma unroll
+    for (int rt = 0; rt < R / 16; ++rt)
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[(int64_t)(16 * rt + 4 * lg + j) * ld + n0 + 16 * t + li] = v[rt][t][j];
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < R / 16; ++rt)
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * rt + 4 * lg + j;
+          if (r < nvalid) out[(int64_t)r * ld + n0 + 16 * t + li] = v[rt][t][j];
+        }
+  }
+}
+
 // Shared-memory block and forward pass (phases A, B and the output-layer dot
 // products of C) common to rowpass_kernel and policy_kernel, so the rollout's
 // policy/value forward and the update's forward are the same instructions in
@@ -337,10 +380,10 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         const float h = tanh_f32(acc[rt][t][j]);                   // fc1 + tanh
         h1[rt][t][j] = h;
         sm.h1s[r][n] = h;
-        if (h1out != nullptr && r < nvalid) h1out[(int64_t)r * H + n] = h;
       }
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
+  if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
   PHASE_PROBE(11);
   __syncthreads();
   PHASE_PROBE(1);
@@ -369,16 +412,33 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 #pragma unroll
         for (int q = 0; q < 3; ++q) p[q][rt][j] = fmaf(h, w3[t][q], p[q][rt][j]);
       }
+  // the DPP row sums; NQ is uniform per workgroup (3 actor, 1 critic)
+  float ps[3 * RT * 4];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    if (q >= NQ) break;                                            // uniform per workgroup
+  for (int q = 0; q < 3; ++q)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float v = row16_sum(p[q][rt][j]);
-        if (li == 0) sm.osum[w][16 * rt + 4 * lg + j][q] = v;
-      }
+      for (int j = 0; j < 4; ++j) ps[(q * RT + rt) * 4 + j] = p[q][rt][j];
+  if (NQ == 3) {
+    row16_sum_n<3 * RT * 4>(ps);
+  } else {
+    float p0[RT * 4];
+#pragma unroll
+    for (int k = 0; k < RT * 4; ++k) p0[k] = ps[k];
+    row16_sum_n<RT * 4>(p0);
+#pragma unroll
+    for (int k = 0; k < RT * 4; ++k) ps[k] = p0[k];
+  }
+  if (li == 0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (q >= NQ) break;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm.osum[w][16 * rt + 4 * lg + j][q] = ps[(q * RT + rt) * 4 + j];
+    }
   }
   __syncthreads();
   PHASE_PROBE(3);
@@ -476,13 +536,18 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
 #pragma unroll
     for (int q = 0; q < 4; ++q) dz3s[r][q] = dz[q];
     // the block's b3a / log_std / b3c partials: sums over its R rows, reduced
-    // across these R lanes of wave 0 by a fixed xor tree (deterministic)
+    // across these R lanes of wave 0 in a fixed order: DPP sums of each
+    // 16-lane row, then row 0 + row 1 (readlane), no LDS round trips
+    static_assert(R == 16 || R == 32, "row sums cover one or two DPP rows");
     float* tp = ptail + (int64_t)rb * L.tail;
     float red[7] = {dz[0], dz[1], dz[2], dls[0], dls[1], dls[2], dz[3]};
+    row16_sum_n<7>(red);
+    if (R == 32) {
 #pragma unroll
-    for (int off = 1; off < R; off <<= 1)
-#pragma unroll
-      for (int q = 0; q < 7; ++q) red[q] += __shfl_xor(red[q], off, 64);
+      for (int q = 0; q < 7; ++q)
+        red[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(red[q]), 0)) +
+                 __int_as_float(__builtin_amdgcn_readlane(__float_as_int(red[q]), 16));
+    }
     if (r == 0) {
       if (net == 0) {
 #pragma unroll
@@ -501,6 +566,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
   __syncthreads();
   PHASE_PROBE(4);
   float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
+  float d2v[RT][CT][4];
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const int n = n0 + 16 * t + li;
@@ -516,7 +582,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
         else dh = dz3s[r][3] * w3[t][0];
         const float d2 = dh * (1.0f - h * h);                       // tanh backward
         dzs[r][n] = d2;
-        if (r0 + r < mb) dZ2g[((int64_t)net * mb + r0 + r) * H + n] = d2;
+        d2v[rt][t][j] = d2;
         cb2 += d2;
         if (net == 0) {
           cw[0] = fmaf(dz3s[r][0], h, cw[0]); cw[1] = fmaf(dz3s[r][1], h, cw[1]); cw[2] = fmaf(dz3s[r][2], h, cw[2]);
@@ -533,6 +599,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
       else tp[5 * H + 8 + n] = cw[0];                              // dW3c
     }
   }
+  store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   __syncthreads();
   PHASE_PROBE(5);
 
