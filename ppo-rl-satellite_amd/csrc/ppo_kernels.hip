@@ -13,6 +13,7 @@
 
 #include <cmath>
 #include <string>
+#include <type_traits>
 
 #include "philox_device.h"
 #include "satrl_ppo.h"
@@ -479,6 +480,11 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
 #pragma unroll
   for (int d = 0; d < 3; ++d) { hb3[d] = P[L.b3a + d]; hls[d] = P[L.ls + d]; }
   const float hb3c = P[L.b3c];
+  // the actor head's per-dimension constants (var = exp(log_std)^2, log std,
+  // 1/var), off the head's dependency chain: lanes 0-2 compute them into LDS
+  // right after issuing their row gather (the barriers of the forward pass
+  // publish them)
+  __shared__ float hcs[3][3];
 
   f4 acc[RT][CT];
   float h1[RT][CT][4];
@@ -488,6 +494,13 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
       const int r = q / 26, c = q % 26, row = r0 + r;
       const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
       if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
+    }
+    if (t0 < 3) {
+      const float ls = t0 == 0 ? hls[0] : (t0 == 1 ? hls[1] : hls[2]);
+      const float sd = expf(ls), var = sd * sd;
+      hcs[0][t0] = var;
+      hcs[1][t0] = logf(sd);
+      hcs[2][t0] = 1.0f / var;
     }
   };
   mlp_forward<H, NW, kRows, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
@@ -504,10 +517,10 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
         for (int d = 0; d < 3; ++d) {
           th[d] = tanh_f32(out_sum<NW, kRows>(sm.osum, r, d) + hb3[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
-          const float sd = expf(hls[d]);
-          var[d] = sd * sd;
+          var[d] = hcs[0][d];
           dv[d] = ax[r][d] - mu[d];
-          logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - logf(sd)) - kLogSqrt2Pi;
+          // (the forward expression of gaussian_act, bit for bit: logp_old)
+          logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - hcs[1][d]) - kLogSqrt2Pi;
         }
         const float lsum = (logp[0] + logp[1]) + logp[2];
         const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
@@ -524,9 +537,10 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
         const float dlsum = dratio * ratio;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          const float dmu = dlsum * (dv[d] / var[d]);
+          const float dvv = dv[d] * hcs[2][d];                     // (x - mu) / var
+          const float dmu = dlsum * dvv;
           dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
-          dls[d] = dlsum * (dv[d] * dv[d] / var[d] - 1.0f) - ent_coef * inv;
+          dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
         const float vc = out_sum<NW, kRows>(sm.osum, r, 0) + hb3c;
@@ -567,38 +581,48 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
   PHASE_PROBE(4);
   float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
   float d2v[RT][CT][4];
+  // unswitched on the (workgroup-uniform) net: no per-element branches, and
+  // the critic skips the actor's three output columns
+  auto tail = [&](auto actor) {
+    constexpr bool ACT = decltype(actor)::value;
+    constexpr int NC = ACT ? 3 : 1;
 #pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int n = n0 + 16 * t + li;
-    float cb2 = 0.f, cw[3] = {0.f, 0.f, 0.f};
+    for (int t = 0; t < CT; ++t) {
+      const int n = n0 + 16 * t + li;
+      float cb2 = 0.f, cw[NC];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+      for (int q = 0; q < NC; ++q) cw[q] = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 16 * rt + 4 * lg + j;
-        const float h = acc[rt][t][j];
-        float dh;
-        if (net == 0) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
-        else dh = dz3s[r][3] * w3[t][0];
-        const float d2 = dh * (1.0f - h * h);                       // tanh backward
-        dzs[r][n] = d2;
-        d2v[rt][t][j] = d2;
-        cb2 += d2;
-        if (net == 0) {
-          cw[0] = fmaf(dz3s[r][0], h, cw[0]); cw[1] = fmaf(dz3s[r][1], h, cw[1]); cw[2] = fmaf(dz3s[r][2], h, cw[2]);
-        } else {
-          cw[0] = fmaf(dz3s[r][3], h, cw[0]);
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * rt + 4 * lg + j;
+          const float h = acc[rt][t][j];
+          float dh;
+          if constexpr (ACT) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
+          else dh = dz3s[r][3] * w3[t][0];
+          const float d2 = dh * (1.0f - h * h);                     // tanh backward
+          dzs[r][n] = d2;
+          d2v[rt][t][j] = d2;
+          cb2 += d2;
+          if constexpr (ACT) {
+            cw[0] = fmaf(dz3s[r][0], h, cw[0]); cw[1] = fmaf(dz3s[r][1], h, cw[1]); cw[2] = fmaf(dz3s[r][2], h, cw[2]);
+          } else {
+            cw[0] = fmaf(dz3s[r][3], h, cw[0]);
+          }
         }
-      }
-    cb2 += __shfl_xor(cb2, 16, 64); cb2 += __shfl_xor(cb2, 32, 64);
+      cb2 += __shfl_xor(cb2, 16, 64); cb2 += __shfl_xor(cb2, 32, 64);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) { cw[q] += __shfl_xor(cw[q], 16, 64); cw[q] += __shfl_xor(cw[q], 32, 64); }
-    if (lg == 0) {
-      tp[net * H + n] = cb2;                                       // db2
-      if (net == 0) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
-      else tp[5 * H + 8 + n] = cw[0];                              // dW3c
+      for (int q = 0; q < NC; ++q) { cw[q] += __shfl_xor(cw[q], 16, 64); cw[q] += __shfl_xor(cw[q], 32, 64); }
+      if (lg == 0) {
+        tp[net * H + n] = cb2;                                     // db2
+        if constexpr (ACT) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
+        else tp[5 * H + 8 + n] = cw[0];                            // dW3c
+      }
     }
-  }
+  };
+  if (net == 0) tail(std::true_type{});
+  else tail(std::false_type{});
   store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   __syncthreads();
   PHASE_PROBE(5);
