@@ -225,6 +225,9 @@ __device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4
 // us).  It costs 16 VGPRs, which the policy kernel's occupancy does not
 // afford (59 -> 63 us per rollout step), so there it is off; the MFMA
 // sequence, hence every result bit, is the same either way.
+#ifndef SATRL_RP_BPD
+#define SATRL_RP_BPD 2
+#endif
 template <int K, int LDA, int LDB, int RT, int CT, bool APRE>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
                                           f4 (&acc)[RT][CT]) {
@@ -234,6 +237,24 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   const float* ap = A + i * LDA + 8 * g;
   const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
   float4 x[CT][2], y[CT][2];
+#if SATRL_RP_BPD > 1
+  if constexpr (APRE) {
+    // W2 chunks BPD ahead (BPD + 1 register buffers), LDS A one ahead; fully
+    // unrolled so every buffer index is static
+    constexpr int NB = SATRL_RP_BPD + 1;
+    float4 bb[NB][CT][2], aa[2][RT][2];
+#pragma unroll
+    for (int c = 0; c < SATRL_RP_BPD && c < NC; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
+    a_chunk<LDA, RT>(ap, aa[0]);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (c + SATRL_RP_BPD < NC) b_chunk<CT>(bp + 32 * (c + SATRL_RP_BPD), LDB, bb[(c + SATRL_RP_BPD) % NB]);
+      if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
+      mfma_regs<RT, CT>(aa[c % 2], bb[c % NB], acc);
+    }
+    return;
+  }
+#endif
   if constexpr (APRE) {
     float4 ax[RT][2], ay[RT][2];
     b_chunk<CT>(bp, LDB, x);
