@@ -217,62 +217,73 @@ __device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4
 }
 
 // acc[rt][t] += A[16rt.. +16][K] (LDS, row stride LDA) x B^T with B[n][k]
-// row-major (ld LDB) for columns n0 + 16t, in 32-wide k chunks.  Chunk pairs
-// with two register buffers in a rolled loop (prefetch distance one chunk);
-// loads unconditional and the last pair peeled, so every vmcnt wait is exact.
-// APRE: the LDS A chunk is double-buffered the same way, so a chunk's MFMAs
-// do not start behind a fresh ds_read's latency (the rowpass: 34.7 -> 33.6
-// us).  It costs 16 VGPRs, which the policy kernel's occupancy does not
-// afford (59 -> 63 us per rollout step), so there it is off; the MFMA
-// sequence, hence every result bit, is the same either way.
+// row-major (ld LDB) for columns n0 + 16t, in 32-wide k chunks.  Without
+// APRE (the policy kernel): chunk pairs with two register buffers in a rolled
+// loop (prefetch distance one chunk), loads unconditional and the last pair
+// peeled, so every vmcnt wait is exact.  APRE (the rowpass): the LDS A chunk
+// is double-buffered too, so a chunk's MFMAs do not start behind a fresh
+// ds_read's latency (34.7 -> 33.6 us), and B runs kBPD chunks ahead.  Its
+// registers are what the policy kernel's occupancy does not afford (54 VGPRs
+// allow two 16-wave workgroups per CU; APRE: 59 -> 63 us per rollout step, B
+// two ahead alone: 64 us).  The MFMA sequence, hence every result bit, is the
+// same on every path.
 #ifndef SATRL_RP_BPD
 #define SATRL_RP_BPD 2
 #endif
-template <int K, int LDA, int LDB, int RT, int CT, bool APRE>
+#ifndef SATRL_RP_EARLYB
+#define SATRL_RP_EARLYB 0   // measured: no gain (30.6 vs 30.6 us; in-graph 55.5 vs 55.6)
+#endif
+#ifndef SATRL_RP_EARLYD
+#define SATRL_RP_EARLYD 1   // 30.4 -> 29.8 us, in-graph 55.6 -> 54.7
+#endif
+// APRE path: B chunks kBPD ahead (kBPD + 1 register buffers; distance 2
+// measured best: 30.7 us per rowpass against 32.5 at 1, 31.0 at 3, 31.7 at 4).
+// The first kBPD chunks can be issued early, before the phase's barrier, into
+// a WPre (mfma_rows_pre), and handed to mfma_rows<..., PRE = true>.
+constexpr int kBPD = SATRL_RP_BPD;
+template <int CT>
+struct WPre {
+  float4 bb[kBPD][CT][2];
+};
+template <int LDB, int CT>
+__device__ __forceinline__ void mfma_rows_pre(const float* __restrict__ B, int n0, WPre<CT>& pre) {
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
+#pragma unroll
+  for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, pre.bb[c]);
+}
+
+template <int K, int LDA, int LDB, int RT, int CT, bool APRE, bool PRE = false>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
-                                          f4 (&acc)[RT][CT]) {
+                                          f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr) {
   constexpr int NC = K / 32;
-  static_assert(NC % 2 == 0, "chunk pairs");
+  static_assert(NC % 2 == 0 && NC >= kBPD, "chunk pairs");
+  static_assert(APRE || !PRE, "early-issued chunks feed the APRE path");
   const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
   const float* ap = A + i * LDA + 8 * g;
   const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
-  float4 x[CT][2], y[CT][2];
-#if SATRL_RP_BPD > 1
   if constexpr (APRE) {
-    // W2 chunks BPD ahead (BPD + 1 register buffers), LDS A one ahead; fully
-    // unrolled so every buffer index is static
-    constexpr int NB = SATRL_RP_BPD + 1;
+    // fully unrolled so every buffer index is static
+    constexpr int NB = kBPD + 1;
     float4 bb[NB][CT][2], aa[2][RT][2];
+    if constexpr (PRE) {
 #pragma unroll
-    for (int c = 0; c < SATRL_RP_BPD && c < NC; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
+      for (int c = 0; c < kBPD; ++c)
+#pragma unroll
+        for (int t = 0; t < CT; ++t) { bb[c][t][0] = pre->bb[c][t][0]; bb[c][t][1] = pre->bb[c][t][1]; }
+    } else {
+#pragma unroll
+      for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
+    }
     a_chunk<LDA, RT>(ap, aa[0]);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (c + SATRL_RP_BPD < NC) b_chunk<CT>(bp + 32 * (c + SATRL_RP_BPD), LDB, bb[(c + SATRL_RP_BPD) % NB]);
+      if (c + kBPD < NC) b_chunk<CT>(bp + 32 * (c + kBPD), LDB, bb[(c + kBPD) % NB]);
       if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
       mfma_regs<RT, CT>(aa[c % 2], bb[c % NB], acc);
     }
-    return;
-  }
-#endif
-  if constexpr (APRE) {
-    float4 ax[RT][2], ay[RT][2];
-    b_chunk<CT>(bp, LDB, x);
-    a_chunk<LDA, RT>(ap, ax);
-#pragma unroll 1
-    for (int c = 0; c < NC - 2; c += 2) {
-      b_chunk<CT>(bp + 32 * (c + 1), LDB, y);
-      a_chunk<LDA, RT>(ap + 32 * (c + 1), ay);
-      mfma_regs<RT, CT>(ax, x, acc);
-      b_chunk<CT>(bp + 32 * (c + 2), LDB, x);
-      a_chunk<LDA, RT>(ap + 32 * (c + 2), ax);
-      mfma_regs<RT, CT>(ay, y, acc);
-    }
-    b_chunk<CT>(bp + 32 * (NC - 1), LDB, y);
-    a_chunk<LDA, RT>(ap + 32 * (NC - 1), ay);
-    mfma_regs<RT, CT>(ax, x, acc);
-    mfma_regs<RT, CT>(ay, y, acc);
   } else {
+    float4 x[CT][2], y[CT][2];
     b_chunk<CT>(bp, LDB, x);
 #pragma unroll 1
     for (int c = 0; c < NC - 2; c += 2) {
@@ -390,6 +401,11 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
   mfma_chunk<LDS_S, RT, CT>(&sm.S[li][8 * lg], bw1, acc);
+  // phase B's first W2 chunks go out now: their latency overlaps the fc1 tanh,
+  // the H1 stores and the barrier
+  constexpr bool EB = APRE && SATRL_RP_EARLYB;
+  WPre<CT> preB;
+  if constexpr (EB) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   PHASE_PROBE(10);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -411,7 +427,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  mfma_rows<H, LDA, H, RT, CT, APRE, EB>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -525,6 +541,9 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
     }
   };
   mlp_forward<H, NW, kRows, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  // phase D's first W2T chunks go out now, under the loss head and the tail
+  WPre<CT> preD;
+  if constexpr (SATRL_RP_EARLYD) mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -653,7 +672,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows<H, LDA, H, RT, CT, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc);
+  mfma_rows<H, LDA, H, RT, CT, true, SATRL_RP_EARLYD>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
