@@ -897,7 +897,17 @@ __device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, in
   __syncthreads();
   float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c == 0) {
-    for (int k = 0; k < CH; ++k) tot = f4add(tot, red[k * EB + e]);
+    // the CH partials in order; their LDS reads go out 8 at a time ahead of
+    // the adds (one read round trip per 8, not per 2)
+    constexpr int KB = CH < 8 ? CH : 8;
+#pragma unroll
+    for (int k0 = 0; k0 < CH; k0 += KB) {
+      float4 part[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) part[k] = red[(k0 + k) * EB + e];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) tot = f4add(tot, part[k]);
+    }
   }
   return tot;
 }
