@@ -913,12 +913,28 @@ __device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, in
 }
 
 // block-level f64 pair sum in fixed order, result in every thread
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_d(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+// wave sum of (a, c) in a fixed order: DPP sums of each 16-lane row (the
+// row16_sum stages), then rows 0..3 by readlane -- no ds_bpermute round trips
+__device__ __forceinline__ void wave_sum2(double& a, double& c) {
+  a += dpp_d<0xB1>(a); c += dpp_d<0xB1>(c);
+  a += dpp_d<0x4E>(a); c += dpp_d<0x4E>(c);
+  a += dpp_d<0x141>(a); c += dpp_d<0x141>(c);
+  a += dpp_d<0x140>(a); c += dpp_d<0x140>(c);
+  a = ((lane_d(a, 0) + lane_d(a, 16)) + lane_d(a, 32)) + lane_d(a, 48);
+  c = ((lane_d(c, 0) + lane_d(c, 16)) + lane_d(c, 32)) + lane_d(c, 48);
+}
 __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    a += __shfl_xor(a, off, 64);
-    c += __shfl_xor(c, off, 64);
-  }
+  wave_sum2(a, c);
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh[2 * w] = a; sh[2 * w + 1] = c; }
   __syncthreads();
@@ -1029,7 +1045,6 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
                                                    float* __restrict__ W2T, int net_sel) {
   const Layout L = layout(H);
   __shared__ double sh[8];
-  __shared__ float cst[2][3];                                      // coef, step_size, bc2_sqrt per net
   __shared__ float tile[32][33];
   const int t = threadIdx.x;
   const int ntc = H / 32, nbw = (net_sel < 0 ? 2 : 1) * ntc * ntc;
@@ -1082,19 +1097,21 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   for (int k = t; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
 #endif
   block_sum2(a, c, sh);
-  if (t < 2 && (net_sel < 0 || net_sel == t)) {
-    const double nn = t == 0 ? a : c;
+  // every thread folds the same partials in the same order, so each derives
+  // its own net's constants (no second barrier)
+  float coef, ss, b2s;
+  {
+    const double nn = net == 0 ? a : c;
     const float nrm = (float)sqrt(nn);
-    cst[t][0] = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
+    coef = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
     // bct[2*step] = 1 - beta1**step, bct[2*step+1] = sqrt(1 - beta2**step) (python float
     // math, as torch.optim.Adam computes them); constant 1.0 past the table
-    const int st = (int)steps[t];
+    const int st = (int)steps[net];
     const double bc1 = st < bct_len ? bct[2 * st] : 1.0;
     const double bc2s = st < bct_len ? bct[2 * st + 1] : 1.0;
-    cst[t][1] = (float)((double)lr[t] / bc1);
-    cst[t][2] = (float)bc2s;
+    ss = (float)((double)lr[net] / bc1);
+    b2s = (float)bc2s;
   }
-  __syncthreads();
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
   if (!live) return;                                               // (W1.. tail blocks only: no barrier follows)
@@ -1107,7 +1124,6 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   float4 m = M4[e4], v = V4[e4];
   const float4 p = P4[e4];
 #endif
-  const float coef = cst[net][0], ss = cst[net][1], b2s = cst[net][2];
   float4 pn;
   pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
