@@ -117,7 +117,12 @@ __device__ double select_kth(Smem& sm, int n, int k, double lx, double ly, doubl
     }
     __syncthreads();
   }
-  return from_okey(sm.sel_prefix);
+  // every thread reads the result before any thread can start the next call
+  // (whose thread 0 resets sel_prefix): without this barrier a late wave
+  // could read the reset prefix when the median takes two calls (even count)
+  const unsigned long long r = sm.sel_prefix;
+  __syncthreads();
+  return from_okey(r);
 }
 
 // searchsorted(linspace(-pi, pi, 100), a, side='right') = np.digitize(a, bins)
