@@ -121,6 +121,17 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<0x140>(v);   // row_mirror
   return v;
 }
+// v + v[lane ^ 16] and v + v[lane ^ 32] by the gfx950 permlane swaps (VALU,
+// no ds_bpermute round trip); fp addition commutes, so every lane's bits are
+// those of v + __shfl_xor(v, 16 / 32)
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 // row16_sum of NV values stage by stage: NV independent DPP adds between
 // dependent ones, so no DPP read-after-write s_nop is needed (value-major
 // order left ~90 of them in phase C); every value's ops and order are the
@@ -651,9 +662,9 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
             cw[0] = fmaf(dz3s[r][3], h, cw[0]);
           }
         }
-      cb2 += __shfl_xor(cb2, 16, 64); cb2 += __shfl_xor(cb2, 32, 64);
+      cb2 = xor32_sum(xor16_sum(cb2));
 #pragma unroll
-      for (int q = 0; q < NC; ++q) { cw[q] += __shfl_xor(cw[q], 16, 64); cw[q] += __shfl_xor(cw[q], 32, 64); }
+      for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
       if (lg == 0) {
         tp[net * H + n] = cb2;                                     // db2
         if constexpr (ACT) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
