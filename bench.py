@@ -224,6 +224,17 @@ def main():
     rowpass_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
     rowpass_flop = st.rowpass_flops(a.hidden, a.minibatch)
     rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
+    # the same kernel's average inside the update's graphs (after each step's
+    # Adam rewrote W2/W2T, so the weights come from MALL, not a warm L2), from
+    # the committed rocprofv3 kernel stats of this command
+    in_update_us = None
+    ks_file = os.path.join(ROOT, "profiles", "r1_bench_kernel_stats.csv")
+    if os.path.exists(ks_file):
+        import csv
+        with open(ks_file) as f:
+            for r in csv.DictReader(f):
+                if "rowpass_kernel<%d" % a.hidden in r["name"].replace(" ", ""):
+                    in_update_us = float(r["avg_ns"]) / 1e3
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", "r1_rowpass_pmc.json")
     if os.path.exists(pmc_file):
@@ -403,6 +414,11 @@ def main():
                          "achieved": rowpass_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": rowpass_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
                          "avg_launch_us": rowpass_us, "flop_per_launch": rowpass_flop,
+                         "in_update_avg_launch_us": in_update_us,
+                         "in_update_frac": (rowpass_flop / (in_update_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS
+                                            if in_update_us else None),
+                         "in_update_source": "profiles/r1_bench_kernel_stats.csv (rocprofv3 average over all "
+                                             "rowpass launches of this command, nearly all inside the update)",
                          "traffic_source": "profiles/r1_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)",
                          "note": "f32 MFMA; one net per workgroup of 32 rows, each streams that net's fc2 weights "
                                  "from L2 per phase (DESIGN.md 3.4)"},

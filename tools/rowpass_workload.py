@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Workload for the PMC passes of tools/profile_round.sh: satrl_ppo_rowpass
 launched back to back at the bench configuration (hidden 256, minibatch
-4096 rows gathered by a random permutation from a packed buffer of
-16384 x 2048 transitions, as in one PPO epoch of bench.py)."""
+4096 rows drawn by a random permutation from a packed buffer of
+16384 x 2048 transitions and staged contiguously first, as the update's
+graphs do with satrl_ppo_stage; the staging copy is not a rowpass launch).
+rocprofv3 --pmc counts every dispatch; summarize_profiles.py keeps the
+rowpass ones."""
 import os
 import sys
 
@@ -26,7 +29,8 @@ def main():
     perm = torch.randperm(rows, device="cuda", generator=g)
     st = L.stepper(mb)
     for k in range(iters):
-        st.rowpass(src, perm[k * mb:(k + 1) * mb])
+        rows_k = src.index_select(0, perm[k * mb:(k + 1) * mb])
+        st.rowpass(rows_k, None)
     torch.cuda.synchronize()
     print("ok")
 
