@@ -881,7 +881,13 @@ int dw2_splits(int H, int mb, int net) {
 // latency rounds), then chunk 0 adds the CH partials in order.
 // ---------------------------------------------------------------------------
 struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
-constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;
+#ifndef SATRL_RED_CH1
+#define SATRL_RED_CH1 8
+#endif
+#ifndef SATRL_RED_CHT
+#define SATRL_RED_CHT 32
+#endif
+constexpr int kRedCH1 = SATRL_RED_CH1, kRedCHt = SATRL_RED_CHT, kRedCH2 = 4;
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
