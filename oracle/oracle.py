@@ -66,6 +66,9 @@ def lib():
         L.orc_orbital_elements.restype = C.c_int
         L.orc_solve_alpha.argtypes = [C.c_double] * 7 + [ip]
         L.orc_solve_alpha.restype = C.c_double
+        L.orc_set_jitter.argtypes = [C.c_ulonglong]
+        L.orc_step_planes.argtypes = [C.POINTER(OrcParams), C.c_int64, dp, ip, fp, fp, ip, dp, ip, C.c_int32]
+        L.orc_step_planes.restype = C.c_int
         L.orc_rollout.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcEnv), C.c_int64, C.c_int32,
                                   fp, fp, ip, dp, ip, C.c_int32]
         L.orc_rollout.restype = C.c_int
@@ -166,6 +169,51 @@ def danger_zone(Rc, Vc, Rt, Vt, fuel, fuel_mode):
     cnt = C.c_int32(0)
     rc = lib().orc_danger_zone(*[_dp(a) for a in arrs], float(fuel), int(fuel_mode), C.byref(cnt))
     return rc, cnt.value
+
+
+def set_jitter(seed):
+    """libm-tie probe: seed != 0 moves transcendental results of the
+    restatement by an ulp or two (satenv_oracle.c orc_jit); 0 = exact."""
+    lib().orc_set_jitter(int(seed))
+
+
+def dz_libm_tie(Rc, Vc, Rt, Vt, fuel, fuel_mode, target, seeds=2048):
+    """Is danger-zone count `target` one ulp of libm away?  Returns the first
+    jitter seed under which the restatement's count equals `target`, or 0
+    if none of `seeds` seeds does (a count no ulp-level libm difference can
+    explain)."""
+    try:
+        for s in range(1, int(seeds) + 1):
+            set_jitter(s)
+            rc, c = danger_zone(Rc, Vc, Rt, Vt, fuel, fuel_mode)
+            if rc == 0 and c == int(target):
+                return s
+        return 0
+    finally:
+        set_jitter(0)
+
+
+def step_planes(f64, i32, pa, ea, episode_count, d_capture=15000.0, max_episode_steps=1000, nthreads=8,
+                propagator=0, rk4_substeps=10):
+    """One step of n envs from SoA state planes (satenv_get_state layout:
+    f64 [15][n], i32 [3][n]), no autoreset.  Returns (post f64, post i32,
+    reward f64 [n], done i32 [n])."""
+    p = params(d_capture, max_episode_steps, propagator=propagator, rk4_substeps=rk4_substeps)
+    f = np.array(f64, dtype=np.float64, copy=True, order="C")
+    i = np.array(i32, dtype=np.int32, copy=True, order="C")
+    n = f.shape[1]
+    pa = np.ascontiguousarray(pa, dtype=np.float32)
+    ea = np.ascontiguousarray(ea, dtype=np.float32)
+    cnt = np.ascontiguousarray(episode_count, dtype=np.int32)
+    rew = np.zeros(n)
+    done = np.zeros(n, dtype=np.int32)
+    ip = C.POINTER(C.c_int32)
+    rc = lib().orc_step_planes(C.byref(p), n, _dp(f), i.ctypes.data_as(ip), pa.ctypes.data_as(C.POINTER(C.c_float)),
+                               ea.ctypes.data_as(C.POINTER(C.c_float)), cnt.ctypes.data_as(ip), _dp(rew),
+                               done.ctypes.data_as(ip), int(nthreads))
+    if rc != 0:
+        raise RuntimeError("oracle step error")
+    return f, i, rew, done
 
 
 class OracleEnv:

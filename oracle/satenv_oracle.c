@@ -29,6 +29,42 @@
 #include <omp.h>
 #endif
 
+/* ---- libm-tie probe (tests only) -------------------------------------
+ * With a non-zero jitter seed transcendental results below are moved by one
+ * ulp (two for seeds >= 1024) up or down; a hash of seed and call index picks
+ * which calls move and the direction,
+ * so a test can show that a danger-zone count on which the GPU (OCML) and
+ * this restatement (glibc) disagree is decided at the ulp level: some seed
+ * makes the oracle produce the GPU's count.  Seed 0 (the default) is exact
+ * glibc.  Thread-local: OpenMP rollouts are unaffected.                 */
+static _Thread_local unsigned long long orc_jit_seed = 0, orc_jit_ctr = 0;
+void orc_set_jitter(unsigned long long seed) { orc_jit_seed = seed; orc_jit_ctr = 0; }
+static double orc_jit(double v) {
+    if (!orc_jit_seed || !isfinite(v)) return v;
+    unsigned long long z = orc_jit_seed * 0x9E3779B97F4A7C15ull + (++orc_jit_ctr) * 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 31; z *= 0x94D049BB133111EBull; z ^= z >> 29;
+    /* seed % 3 sets how many calls move: 1/2, 1/8 or 1/32 of them (one
+     * sensitive call may need to move while the others stay); seeds >= 1024
+     * move by two ulps */
+    const unsigned mask = (orc_jit_seed % 3 == 0) ? 1u : ((orc_jit_seed % 3 == 1) ? 7u : 31u);
+    if (((unsigned)(z >> 8) & mask) != 0) return v;
+    const int ulps = orc_jit_seed >= 1024 ? 2 : 1;
+    for (int u = 0; u < ulps; ++u) v = nextafter(v, (z & 1) ? INFINITY : -INFINITY);
+    return v;
+}
+static double j_sin(double x) { return orc_jit(sin(x)); }
+static double j_cos(double x) { return orc_jit(cos(x)); }
+static double j_tan(double x) { return orc_jit(tan(x)); }
+static double j_acos(double x) { return orc_jit(acos(x)); }
+static double j_atan(double x) { return orc_jit(atan(x)); }
+static double j_pow(double x, double y) { return orc_jit(pow(x, y)); }
+#define sin j_sin
+#define cos j_cos
+#define tan j_tan
+#define acos j_acos
+#define atan j_atan
+#define pow j_pow
+
 static const double ORC_PI = 3.141592653589793;      /* np.pi */
 static const double ORC_2PI = 6.283185307179586;     /* 2 * np.pi */
 
@@ -677,6 +713,44 @@ int orc_rollout(const orc_params* p, orc_env* envs, int64_t n, int32_t steps, co
             reward_out[k] = r; done_out[k] = d;
             if (d) { orc_reset(&envs[i], envs[i].flag, obs); episode_count[i] = 0; }
         }
+    }
+    return err ? -1 : 0;
+}
+
+/* one step-locked step of n envs given as SoA planes (the product's
+ * satenv_get_state layout: f64 [15][n] Pp Pv Ep Ev fuel_c fuel_t dis,
+ * i32 [3][n] dz count bits with bits = fc_mode | ft_mode<<2 | vel_int<<4 |
+ * flag<<5), episode_count[i] given; writes reward, done and the post-step
+ * planes back in place (no autoreset).  Tests use it to compare every step
+ * of a GPU rollout against the restatement started from the GPU's own state. */
+int orc_step_planes(const orc_params* p, int64_t n, double* f64, int32_t* i32, const float* pa, const float* ea,
+                    const int32_t* episode_count, double* reward_out, int32_t* done_out, int32_t nthreads) {
+    int err = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static) reduction(| : err)
+#endif
+    for (int64_t i = 0; i < n; ++i) {
+        orc_env e;
+        for (int k = 0; k < 3; ++k) {
+            e.Pp[k] = f64[k * n + i]; e.Pv[k] = f64[(3 + k) * n + i];
+            e.Ep[k] = f64[(6 + k) * n + i]; e.Ev[k] = f64[(9 + k) * n + i];
+        }
+        e.fuel_c = f64[12 * n + i]; e.fuel_t = f64[13 * n + i]; e.dis = f64[14 * n + i];
+        const int32_t b = i32[2 * n + i];
+        e.dz = i32[i];
+        e.fuel_c_mode = b & 3; e.fuel_t_mode = (b >> 2) & 3; e.vel_int = (b >> 4) & 1; e.flag = (b >> 5) & 1;
+        double obs[18], r;
+        int32_t d;
+        err |= (orc_step(p, &e, pa + 3 * i, ea + 3 * i, episode_count[i], obs, &r, &d) != 0);
+        reward_out[i] = r; done_out[i] = d;
+        for (int k = 0; k < 3; ++k) {
+            f64[k * n + i] = e.Pp[k]; f64[(3 + k) * n + i] = e.Pv[k];
+            f64[(6 + k) * n + i] = e.Ep[k]; f64[(9 + k) * n + i] = e.Ev[k];
+        }
+        f64[12 * n + i] = e.fuel_c; f64[13 * n + i] = e.fuel_t; f64[14 * n + i] = e.dis;
+        i32[i] = e.dz; i32[n + i] = episode_count[i];
+        i32[2 * n + i] = (e.fuel_c_mode & 3) | ((e.fuel_t_mode & 3) << 2) | ((e.vel_int & 1) << 4) | ((e.flag & 1) << 5);
     }
     return err ? -1 : 0;
 }

@@ -80,6 +80,16 @@ typedef struct {
 /* fills n1*(n2+1)*(n3+1) directions; returns the number with status 1 */
 int64_t orc_reachable_domain(const orc_rd_params* p, double* rf_max, double* rf_min, uint8_t* status);
 
+/* libm-tie probe: non-zero seed = transcendental results moved by one
+ * (seed >= 1024: two) ulp, which calls and which way from a hash of seed
+ * and call index; 0 = exact glibc (default)                              */
+void orc_set_jitter(unsigned long long seed);
+
+/* one step of n envs held as SoA planes (satenv_get_state layout), in place */
+int  orc_step_planes(const orc_params* p, int64_t n, double* f64, int32_t* i32, const float* pa,
+                     const float* ea, const int32_t* episode_count, double* reward_out, int32_t* done_out,
+                     int32_t nthreads);
+
 /* batched replay for the CPU baseline: n envs x steps, actions [steps][n][3] */
 int  orc_rollout(const orc_params* p, orc_env* envs, int64_t n, int32_t steps,
                  const float* pa, const float* ea, int32_t* episode_count,

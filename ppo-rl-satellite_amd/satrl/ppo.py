@@ -214,7 +214,10 @@ class FusedMinibatch:
         self.dZ2 = torch.empty(2 * self.mb * H, **f32)
         self.ptail = torch.empty(self.nwg * (6 * H + 12), **f32)
         self.pw1 = torch.empty(self.nwg * 2 * H * 20, **f32)
-        self.p2 = torch.empty(2 * self.S * H * H, **f32)
+        # sized for the largest split count any minibatch size can produce
+        # (dw2_splits caps S at 256 / tiles), so a ragged tail minibatch whose
+        # S exceeds the full minibatch's never writes past the slabs
+        self.p2 = torch.empty(2 * self.max_splits(H) * H * H, **f32)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
@@ -253,6 +256,12 @@ class FusedMinibatch:
         per_row = 2 * (2 * (2 * 18 * H + H) + 2 * (2 * H * H)) + 2 * 3 * 3 * H + 2 * 1 * 3 * H
         return per_row * mb
 
+    def max_splits(self, H):
+        """Upper bound of splits(H, mb) over every mb (the p2 capacity)."""
+        if self.lib_gemm:
+            return max(self.S, 4)
+        return max(self.S, 256 // (2 * (H // 64) ** 2))
+
     def splits(self, H, mb):
         """split-K ways of the dW2 product for a minibatch of mb rows."""
         if self.lib_gemm:
@@ -282,6 +291,8 @@ class FusedMinibatch:
         L = self.L
         H = L.H
         S = self.S if mb == self.mb else self.splits(H, mb)
+        if S > self.max_splits(H):
+            raise _lib.NativeError(f"dW2 split count {S} exceeds the slab capacity {self.max_splits(H)}")
         lib, sp = _lib.lib(), stream_ptr()
         nsq = self.nsq[max(net, 0)]
         H1, dZ2 = self.rowpass(src, idx, mb, net)
@@ -485,9 +496,15 @@ class PPOLearner:
 
     # -- lr ---------------------------------------------------------------------
     def lr_decay(self, total_steps):
-        """ppo_continuous.py:244-250."""
-        lr_a_now = self.lr_a * (1 - total_steps / self.max_train_steps)
-        lr_c_now = self.lr_c * (1 - total_steps / self.max_train_steps)
+        """ppo_continuous.py:244-250.  The reference's total_steps is an
+        episode index below max_train_steps (its loop stops there,
+        CPPO_main.py:110); the vectorised engine counts finished episodes over
+        all envs and ranks, which can pass the budget inside an iteration, so
+        the progress fraction is clamped to [0, 1] and lr never goes negative
+        (identical to the reference wherever the reference runs)."""
+        frac = min(max(float(total_steps) / self.max_train_steps, 0.0), 1.0)
+        lr_a_now = self.lr_a * (1 - frac)
+        lr_c_now = self.lr_c * (1 - frac)
         self.lr.copy_(torch.tensor([lr_a_now, lr_c_now], dtype=torch.float32))
 
     @property

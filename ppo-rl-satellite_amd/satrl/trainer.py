@@ -329,6 +329,21 @@ class VecTrainer:
         self.iteration_count += 1
         return st.cpu().numpy()
 
+    @property
+    def budget_reached(self):
+        """True once the finished episodes (all envs, all ranks) reach
+        max_train_steps: the reference's loop ends there (CPPO_main.py:110,
+        `for epsiode in range(max_train_steps)`), and lr_decay is at 0."""
+        return self.episodes >= self.args.max_train_steps
+
+    def train(self, max_iterations=None, timers=None):
+        """Iterations until the episode budget (or max_iterations) is reached;
+        returns the per-iteration statistics."""
+        out = []
+        while not self.budget_reached and (max_iterations is None or len(out) < max_iterations):
+            out.append(self.iteration(timers))
+        return out
+
     def iteration(self, timers=None):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         ev[0].record()

@@ -36,3 +36,33 @@ def oracle():
 
 TRAJ_NAMES = ["traj_uniform_f0", "traj_wide_f0", "traj_chase_f0", "traj_uniform_f1", "traj_chase_f1"]
 STATE_KEYS = ["Pp", "Pv", "Ep", "Ev", "fuel_c", "fuel_t", "dis", "dz", "fuel_c_mode", "fuel_t_mode", "vel_int", "flag"]
+
+
+R_CW = np.array([27098000.0, 32306000.0, 0.0])       # environment.py:338
+V_CW = np.array([-2350.0, 1970.0, 0.0])              # environment.py:339
+
+
+def assert_dz_libm_ties(oracle, Pp, Pv, Ep, Ev, fuel, fuel_mode, got, ref, what, seeds=2048, absolute=False):
+    """Every case where the GPU's danger-zone count `got` differs from the
+    glibc restatement's `ref` must be a libm tie: some ulp-jitter seed of the
+    oracle (oracle.dz_libm_tie) reproduces the GPU's count from the same
+    relative state (absolute = the CW reference point + relative, as
+    environment.py:334-343 builds it; `absolute`: the states are absolute
+    already).  Returns the mismatching indices."""
+    bad = np.nonzero(np.asarray(got) != np.asarray(ref))[0]
+    lines = []
+    R0, V0 = (np.zeros(3), np.zeros(3)) if absolute else (R_CW, V_CW)
+    for i in bad:
+        seed = oracle.dz_libm_tie(R0 + Pp[i], V0 + Pv[i], R0 + Ep[i], V0 + Ev[i], float(fuel[i]),
+                                  int(fuel_mode[i]), int(got[i]), seeds=seeds)
+        lines.append(f"  case {i}: gpu {int(got[i])} glibc {int(ref[i])} -> jitter seed {seed}")
+        if seed == 0:               # keep the state for offline analysis (gpurun_out/ comes back from the box)
+            os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+            np.savez(os.path.join(ROOT, "gpurun_out", "dz_nontie_%s_%d.npz" % (what.replace(" ", "_"), i)),
+                     Rc=R0 + Pp[i], Vc=V0 + Pv[i], Rt=R0 + Ep[i], Vt=V0 + Ev[i], fuel=float(fuel[i]),
+                     mode=int(fuel_mode[i]), got=int(got[i]), ref=int(ref[i]))
+        assert seed != 0, f"{what}: case {i} (gpu {got[i]}, glibc {ref[i]}) is not a libm tie"
+    if len(bad):
+        print(f"{what}: {len(bad)} danger-zone count(s) differ from glibc, all libm ties" +
+              "".join("\n" + l for l in lines))
+    return bad

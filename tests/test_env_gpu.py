@@ -1,16 +1,19 @@
 """GPU parity of the env kernel (C-ABI libsatrl.so) against the golden
 vectors and the CPU oracle.  Tolerances (DESIGN.md "Parity"):
-  * kinematics / obs: bit-exact (no transcendental on that path)
-  * reward: |diff| <= 1e-12 * max(1,|r|) where the danger-zone count agrees
-  * danger-zone count: exact except libm-sensitive ties (OCML vs glibc),
-    bounded to <= 0.5 % of cases
+  * kinematics / obs / done: bit-exact (no transcendental on that path)
+  * reward: |diff| <= 1e-12 * max(1,|r|) where the danger-zone count agrees;
+    where it does not, the difference is exactly the count's reward term
+  * danger-zone count: exact, except libm ties (OCML vs glibc): every
+    mismatch is listed and must be reproduced by the oracle under a one-ulp
+    jitter of its transcendentals (conftest.assert_dz_libm_ties), and the
+    number of mismatches is capped at what was measured
   * fsolve root: |diff| <= 1e-9 * max(1, |x|) (converged root; OCML sin/cos)
 """
 import numpy as np
 import pytest
 import torch
 
-from conftest import STATE_KEYS, TRAJ_NAMES, golden
+from conftest import R_CW, STATE_KEYS, TRAJ_NAMES, V_CW, assert_dz_libm_ties, golden
 
 pytestmark = pytest.mark.gpu
 
@@ -77,7 +80,7 @@ def test_straight_line_sincos_is_the_library_sincos(satrl_env):
     assert np.array_equal(s0, s1) and np.array_equal(c0, c1)
 
 
-def test_danger_zone_counts(satrl_env):
+def test_danger_zone_counts(satrl_env, oracle):
     from satrl import _lib
     d = golden("dz_cases")
     n = len(d["X"])
@@ -88,15 +91,29 @@ def test_danger_zone_counts(satrl_env):
     _lib.check(_lib.lib().satenv_danger_zone(n, _lib.ptr(X), _lib.ptr(fuel), _lib.ptr(mode), _lib.ptr(out),
                                              _lib.stream_ptr()), "satenv_danger_zone")
     got = out.cpu().numpy()
-    mism_glibc = np.mean(got != d["count_glibc"])
-    mism_ref = np.mean(got != d["count"])
-    print(f"dz parity: mismatch vs glibc-ref {mism_glibc:.4%}, vs ref {mism_ref:.4%}")
     assert (got >= 0).all()
-    assert mism_glibc <= 0.005 and mism_ref <= 0.005
+    Xa = d["X"]                              # absolute states (x + 0.0 is exact)
+    bad = assert_dz_libm_ties(oracle, Xa[:, 0:3], Xa[:, 3:6], Xa[:, 6:9], Xa[:, 9:12], d["fuel"], d["mode"], got,
+                              d["count_glibc"], "dz_cases", absolute=True)
+    mism_ref = int(np.sum(got != d["count"]))
+    print(f"dz parity: {len(bad)} / {n} differ from the glibc reference, {mism_ref} from the SVML reference")
+    assert len(bad) <= 2, len(bad)          # measured: 1 (round 2)
+
+
+# libm-tie danger-zone counts measured per trajectory (round 2); a new
+# mismatch, even a tie, fails the test until it is looked at
+MAX_TRAJ_DZ_TIES = {"traj_uniform_f0": 0, "traj_wide_f0": 0, "traj_chase_f0": 1, "traj_uniform_f1": 0,
+                    "traj_chase_f1": 0}
+
+
+def _dz_term(dz):
+    """The danger-zone count's reward term (environment.py:165-168)."""
+    dz = np.asarray(dz)
+    return np.where(dz == 0, -1.0, dz * 0.5)
 
 
 @pytest.mark.parametrize("name", TRAJ_NAMES)
-def test_step_kernel_per_step(satrl_env, name):
+def test_step_kernel_per_step(satrl_env, oracle, name):
     """Every recorded step is one env of a single batched kernel launch."""
     E = satrl_env
     d = golden(name)
@@ -121,12 +138,17 @@ def test_step_kernel_per_step(satrl_env, name):
     assert np.array_equal(done, d["done"])
     assert np.array_equal(fa, fr), "state planes must be bit-exact"
     assert np.array_equal(ia[2], ir[2]), "fuel modes / vel_int / flag"
+    bad = assert_dz_libm_ties(oracle, d["a_Pp"], d["a_Pv"], d["a_Ep"], d["a_Ev"], d["a_fuel_c"],
+                              d["a_fuel_c_mode"], ia[0], d["a_dz_glibc"], name)
+    assert len(bad) <= MAX_TRAJ_DZ_TIES[name], (name, len(bad))
     dz_ok = ia[0] == d["a_dz_glibc"]
-    print(f"{name}: dz agree {dz_ok.mean():.4%}")
-    assert dz_ok.mean() >= 0.995
     rr = d["r_glibc"]
     rel = np.abs(r - rr) / np.maximum(1.0, np.abs(rr))
     assert (rel[dz_ok] <= 1e-12).all(), rel[dz_ok].max()
+    # where the count is a tie, the reward moves by exactly that term (environment.py:165-168, :251)
+    sign = np.where(d["a_flag"] == 0, 1.0, -1.0)
+    expect = rr + sign * (_dz_term(ia[0]) - _dz_term(d["a_dz_glibc"]))
+    assert (np.abs(r - expect)[~dz_ok] <= 1e-12 * np.maximum(1.0, np.abs(rr[~dz_ok]))).all()
 
 
 @pytest.mark.parametrize("name", TRAJ_NAMES)
@@ -158,26 +180,59 @@ def test_replay_return_n1(satrl_env, name):
     assert abs(ret - ret_ref) <= tol
 
 
-def test_autoreset_matches_oracle(satrl_env, oracle):
-    """step_autoreset over 64 envs x 300 steps vs the oracle's batched replay."""
-    E = satrl_env
-    n, T = 64, 300
-    rng = np.random.default_rng(5)
-    pa = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
-    ea = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
-    rew_o, done_o = oracle.rollout(n, T, pa, ea, d_capture=15000.0, max_episode_steps=120)
-    env = E.VecSatellites(n, d_capture=15000.0, max_episode_steps=120)
+def _locked_autoreset_rollout(E, oracle, n, T, seed, d_capture, max_ep, what):
+    """step_autoreset of n envs over T steps of U(-1.6, 1.6) actions, every
+    step checked against the oracle started from the GPU's own pre-step state
+    (oracle.step_planes), so one libm tie cannot desynchronise what follows.
+    Per step: done bit-exact; kinematics, fuel and dis planes bit-exact; obs
+    (f32) bit-exact for live envs; the danger-zone count exact except listed
+    libm ties; reward (f32) equal to the oracle's f64 reward rounded to f32
+    within 1 f32 ulp, or, on a tie, to it plus the count term's difference.
+    Returns (ties, steps with a live count)."""
+    rng = np.random.default_rng(seed)
+    env = E.VecSatellites(n, d_capture=d_capture, max_episode_steps=max_ep)
     env.reset(0)
-    R = np.zeros((T, n)); D = np.zeros((T, n), np.int32)
+    ties = 0
+    counted = 0
+    done_total = 0
     for t in range(T):
-        _, r, dn = env.step_autoreset(torch.tensor(pa[t], device="cuda"), torch.tensor(ea[t], device="cuda"))
-        R[t] = r.cpu().numpy(); D[t] = dn.cpu().numpy()
-    assert np.array_equal(D, done_o)
-    agree = np.abs(R - rew_o.astype(np.float32)) <= 1e-6 * np.maximum(1, np.abs(rew_o))
-    print(f"autoreset reward agreement {agree.mean():.4%}")
-    assert agree.mean() >= 0.995
+        pa = rng.uniform(-1.6, 1.6, (n, 3)).astype(np.float32)
+        ea = rng.uniform(-1.6, 1.6, (n, 3)).astype(np.float32)
+        f0, i0 = [x.cpu().numpy() for x in env.get_state()]
+        fo, io, ro, do = oracle.step_planes(f0, i0, pa, ea, i0[1] + 1, d_capture=d_capture, max_episode_steps=max_ep)
+        obs, r, dn = env.step_autoreset(torch.tensor(pa, device="cuda"), torch.tensor(ea, device="cuda"))
+        f1, i1 = [x.cpu().numpy() for x in env.get_state()]
+        dn = dn.cpu().numpy().astype(np.int32)
+        r = r.cpu().numpy()
+        obs = obs.cpu().numpy()
+        assert np.array_equal(dn, do), (what, t)
+        live = dn == 0
+        done_total += int((~live).sum())
+        assert np.array_equal(f1[:, live], fo[:, live]), (what, t)
+        assert np.array_equal(i1[2, live], io[2, live]), (what, t)
+        ob_o = np.concatenate([fo[0:3] - fo[6:9], fo[3:6] - fo[9:12], fo[0:12]]).T.astype(np.float32)
+        assert np.array_equal(obs[live], ob_o[live]), (what, t)
+        # the count is only computed on non-terminal steps (environment.py:139-150)
+        bad = assert_dz_libm_ties(oracle, fo[0:3].T, fo[3:6].T, fo[6:9].T, fo[9:12].T, fo[12], io[2] & 3,
+                                  np.where(live, i1[0], io[0]), io[0], f"{what} t={t}")
+        ties += len(bad)
+        counted += int(live.sum())
+        expect = ro.copy()
+        expect[bad] = ro[bad] + (_dz_term(i1[0][bad]) - _dz_term(io[0][bad]))
+        e32 = expect.astype(np.float32)
+        ulp = np.spacing(np.abs(e32))
+        assert (np.abs(r - e32) <= ulp).all(), (what, t, np.abs(r - e32).max())
+    assert env.check_errors() == 0
     st = env.stats.cpu().numpy()
-    assert st[0] == D.sum()
+    assert st[0] == done_total
+    print(f"{what}: {ties} libm-tie count(s) in {counted} counted env-steps, {done_total} episodes ended")
+    return ties, counted
+
+
+def test_autoreset_matches_oracle(satrl_env, oracle):
+    """step_autoreset over 64 envs x 300 steps, step-locked to the oracle."""
+    ties, counted = _locked_autoreset_rollout(satrl_env, oracle, 64, 300, 5, 15000.0, 120, "autoreset 64x300")
+    assert ties <= 2, ties
 
 
 # --- RK4 propagators (SURVEY.md §8f rank 3) ---------------------------------------
@@ -238,23 +293,8 @@ def test_env_rk4_cw_mode_bitexact_vs_oracle(satrl_env, oracle):
 
 @pytest.mark.parametrize("n", [1000, 20000])
 def test_autoreset_block_geometries_vs_oracle(satrl_env, oracle, n):
-    """Small and large env counts (64- vs 128-lane workgroups) against the
-    oracle rollout.  Bar: the
-    env tolerance of this file -- rewards within 1e-6 rel except where a
-    libm-sensitive danger-zone count flips (<= 0.1 % of env-steps)."""
-    T = 24
-    rng = np.random.default_rng(n)
-    pa = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
-    ea = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
-    rew_o, done_o = oracle.rollout(n, T, pa, ea, d_capture=15000.0, max_episode_steps=10, nthreads=8)
-    env = satrl_env.VecSatellites(n, d_capture=15000.0, max_episode_steps=10)
-    env.reset(0)
-    bad = 0
-    for t in range(T):
-        _, r, d = env.step_autoreset(torch.tensor(pa[t], device="cuda"), torch.tensor(ea[t], device="cuda"))
-        r = r.cpu().numpy().astype(np.float64)
-        ref = rew_o[t].astype(np.float32).astype(np.float64)
-        assert np.mean(d.cpu().numpy() != done_o[t]) <= 1e-3, t
-        bad += int(np.sum(np.abs(r - ref) > 1e-6 * np.maximum(1.0, np.abs(ref))))
-    assert bad <= 1e-3 * n * T, bad
-    assert env.check_errors() == 0
+    """Small and large env counts (64- vs 128-lane workgroups) step-locked to
+    the oracle (same bars as test_autoreset_matches_oracle: done exact, counts
+    exact but for listed libm ties)."""
+    ties, counted = _locked_autoreset_rollout(satrl_env, oracle, n, 24, n, 15000.0, 10, f"autoreset n={n}")
+    assert ties <= max(2, counted // 20000), (ties, counted)

@@ -48,6 +48,31 @@ def test_danger_zone_counts(oracle):
     assert set(np.unique(got)) == {0, 1, 2}
 
 
+def test_libm_tie_probe(oracle):
+    """The ulp-jitter probe the GPU tests use to prove a count mismatch is a
+    libm tie: it reproduces the reference's own SVML-vs-glibc count
+    disagreement in dz_cases, and flips none of 300 random cases (so a
+    'tie' verdict is specific, not something every state allows)."""
+    from conftest import R_CW, V_CW  # noqa: F401
+    d = golden("dz_cases")
+    X, fuel, mode = d["X"], d["fuel"], d["mode"]
+    mis = np.nonzero(d["count"] != d["count_glibc"])[0]
+    assert len(mis) >= 1
+    for i in mis:
+        x = X[i]
+        assert oracle.dz_libm_tie(x[0:3], x[3:6], x[6:9], x[9:12], fuel[i], mode[i], d["count"][i]) != 0, i
+    rng = np.random.default_rng(0)
+    flips = 0
+    for i in rng.choice(len(X), 300, replace=False):
+        x = X[i]
+        for k in {0, 1, 2} - {int(d["count_glibc"][i])}:
+            flips += oracle.dz_libm_tie(x[0:3], x[3:6], x[6:9], x[9:12], fuel[i], mode[i], k, seeds=64) != 0
+    assert flips == 0, flips
+    # seed 0 is the exact restatement again
+    x = X[0]
+    assert oracle.danger_zone(x[0:3], x[3:6], x[6:9], x[9:12], fuel[0], mode[0])[1] == d["count_glibc"][0]
+
+
 @pytest.mark.parametrize("name", TRAJ_NAMES)
 def test_traj_per_step(oracle, name):
     d = golden(name)

@@ -180,7 +180,8 @@ def test_update_matches_reference():
 
 
 @pytest.mark.parametrize("H,split,mb", [(64, False, 512), (256, False, 512), (256, True, 512),
-                                         (256, False, 777), (64, False, 100)])
+                                         (256, False, 777), (64, False, 100),
+                                         (256, False, 4096), (64, False, 4096)])
 def test_fused_step_vs_torch_autograd(H, split, mb):
     """satrl_ppo_rowpass (f32 MFMA) + hipBLASLt dW2 + reduce + Adam vs plain torch fp32 autograd +
     clip_grad_norm_ + torch.optim.Adam on the same minibatch; mb 777 / 100 are
@@ -222,6 +223,98 @@ def test_fused_step_vs_torch_autograd(H, split, mb):
     assert L.steps.cpu().tolist() == [1.0, 1.0]
     # Adam also refreshed fc2.weight^T (the dH1 operand of the next rowpass)
     assert torch.equal(L.W2T.view(2, H, H), L.P[:2 * H * H].view(2, H, H).transpose(1, 2))
+
+
+def _packed_rows(B, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    src = torch.zeros((B, 32), device="cuda")
+    src[:, 0:18] = torch.randn((B, 18), device="cuda", generator=g)
+    src[:, 18:21] = torch.rand((B, 3), device="cuda", generator=g) * 3.2 - 1.6
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+    src[:, 24] = torch.randn(B, device="cuda", generator=g)
+    src[:, 25] = torch.randn(B, device="cuda", generator=g) * 5
+    return src, g
+
+
+def _reference_epoch(actor, critic, src, perm, mb, lr, eps=1e-5):
+    """BatchSampler(drop_last=False) minibatches of one epoch on plain torch
+    fp32 modules with persistent Adam state (ppo_continuous.py:212-239)."""
+    import copy
+    from torch_reference import actor_loss, critic_loss
+    actor, critic = copy.deepcopy(actor), copy.deepcopy(critic)
+    for p in list(actor.parameters()) + list(critic.parameters()):
+        p.data = p.data.contiguous().clone()
+        p.requires_grad_(True)
+    oa = torch.optim.Adam(actor.parameters(), lr=lr, eps=eps)
+    oc = torch.optim.Adam(critic.parameters(), lr=lr, eps=eps)
+    for k in range(0, perm.numel(), mb):
+        rows = src[perm[k:k + mb]]
+        s, a, lp, adv, vt = rows[:, 0:18], rows[:, 18:21], rows[:, 21:24], rows[:, 24:25], rows[:, 25:26]
+        oa.zero_grad()
+        actor_loss(actor, s, a, lp, adv, 0.1, 0.01).backward()
+        torch.nn.utils.clip_grad_norm_(actor.parameters(), 0.5)
+        oa.step()
+        oc.zero_grad()
+        critic_loss(critic, s, vt).backward()
+        torch.nn.utils.clip_grad_norm_(critic.parameters(), 0.5)
+        oc.step()
+    params = {"actor." + n: p.detach().clone() for n, p in actor.named_parameters()}
+    params.update({"critic." + n: p.detach().clone() for n, p in critic.named_parameters()})
+    return params
+
+
+@pytest.mark.parametrize("H,mb,B,graph", [(128, 1056, 2080, False), (64, 4128, 8192, False),
+                                          (256, 4096, 4873, True), (64, 4096, 4873, True)])
+def test_epoch_with_ragged_tail_vs_torch(H, mb, B, graph):
+    """One epoch (full minibatches, graphed or eager, then the ragged
+    BatchSampler tail) vs plain torch fp32 autograd + clip + Adam with
+    persistent optimiser state.  (128, 1056, 2080) and (64, 4128, 8192) are
+    shapes whose tail has more dW2 splits than the full minibatch (the p2
+    slabs are sized for the largest split count)."""
+    from satrl.ppo import PPOLearner
+    torch.manual_seed(5)
+    args = _args(hidden_width=H, mini_batch_size=mb, batch_size=B, K_epochs=1, use_lr_decay=False)
+    L = PPOLearner(args, "pursuer", use_graph=graph, graph_group=1)
+    with torch.no_grad():
+        for p in list(L.actor.parameters()) + list(L.critic.parameters()):
+            p.add_(torch.randn_like(p) * 0.05)
+    src, g = _packed_rows(B, seed=1)
+    perm = torch.randperm(B, device="cuda", generator=g)
+    ref = _reference_epoch(L.actor, L.critic, src, perm, mb, args.lr_a)
+    L.update_packed(src, 0, perms=[perm])
+    torch.cuda.synchronize()
+    P = L.flat_views(L.P)
+    nsteps = -(-B // mb)
+    for k, r in ref.items():
+        got = P[k].reshape(r.shape)
+        assert torch.allclose(got, r, rtol=1e-5, atol=2e-7 * nsteps), (k, (got - r).abs().max().item())
+    assert L.steps.cpu().tolist() == [float(nsteps)] * 2
+
+
+def test_lr_decay_is_clamped_at_the_budget():
+    """ppo_continuous.py:244-250 with the engine's episode count past
+    max_train_steps: lr stops at 0 instead of turning negative (a negative
+    lr would make Adam ascend), and VecTrainer.train stops at the budget."""
+    from satrl.ppo import PPOLearner
+    from satrl.trainer import VecTrainer
+    args = _args(hidden_width=64, max_train_steps=100)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    L.lr_decay(50)
+    assert L.lr_now[0] == pytest.approx(1e-4, rel=1e-6)
+    L.lr_decay(100)
+    assert L.lr_now == (0.0, 0.0)
+    L.lr_decay(10 ** 6)
+    assert L.lr_now == (0.0, 0.0)
+    args = _args(batch_size=64 * 32, mini_batch_size=512, hidden_width=64, K_epochs=1, num_envs=64, horizon=32,
+                 max_episode_steps=10, seed=3, rollout_graph_chunk=8, update_graph_group=2, max_train_steps=300)
+    tr = VecTrainer(args, flag=0, d_capture=15000.0)
+    stats = tr.train(max_iterations=20)
+    assert tr.budget_reached and len(stats) < 20
+    assert tr.episodes >= 300
+    la, lc = tr.learner.lr_now
+    assert 0.0 <= la < args.lr_a and 0.0 <= lc < args.lr_c
+    tr.update()                                   # one more update past the budget: lr 0, not negative
+    assert tr.learner.lr_now == (0.0, 0.0)
 
 
 def test_vec_trainer_iteration_and_determinism():
