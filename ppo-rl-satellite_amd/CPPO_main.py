@@ -25,9 +25,12 @@ def main():
     ap.add_argument("--episodes", type=int, default=None)
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--iterations", type=int, default=1)
+    ap.add_argument("--device", default=None,
+                    help="'cpu': the drop-in on host cores (env host build + torch-CPU agents; BASELINE configs[0])")
     a = ap.parse_args()
     # CPPO_main.py:326-334
-    args = args_param(max_episode_steps=64, batch_size=64, max_train_steps=5000, K_epochs=3, chkpt_dir=a.chkpt_dir)
+    args = args_param(max_episode_steps=64, batch_size=64, max_train_steps=5000, K_epochs=3, chkpt_dir=a.chkpt_dir,
+                      device=a.device)
     if a.vec:
         args = args_param(max_episode_steps=1000, num_envs=a.num_envs, horizon=2048, batch_size=a.num_envs * 2048,
                           mini_batch_size=4096, hidden_width=256, K_epochs=10, chkpt_dir=a.chkpt_dir)
@@ -39,7 +42,7 @@ def main():
                      Pursuer_vector=np.array([1710, 1140, 1300]),
                      Escaper_position=np.array([1850000, 2000000, 1000000]),
                      Escaper_vector=np.array([1710, 1140, 1300]),
-                     d_capture=50000, args=args)
+                     d_capture=50000, args=args, device=a.device)
     if a.train_pursuer:
         train_pursuer_network(args, env, show_picture=False, pre_train=True, d_capture=15000, max_episodes=a.episodes)
     elif a.train_evader:

@@ -13,9 +13,30 @@
 // Transcendentals are OCML (gfx950), which differs from the reference's
 // numpy/glibc libm by <= 1-2 ulp; parity is therefore a tolerance on
 // continuous outputs and exact on counts/done except libm-sensitive ties.
+//
+// One source, two targets: hipcc compiles it for gfx950 (the env kernels)
+// and g++ compiles the same functions for the host (satenv_cpu.cpp, the
+// satenv_cpu_* ABI: SURVEY.md §7 "one FP64 math core").  On the host the
+// transcendentals are glibc's, so the host build computes what the
+// reference computes with glibc libm; only the fsolve residual's sincos
+// differs by target (OCML's transcription on the device, see resid()).
 #pragma once
-#include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SATENV_HD __host__ __device__ __forceinline__
+#define SATENV_HD_NOINLINE __host__ __device__ __noinline__
+#else
+#include <cmath>
+#include <cstring>
+#define SATENV_HD static inline
+#define SATENV_HD_NOINLINE static __attribute__((noinline))
+static inline long long __double_as_longlong(double x) { long long v; std::memcpy(&v, &x, 8); return v; }
+static inline double __longlong_as_double(long long v) { double x; std::memcpy(&x, &v, 8); return x; }
+using std::acos; using std::atan; using std::cos; using std::fabs; using std::fma; using std::pow; using std::rint;
+using std::sin; using std::sqrt; using std::trunc;
+#endif
 
 #include "satenv.h"
 
@@ -29,21 +50,39 @@ constexpr double kEpsMch = 2.220446049250313e-16;
 enum : int { kPyInt = 0, kI64 = 1, kF32 = 2, kF64 = 3 };
 
 // per-env int "bits" plane: [1:0] fuel_c mode, [3:2] fuel_t mode, [4] vel_int, [5] flag
-__device__ __forceinline__ int fc_mode(int b) { return b & 3; }
-__device__ __forceinline__ int ft_mode(int b) { return (b >> 2) & 3; }
-__device__ __forceinline__ int vel_int(int b) { return (b >> 4) & 1; }
-__device__ __forceinline__ int env_flag(int b) { return (b >> 5) & 1; }
-__device__ __forceinline__ int make_bits(int fc, int ft, int vi, int flag) {
+SATENV_HD int fc_mode(int b) { return b & 3; }
+SATENV_HD int ft_mode(int b) { return (b >> 2) & 3; }
+SATENV_HD int vel_int(int b) { return (b >> 4) & 1; }
+SATENV_HD int env_flag(int b) { return (b >> 5) & 1; }
+SATENV_HD int make_bits(int fc, int ft, int vi, int flag) {
   return (fc & 3) | ((ft & 3) << 2) | ((vi & 1) << 4) | ((flag & 1) << 5);
 }
 
 using Params = satenv_params;   // include/satenv.h
 
+// python/numpy scalar `x ** 2` (the reference squares scalars with pow):
+// glibc pow(x, 2.0) on the host -- which is not always x*x, it is off by an
+// ulp on ~0.05 % of inputs -- and the correctly rounded x*x on gfx950
+SATENV_HD double pow2(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return x * x;
+#else
+  return pow(x, 2.0);
+#endif
+}
+SATENV_HD float pow2f(float x) {            // np.float32 ** 2
+#if defined(__HIP_DEVICE_COMPILE__)
+  return x * x;
+#else
+  return powf(x, 2.0f);
+#endif
+}
+
 // OpenBLAS ddot, n = 3 (numpy np.dot / np.linalg.norm of 3-vectors)
-__device__ __forceinline__ double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
+SATENV_HD double dot3(double a0, double a1, double a2, double b0, double b1, double b2) {
   return fma(a2, b2, fma(a1, b1, a0 * b0));
 }
-__device__ __forceinline__ double norm3(double a0, double a1, double a2) {
+SATENV_HD double norm3(double a0, double a1, double a2) {
   return sqrt(dot3(a0, a1, a2, a0, a1, a2));
 }
 
@@ -54,12 +93,12 @@ __device__ __forceinline__ double norm3(double a0, double a1, double a2) {
 // ---------------------------------------------------------------------------
 struct Elements { double a, e, i, omega, Omega, f; };
 
-__device__ __forceinline__ int orbital_elements(double mu, double R0, double R1, double R2, double V0,
+SATENV_HD int orbital_elements(double mu, double R0, double R1, double R2, double V0,
                                                 double V1, double V2, Elements& out) {
   const double r_norm = norm3(R0, R1, R2);
   const double v_norm = norm3(V0, V1, V2);
   const double r_dot_v = dot3(R0, R1, R2, V0, V1, V2);
-  const double v2 = v_norm * v_norm;                       // v_norm ** 2
+  const double v2 = pow2(v_norm);                          // v_norm ** 2
   const double en = 2.0 / r_norm - v2 / mu;                // :186
   if (en == 0.0) return -5;
   out.a = 1.0 / fabs(en);                                  // :188
@@ -102,7 +141,7 @@ __device__ __forceinline__ int orbital_elements(double mu, double R0, double R1,
 // interleave -- sincos() itself branches to the large-argument reduction,
 // which serialises independent calls.  |x| >= 2^30 and inf/NaN go to
 // sincos() (see sincos_fast).
-__device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_out) {
+SATENV_HD void sincos_small(double x, double& s_out, double& c_out) {
   const double ax = fabs(x);
   // __ocmlpriv_trigredsmall_f64
   const double q = rint(ax * 0x1.45f306dc9c883p-1);                 // 2/pi
@@ -158,22 +197,22 @@ __device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_
 
 // sincos() with the straight-line body for |x| < 2^30 (every argument of
 // the env step in practice); the rare rest takes the library call
-__device__ __forceinline__ void sincos_fast(double x, double& s, double& c) {
+SATENV_HD void sincos_fast(double x, double& s, double& c) {
   sincos_small(x, s, c);
   if (!(fabs(x) < 0x1.0p+30)) sincos(x, &s, &c);
 }
 
-__device__ __forceinline__ double resid(double A, double st, double dvm, double a) {
+SATENV_HD double resid(double A, double st, double dvm, double a) {
   double s, c;
-#ifdef SATENV_RESID_LIBSINCOS
-  sincos(a, &s, &c);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(SATENV_RESID_LIBSINCOS)
+  sincos_fast(a, s, c);          // gfx950: OCML's sincos, straight-line
 #else
-  sincos_fast(a, s, c);
+  sincos(a, &s, &c);             // host (glibc) / library check build
 #endif
   return A * (dvm * c) + st * (-dvm * s);
 }
 
-__device__ __noinline__ double hybrd1(double A, double st, double dvm, double x) {
+SATENV_HD_NOINLINE double hybrd1(double A, double st, double dvm, double x) {
   const double xtol = 1.49012e-08, factor = 100.0;
   const double eps = 1.4901161193847656e-08;               // sqrt(max(epsfcn, epsmch))
   double fvec = resid(A, st, dvm, x);
@@ -295,10 +334,10 @@ struct Pursuer { double u, dv2, e, f0, p, r, sf0, X, sq; };
 // count can advance all four of an env's solves in one hybrdN<4>
 struct RfSolve { bool ok; double vx0, vy0, dvm, st, ct; double A[2], ag[2]; };
 
-__device__ __forceinline__ void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
+SATENV_HD void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
   const double d = f_c - P.f0;
   const double sd = sin(d);
-  const double temp1 = (sd * sd) / (P.u * (P.X * P.X) / (P.p * P.dv2) - 1.0);    // :466
+  const double temp1 = pow2(sd) / (P.u * pow2(P.X) / (P.p * P.dv2) - 1.0);      // :466
   q.ok = (0.0 <= temp1);                                                         // else (0, 0), :477
   q.vx0 = q.vy0 = q.dvm = q.st = q.ct = 0.0;
   q.A[0] = q.A[1] = 0.0;
@@ -307,7 +346,7 @@ __device__ __forceinline__ void rf_setup(const Pursuer& P, double f_c, RfSolve& 
   if (!q.ok) return;
   const double beta = atan(0.0 / sd);                                            // tan(fai)=0, :469
   const double sb = sin(beta), cb = cos(beta);
-  q.dvm = sqrt(P.dv2 - P.u * (P.X * P.X) * (sb * sb) / P.p);                     // :470
+  q.dvm = sqrt(P.dv2 - P.u * pow2(P.X) * pow2(sb) / P.p);                        // :470
   double theta = 0.0;
   if ((-kTwoPi <= d && d < -kPi) || (0.0 <= d && d < kPi)) theta = acos(cos(d) * 1.0);          // :473
   else if ((-kPi <= d && d < 0.0) || (kPi <= d && d < kTwoPi)) theta = kTwoPi - acos(cos(d) * 1.0);
@@ -325,7 +364,7 @@ __device__ __forceinline__ void rf_setup(const Pursuer& P, double f_c, RfSolve& 
 }
 
 // rf from the two solutions, abs and sort (:525-530, :549-556)
-__device__ __forceinline__ void rf_finish(const Pursuer& P, const RfSolve& q, double al0, double al1, double& rmax,
+SATENV_HD void rf_finish(const Pursuer& P, const RfSolve& q, double al0, double al1, double& rmax,
                                           double& rmin) {
   if (!q.ok) { rmax = 0.0; rmin = 0.0; return; }
   double rf[2];
@@ -335,7 +374,7 @@ __device__ __forceinline__ void rf_finish(const Pursuer& P, const RfSolve& q, do
     sincos(k == 0 ? al0 : al1, &sa, &ca);
     const double vx = q.vx0 + q.dvm * ca, vy = q.vy0 + q.dvm * sa;               // :525-528
     const double hm = P.r * vy;
-    rf[k] = (hm * hm) / (P.u * (1.0 - q.ct) + hm * vy * q.ct - hm * vx * q.st);  // :530
+    rf[k] = pow2(hm) / (P.u * (1.0 - q.ct) + hm * vy * q.ct - hm * vx * q.st);   // :530
   }
   rmax = fabs(rf[0]);
   rmin = fabs(rf[1]);
@@ -343,9 +382,10 @@ __device__ __forceinline__ void rf_finish(const Pursuer& P, const RfSolve& q, do
 }
 
 // self.Delta_V_c ** 2 by numpy scalar type
-__device__ __forceinline__ double fuel_sq(double fuel, int mode) {
-  if (mode == kF32) { const float f = (float)fuel; return (double)(f * f); }
-  return fuel * fuel;
+SATENV_HD double fuel_sq(double fuel, int mode) {
+  if (mode == kF32) return (double)pow2f((float)fuel);
+  const double exact = fuel * fuel;                        // python int ** 2: exact
+  return (mode == kF64) ? pow2(fuel) : exact;              // (one expression on gfx950)
 }
 
 // environment.py:317-332 + satellite_function.py:18-99,317-373, cut at its
@@ -356,7 +396,7 @@ __device__ __forceinline__ double fuel_sq(double fuel, int mode) {
 // <0 (a non-6-element orbit branch).
 struct DzCtx { Pursuer P; RfSolve q[2]; double r_ft1, r_ft2; };
 
-__device__ __forceinline__ int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
+SATENV_HD int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
                                         double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
                                         double Ev1, double Ev2, double fuel, int fmode, DzCtx& z) {
   const double u = 3.986e14;                                // Time_window_of_danger_zone default u
@@ -376,7 +416,7 @@ __device__ __forceinline__ int dz_setup(const Params& prm, double Pp0, double Pp
   sincos(C.f, &sf0, &cf0);
   P.sf0 = sf0;
   P.X = 1.0 + C.e * cf0;
-  P.p = C.a * (1.0 - C.e * C.e);                                                 // :58
+  P.p = C.a * (1.0 - pow2(C.e));                                                 // :58
   P.r = P.p / P.X;                                                               // :57 (a(1-e^2)/(1+e cos f0))
   P.sq = sqrt(u / P.p);
   // :317-339 latitudinal angles
@@ -392,14 +432,14 @@ __device__ __forceinline__ int dz_setup(const Params& prm, double Pp0, double Pp
   const double u_t1 = atan(temp2), u_t2 = u_t1 + kPi;
   rf_setup(P, u_c1 - C.omega, z.q[0]);                                           // rf_extreme_point('orbit_c1')
   rf_setup(P, u_c2 - C.omega, z.q[1]);                                           // ('orbit_c2')
-  const double pt = T.a * (1.0 - T.e * T.e);
+  const double pt = T.a * (1.0 - pow2(T.e));
   z.r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                             // :363 (cross-wired f_t2)
   z.r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                             // :365
   return 0;
 }
 
 // al[2c + k] = the fsolve solution of problem (c, k)
-__device__ __forceinline__ int dz_finish(const DzCtx& z, const double (&al)[4]) {
+SATENV_HD int dz_finish(const DzCtx& z, const double (&al)[4]) {
   double mx1, mn1, mx2, mn2;
   rf_finish(z.P, z.q[0], al[0], al[1], mx1, mn1);
   rf_finish(z.P, z.q[1], al[2], al[3], mx2, mn2);
@@ -408,7 +448,7 @@ __device__ __forceinline__ int dz_finish(const DzCtx& z, const double (&al)[4]) 
 }
 
 // the whole count in one lane (the four solves one after another)
-__device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
+SATENV_HD int danger_zone(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
                                            double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
                                            double Ev1, double Ev2, double fuel, int fmode, int& count) {
   DzCtx z;
@@ -425,12 +465,12 @@ __device__ __forceinline__ int danger_zone(const Params& prm, double Pp0, double
 }
 
 // np.clip(a, -1.6, 1.6) on np.float32
-__device__ __forceinline__ float clip16(float a) {
+SATENV_HD float clip16(float a) {
   return a < -1.6f ? -1.6f : (a > 1.6f ? 1.6f : a);
 }
 
 // fuel -= |a0|+|a1|+|a2| under numpy scalar promotion (environment.py:106-107)
-__device__ __forceinline__ void fuel_sub(double& fuel, int& mode, bool zero_int_action, float s) {
+SATENV_HD void fuel_sub(double& fuel, int& mode, bool zero_int_action, float s) {
   if (zero_int_action) {
     mode = (mode == kPyInt) ? kI64 : ((mode == kF32) ? kF64 : mode);
     return;
@@ -439,13 +479,13 @@ __device__ __forceinline__ void fuel_sub(double& fuel, int& mode, bool zero_int_
   else { fuel = fuel - (double)s; mode = kF64; }
 }
 
-__device__ __forceinline__ double cos_sim(double a0, double a1, double a2, double b0, double b1, double b2) {
+SATENV_HD double cos_sim(double a0, double a1, double a2, double b0, double b1, double b2) {
   const double na = norm3(a0, a1, a2), nb = norm3(b0, b1, b2);
   return dot3(a0 / na, a1 / na, a2 / na, b0 / nb, b1 / nb, b2 / nb);
 }
 
 // float32 np.linalg.norm (OpenBLAS sdot: f32 products summed in double)
-__device__ __forceinline__ float norm3f(float a0, float a1, float a2) {
+SATENV_HD float norm3f(float a0, float a1, float a2) {
   double s = (double)(a0 * a0);
   s += (double)(a1 * a1);
   s += (double)(a2 * a2);
@@ -461,7 +501,7 @@ __device__ __forceinline__ float norm3f(float a0, float a1, float a2) {
 // reference's rounding order.
 // ---------------------------------------------------------------------------
 template <class F>
-__device__ __forceinline__ void rk4_step(F f, const double (&r0)[6], double h, double (&out)[6]) {
+SATENV_HD void rk4_step(F f, const double (&r0)[6], double h, double (&out)[6]) {
   double k1[6], k2[6], k3[6], k4[6], t[6];
   const double h2 = h / 2.0, h6 = h / 6.0;
   f(r0, k1);
@@ -479,7 +519,7 @@ __device__ __forceinline__ void rk4_step(F f, const double (&r0)[6], double h, d
 }
 
 // StateEq (:15-31), km units; `**` on numpy scalars is pow()
-__device__ __forceinline__ void j2_rhs(const double (&rv)[6], double (&f)[6]) {
+SATENV_HD void j2_rhs(const double (&rv)[6], double (&f)[6]) {
   constexpr double kMu = 398600.0, kRe = 6378.137, kJ2 = 0.00108263;
   const double x = rv[0], y = rv[1], z = rv[2];
   const double r = sqrt((pow(x, 2.0) + pow(y, 2.0)) + pow(z, 2.0));
@@ -492,7 +532,7 @@ __device__ __forceinline__ void j2_rhs(const double (&rv)[6], double (&f)[6]) {
 }
 
 // RK4 on the CW ODE (propagator 1), t seconds in nsub steps
-__device__ __forceinline__ void cw_rk4(double (&s)[6], double w, double t, int nsub) {
+SATENV_HD void cw_rk4(double (&s)[6], double w, double t, int nsub) {
   const double w2 = w * w, h = t / (double)nsub;
   auto f = [w, w2](const double (&x)[6], double (&o)[6]) {
     o[0] = x[3]; o[1] = x[4]; o[2] = x[5];

@@ -82,6 +82,18 @@ _SIGS = {
     "satenv_surrogate": ([_vp, _vp, _vp, _vp], C.c_int),
     "satenv_surrogate_mlp": ([_i64, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_ellipse_fit": ([_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_last_error": ([], C.c_char_p),
+    "satenv_cpu_create": ([C.POINTER(_vp), _i64, C.POINTER(SatenvParams), C.c_int], C.c_int),
+    "satenv_cpu_destroy": ([_vp], C.c_int),
+    "satenv_cpu_num_envs": ([_vp, C.POINTER(_i64)], C.c_int),
+    "satenv_cpu_set_params": ([_vp, C.POINTER(SatenvParams)], C.c_int),
+    "satenv_cpu_reset": ([_vp, _i32, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_step": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_step_autoreset": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_get_state": ([_vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_set_state": ([_vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_danger_zone": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_cpu_check": ([_vp, C.POINTER(_i32)], C.c_int),
     "satrl_gae": ([_i64, _i64, _vp, _vp, _vp, C.c_float, C.c_float, _vp, _vp, _vp], C.c_int),
     "satrl_gaussian_sample": ([_i64, _vp, _vp, C.c_float, C.c_uint64, C.c_uint32, _i64, C.c_uint64, _vp, _vp, _vp,
                                _vp],
@@ -133,7 +145,8 @@ def lib():
 def check(rc: int, what: str):
     if rc != 0:
         L = lib()
-        msg = (L.satenv_last_error() if what.startswith("satenv") else
+        msg = (L.satenv_cpu_last_error() if what.startswith("satenv_cpu") else
+               L.satenv_last_error() if what.startswith("satenv") else
                L.satrl_ppo_last_error() if what.startswith("satrl_ppo") else L.satrl_last_error()).decode()
         raise NativeError(f"{what} failed ({rc}): {msg}")
 
@@ -150,9 +163,20 @@ def stream_ptr(stream=None):
     return C.c_void_p(s.cuda_stream)
 
 
+def require_cpu(t, dtype, shape=None, name="tensor"):
+    """Host-build (satenv_cpu_*) argument check: a contiguous CPU tensor."""
+    if t.is_cuda:
+        raise NativeError(f"{name} must be a host (cpu) tensor for the host build")
+    return _require(t, dtype, shape, name)
+
+
 def require_cuda(t, dtype, shape=None, name="tensor"):
     if not t.is_cuda:
         raise NativeError(f"{name} must be a device (cuda/HIP) tensor")
+    return _require(t, dtype, shape, name)
+
+
+def _require(t, dtype, shape, name):
     if t.dtype != dtype:
         raise NativeError(f"{name} must be {dtype}, got {t.dtype}")
     if not t.is_contiguous():

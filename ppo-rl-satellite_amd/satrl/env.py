@@ -7,8 +7,12 @@
   keywords, ``reset(Flag)`` / ``step(pursuer_action, escaper_action,
   epsiode_count)`` signatures, numpy outputs with the reference's dtypes and
   the attributes its callers read (``observation_space``, ``action_space``,
-  ``d_capture`` ...).  It runs one env on the GPU kernel -- there is no CPU
-  implementation in the product.
+  ``d_capture`` ...).  It runs one env on the GPU kernel.
+
+Both run on the host build of the same env ABI (include/satenv_cpu.h: the
+step source compiled by g++, OpenMP over envs) when asked with
+device="cpu" -- BASELINE.json configs[0], CPPO_main on a machine without a
+GPU.  Nothing falls back to it: without a GPU the default device raises.
 """
 from __future__ import annotations
 
@@ -19,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import ACT_DIM, OBS_DIM, SATENV_F64_PLANES, SATENV_I32_PLANES, check, ptr, require_cuda, stream_ptr
+from ._lib import ACT_DIM, OBS_DIM, SATENV_F64_PLANES, SATENV_I32_PLANES, check, ptr, require_cpu, require_cuda, stream_ptr
 
 PYINT, I64, F32, F64 = 0, 1, 2, 3
 STATE_F64 = ["Pp0", "Pp1", "Pp2", "Pv0", "Pv1", "Pv2", "Ep0", "Ep1", "Ep2", "Ev0", "Ev1", "Ev2",
@@ -100,30 +104,46 @@ class VecSatellites:
     """``num_envs`` reference environments stepped by one HIP kernel launch.
 
     Tensors are device tensors on ``device`` (actions f32 [N,3]); every call
-    is asynchronous on the current torch stream.
-    """
+    is asynchronous on the current torch stream.  device="cpu": the host
+    build (satenv_cpu_*, synchronous, `threads` OpenMP threads, 0 = all)."""
 
     def __init__(self, num_envs: int, device=None, d_capture: float = 100000.0, d_range: float = 100000.0,
-                 max_episode_steps: int = 1000, Flag: int = 0, fuel_c=320, fuel_t=320, **params):
-        if not torch.cuda.is_available():
-            raise _lib.NativeError("VecSatellites needs a HIP device (MI355X); no CPU implementation exists")
-        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+                 max_episode_steps: int = 1000, Flag: int = 0, fuel_c=320, fuel_t=320, threads: int = 0, **params):
+        self.host = device is not None and torch.device(device).type == "cpu"
+        if not self.host and not torch.cuda.is_available():
+            raise _lib.NativeError("VecSatellites needs a HIP device (MI355X); the host build runs only when asked "
+                                   "for with device='cpu'")
+        if self.host:
+            self.device = torch.device("cpu")
+        else:
+            self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self._api = "satenv_cpu_" if self.host else "satenv_"
+        self._req = require_cpu if self.host else require_cuda
         self.num_envs = int(num_envs)
         self._p = default_params(d_capture=float(d_capture), d_range=float(d_range),
                                  max_episode_steps=int(max_episode_steps), flag=int(Flag), fuel_c0=float(fuel_c),
                                  fuel_t0=float(fuel_t), fuel_c0_mode=_num_mode(fuel_c),
                                  fuel_t0_mode=_num_mode(fuel_t), **params)
         h = C.c_void_p()
-        with torch.cuda.device(self.device):
-            check(_lib.lib().satenv_create(C.byref(h), self.num_envs, C.byref(self._p), self.device.index or 0),
-                  "satenv_create")
+        if self.host:
+            check(self._fn("create")(C.byref(h), self.num_envs, C.byref(self._p), int(threads)), "satenv_cpu_create")
+        else:
+            with torch.cuda.device(self.device):
+                check(_lib.lib().satenv_create(C.byref(h), self.num_envs, C.byref(self._p), self.device.index or 0),
+                      "satenv_create")
         self._h = h
         self.observation_space, self.action_space, self.action_space_beta = _spaces()
         self.stats = torch.zeros(4, dtype=torch.float64, device=self.device)
 
+    def _fn(self, name):
+        return getattr(_lib.lib(), self._api + name)
+
+    def _sp(self):
+        return None if self.host else stream_ptr()
+
     # -- parameters -----------------------------------------------------------
     def _push_params(self):
-        check(_lib.lib().satenv_set_params(self._h, C.byref(self._p)), "satenv_set_params")
+        check(self._fn("set_params")(self._h, C.byref(self._p)), self._api + "set_params")
 
     @property
     def d_capture(self):
@@ -159,9 +179,9 @@ class VecSatellites:
         if obs_out is None and obs64_out is None:
             obs_out = torch.empty((n, OBS_DIM), dtype=torch.float32, device=self.device)
         if mask is not None:
-            require_cuda(mask, torch.uint8, (n,), "mask")
-        check(_lib.lib().satenv_reset(self._h, int(Flag), ptr(mask), ptr(obs_out), ptr(obs64_out), stream_ptr()),
-              "satenv_reset")
+            self._req(mask, torch.uint8, (n,), "mask")
+        check(self._fn("reset")(self._h, int(Flag), ptr(mask), ptr(obs_out), ptr(obs64_out), self._sp()),
+              self._api + "reset")
         return obs_out if obs_out is not None else obs64_out
 
     def step(self, pursuer_action, escaper_action, epsiode_count=None, obs_out=None, obs64_out=None,
@@ -170,19 +190,18 @@ class VecSatellites:
 
         Returns (obs f32 [N,18] or obs64, reward f64 [N], done u8 [N])."""
         n = self.num_envs
-        require_cuda(pursuer_action, torch.float32, (n, ACT_DIM), "pursuer_action")
-        require_cuda(escaper_action, torch.float32, (n, ACT_DIM), "escaper_action")
+        self._req(pursuer_action, torch.float32, (n, ACT_DIM), "pursuer_action")
+        self._req(escaper_action, torch.float32, (n, ACT_DIM), "escaper_action")
         if epsiode_count is not None:
-            require_cuda(epsiode_count, torch.int32, (n,), "epsiode_count")
+            self._req(epsiode_count, torch.int32, (n,), "epsiode_count")
         if obs_out is None and obs64_out is None:
             obs_out = torch.empty((n, OBS_DIM), dtype=torch.float32, device=self.device)
         if reward_out is None:
             reward_out = torch.empty(n, dtype=torch.float64, device=self.device)
         if done_out is None:
             done_out = torch.empty(n, dtype=torch.uint8, device=self.device)
-        check(_lib.lib().satenv_step(self._h, ptr(pursuer_action), ptr(escaper_action), ptr(epsiode_count),
-                                     ptr(obs_out), ptr(obs64_out), ptr(reward_out), ptr(done_out), stream_ptr()),
-              "satenv_step")
+        check(self._fn("step")(self._h, ptr(pursuer_action), ptr(escaper_action), ptr(epsiode_count), ptr(obs_out),
+                               ptr(obs64_out), ptr(reward_out), ptr(done_out), self._sp()), self._api + "step")
         return (obs_out if obs_out is not None else obs64_out), reward_out, done_out
 
     def step_autoreset(self, pursuer_action, escaper_action, obs_out=None, reward_out=None, done_out=None,
@@ -197,35 +216,37 @@ class VecSatellites:
             reward_out = torch.empty(n, dtype=torch.float32, device=self.device)
         if done_out is None:
             done_out = torch.empty(n, dtype=torch.uint8, device=self.device)
-        check(_lib.lib().satenv_step_autoreset(self._h, ptr(pursuer_action), ptr(escaper_action), ptr(obs_out),
-                                               ptr(reward_out), ptr(done_out), ptr(self.stats) if stats else None,
-                                               stream_ptr()), "satenv_step_autoreset")
+        if self.host:
+            self._req(pursuer_action, torch.float32, (n, ACT_DIM), "pursuer_action")
+            self._req(escaper_action, torch.float32, (n, ACT_DIM), "escaper_action")
+        check(self._fn("step_autoreset")(self._h, ptr(pursuer_action), ptr(escaper_action), ptr(obs_out),
+                                         ptr(reward_out), ptr(done_out), ptr(self.stats) if stats else None,
+                                         self._sp()), self._api + "step_autoreset")
         return obs_out, reward_out, done_out
 
     def get_state(self):
         n = self.num_envs
         f = torch.empty((SATENV_F64_PLANES, n), dtype=torch.float64, device=self.device)
         i = torch.empty((SATENV_I32_PLANES, n), dtype=torch.int32, device=self.device)
-        check(_lib.lib().satenv_get_state(self._h, ptr(f), ptr(i), stream_ptr()), "satenv_get_state")
+        check(self._fn("get_state")(self._h, ptr(f), ptr(i), self._sp()), self._api + "get_state")
         return f, i
 
     def set_state(self, f64_planes=None, i32_planes=None):
         n = self.num_envs
         if f64_planes is not None:
-            require_cuda(f64_planes, torch.float64, (SATENV_F64_PLANES, n), "f64_planes")
+            self._req(f64_planes, torch.float64, (SATENV_F64_PLANES, n), "f64_planes")
         if i32_planes is not None:
-            require_cuda(i32_planes, torch.int32, (SATENV_I32_PLANES, n), "i32_planes")
-        check(_lib.lib().satenv_set_state(self._h, ptr(f64_planes), ptr(i32_planes), stream_ptr()),
-              "satenv_set_state")
+            self._req(i32_planes, torch.int32, (SATENV_I32_PLANES, n), "i32_planes")
+        check(self._fn("set_state")(self._h, ptr(f64_planes), ptr(i32_planes), self._sp()), self._api + "set_state")
 
     def check_errors(self) -> int:
         st = C.c_int32(0)
-        check(_lib.lib().satenv_check(self._h, C.byref(st)), "satenv_check")
+        check(self._fn("check")(self._h, C.byref(st)), self._api + "check")
         return st.value
 
     def close(self):
         if getattr(self, "_h", None):
-            _lib.lib().satenv_destroy(self._h)
+            self._fn("destroy")(self._h)
             self._h = None
 
     def __del__(self):
@@ -371,7 +392,7 @@ class satellites:  # noqa: N801  (reference class name)
         self._cnt.fill_(int(epsiode_count))
         self._v.step(self._pa, self._ea, self._cnt, obs_out=None, obs64_out=self._obs, reward_out=self._r,
                      done_out=self._d)
-        obs = self._obs[0].cpu().numpy()
+        obs = self._obs[0].cpu().numpy().copy()      # a fresh array per step (on device="cpu" .cpu() aliases)
         r = float(self._r.item())
         done = bool(self._d.item())
         if done:

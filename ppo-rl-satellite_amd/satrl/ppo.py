@@ -561,7 +561,10 @@ class PPOLearner:
         self.sync_w2t()
         st = self.stepper(min(self.mini_batch_size, B))
         for ep in range(self.K_epochs):
-            perm = perms[ep] if perms is not None else torch.randperm(B, device=self.device, generator=generator)
+            if perms is None:
+                perm = torch.randperm(B, device=self.device, generator=generator)
+            else:
+                perm = perms(ep) if callable(perms) else perms[ep]     # a callable draws each epoch's order lazily
             st.run(src, perm)
         if self.use_lr_decay:
             self.lr_decay(total_steps)
@@ -579,6 +582,82 @@ class PPOLearner:
         return out
 
 
+class HostLearner:
+    """The N = 1 drop-in's agent on host cores (device="cpu"; BASELINE.json
+    configs[0]: CPPO_main.py on CPU, no GPU).  The networks are the same
+    nn.Modules, stepped by torch's CPU autograd, clip_grad_norm_ and Adam in
+    the order of ppo_continuous.py:212-239 (actor step, then critic step, per
+    minibatch); the vectorised engine never uses it (its update is the HIP
+    minibatch step of PPOLearner)."""
+
+    def __init__(self, args, agent_idx):
+        self.device = torch.device("cpu")
+        self.actor = Actor_Gaussian(args, agent_idx)
+        self.critic = Critic(args, agent_idx)
+        self.lr_a, self.lr_c = args.lr_a, args.lr_c
+        self.max_train_steps = args.max_train_steps
+        self.K_epochs, self.epsilon, self.entropy_coef = args.K_epochs, args.epsilon, args.entropy_coef
+        self.use_grad_clip, self.use_lr_decay, self.use_adv_norm = (args.use_grad_clip, args.use_lr_decay,
+                                                                   args.use_adv_norm)
+        kw = {"eps": 1e-5} if args.set_adam_eps else {}                  # ppo_continuous.py:161-166
+        self.opts = (torch.optim.Adam(self.actor.parameters(), lr=self.lr_a, **kw),
+                     torch.optim.Adam(self.critic.parameters(), lr=self.lr_c, **kw))
+
+    def normalize_adv(self, adv):
+        return (adv - adv.mean()) / (adv.std() + 1e-5) if self.use_adv_norm else adv
+
+    def lr_decay(self, total_steps):
+        frac = min(max(float(total_steps) / self.max_train_steps, 0.0), 1.0)    # as PPOLearner.lr_decay
+        for opt, lr in zip(self.opts, (self.lr_a, self.lr_c)):
+            for g in opt.param_groups:
+                g["lr"] = lr * (1 - frac)
+
+    @property
+    def lr_now(self):
+        return tuple(opt.param_groups[0]["lr"] for opt in self.opts)
+
+    def _minibatch(self, rows):
+        # contiguous column blocks, as the reference's s[index], a[index] ... are
+        s, a, lp_old, adv, vt = (rows[:, lo:hi].contiguous() for lo, hi in ((0, 18), (18, 21), (21, 24), (24, 25),
+                                                                             (25, 26)))
+        dist = self.actor.get_dist(s)
+        ent = dist.entropy().sum(1, keepdim=True)
+        ratio = torch.exp(dist.log_prob(a).sum(1, keepdim=True) - lp_old.sum(1, keepdim=True))
+        loss = -torch.min(ratio * adv, torch.clamp(ratio, 1 - self.epsilon, 1 + self.epsilon) * adv)
+        losses = ((loss - self.entropy_coef * ent).mean(), lambda: F.mse_loss(vt, self.critic(s)))
+        for k, (net, opt) in enumerate(zip((self.actor, self.critic), self.opts)):
+            opt.zero_grad()
+            (losses[0] if k == 0 else losses[1]()).backward()
+            if self.use_grad_clip:
+                torch.nn.utils.clip_grad_norm_(net.parameters(), 0.5)
+            opt.step()
+
+    def update_packed(self, src, total_steps, perms):
+        """K epochs over the packed rows [B, 32] in the given minibatch orders."""
+        mb = self.mini_batch_size
+        for ep in range(self.K_epochs):
+            perm = perms[ep]
+            for k in range(0, perm.numel(), mb):
+                self._minibatch(src[perm[k:k + mb]])
+        if self.use_lr_decay:
+            self.lr_decay(total_steps)
+
+
+def _gae_host(r, vs, vs_, dw, done, gamma, lamda):
+    """ppo_continuous.py:198-208 on host arrays: f32 deltas, then the reverse
+    scan with numpy-scalar arithmetic (f32, python floats weak) as the
+    reference's loop runs it."""
+    deltas = (r + gamma * (1.0 - dw) * vs_ - vs).reshape(-1).numpy()
+    d = done.reshape(-1).numpy()
+    adv = np.empty_like(deltas)
+    g = 0
+    for t in range(len(deltas) - 1, -1, -1):
+        g = deltas[t] + gamma * lamda * g * (1.0 - d[t])
+        adv[t] = g
+    adv = torch.from_numpy(adv)
+    return adv, adv + vs.reshape(-1)
+
+
 class PPO_continuous:  # noqa: N801
     """Drop-in for ppo_continuous.PPO_continuous (ppo_continuous.py:136-258).
 
@@ -593,7 +672,12 @@ class PPO_continuous:  # noqa: N801
         if args.policy_dist != "Gaussian":
             raise NotImplementedError("only the Gaussian policy (CPPO_main.py:17 default) is on the hot path")
         self.policy_dist = args.policy_dist
-        self.L = PPOLearner(args, agent_idx, device=device, graph_group=4)
+        dev = device if device is not None else getattr(args, "device", None)
+        if dev is not None and torch.device(dev).type == "cpu":
+            self.L = HostLearner(args, agent_idx)          # device="cpu" only when asked (configs[0])
+            self.L.mini_batch_size = args.mini_batch_size
+        else:
+            self.L = PPOLearner(args, agent_idx, device=device, graph_group=4)
         self.actor, self.critic = self.L.actor, self.L.critic
         self.max_action = args.max_action
         self.batch_size = args.batch_size
@@ -629,8 +713,9 @@ class PPO_continuous:  # noqa: N801
         with torch.no_grad():
             vs = self.critic(s)
             vs_ = self.critic(s_)
-            adv, v_target = _gae_explicit(r.reshape(-1), vs.reshape(-1), vs_.reshape(-1), dw.reshape(-1),
-                                          done.reshape(-1), self.gamma, self.lamda)
+            gae_fn = _gae_host if isinstance(self.L, HostLearner) else _gae_explicit
+            adv, v_target = gae_fn(r.reshape(-1), vs.reshape(-1), vs_.reshape(-1), dw.reshape(-1),
+                                   done.reshape(-1), self.gamma, self.lamda)
             adv = adv.reshape(-1, 1)
             v_target = v_target.reshape(-1, 1)
             adv = self.L.normalize_adv(adv)

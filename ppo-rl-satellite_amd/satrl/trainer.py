@@ -36,7 +36,7 @@ class args_param:  # noqa: N801
                  use_lr_decay=True, use_grad_clip=True, use_orthogonal_init=True, set_adam_eps=True, use_tanh=True,
                  chkpt_dir="/mnt/datab/home/yuanwenzheng/PICTURE1",
                  num_envs=1, horizon=None, seed=0, rollout_graph_chunk=64, update_graph_group=64, device=None,
-                 surrogate=False):
+                 surrogate=False, dp_minibatch="global", minibatch_sampler=None):
         self.max_train_steps = max_train_steps
         self.evaluate_freq = evaluate_freq
         self.save_freq = save_freq
@@ -73,6 +73,20 @@ class args_param:  # noqa: N801
         # config 5: evaluate the ImprovedNN surrogate (bf16) on every env step into
         # VecTrainer.ellipse_params (environment.py:158); a path or state_dict loads weights
         self.surrogate = surrogate
+        # data parallelism: "global" -- mini_batch_size is the
+        # GLOBAL minibatch, each of W ranks steps mini_batch_size / W of its
+        # rows per Adam step (the reference's minibatch semantics,
+        # ppo_continuous.py:213); "per_gpu" -- every rank steps
+        # mini_batch_size local rows (global minibatch mini_batch_size * W).
+        self.dp_minibatch = dp_minibatch
+        # minibatch index sampler of the vectorised engine: "uniform" =
+        # BatchSampler(SubsetRandomSampler(range(B))) over the local table
+        # (the reference's distribution); "stratified" = every minibatch holds
+        # mini_batch_size / 8 rows of each of 8 fixed global env blocks, drawn
+        # by per-block generators, so W = 1, 2, 4, 8 ranks draw the same
+        # global minibatches (None: uniform on one process, stratified under
+        # "global" data parallelism)
+        self.minibatch_sampler = minibatch_sampler
         # set by the train_* functions from the env (CPPO_main.py:99-101)
         self.state_dim = 18
         self.action_dim = 3
@@ -180,6 +194,32 @@ def test_network(args, env, show_pictures=False, d_capture=0):
 # ---------------------------------------------------------------------------
 # vectorised engine
 # ---------------------------------------------------------------------------
+def stratified_epoch_perm(T, n_local, world, rank, global_mb, gens, strata=8, device=None):
+    """One epoch's minibatch order for rank `rank` of `world`.
+
+    The global table is [T, n_local * world] (row t * N_glob + global env),
+    cut into `strata` blocks of consecutive global envs; rank r owns blocks
+    [r * strata / world, (r + 1) * strata / world).  Block s draws its own
+    permutation of its T * N_glob / strata rows from gens[s]; global
+    minibatch k is the concatenation over blocks of their k-th chunk of
+    global_mb / strata rows (the tail: the leftover rows of every block).  A
+    rank returns its blocks' share in LOCAL rows (t * n_local + local env),
+    minibatch-major, so every rank steps global_mb / world rows of each
+    global minibatch and W = 1, 2, 4, 8 draw the same global minibatches."""
+    Ns = n_local * world // strata
+    Bs = T * Ns
+    c = global_mb // strata
+    nfull = Bs // c
+    full, tail = [], []
+    for s_ in range(rank * (strata // world), (rank + 1) * (strata // world)):
+        q = torch.randperm(Bs, device=device, generator=gens[s_])
+        t, e = q // Ns, q % Ns + (s_ * Ns - rank * n_local)
+        loc = t * n_local + e
+        full.append(loc[:nfull * c].view(nfull, c))
+        tail.append(loc[nfull * c:])
+    return torch.cat([torch.cat(full, 1).reshape(-1)] + tail)
+
+
 class VecTrainer:
     """N envs x horizon T per iteration on one GPU (one process per GPU)."""
 
@@ -203,6 +243,7 @@ class VecTrainer:
         self.learner = self.pursuer if self.flag == 0 else self.evader
         if pg is not None:
             self._broadcast_params()
+        self._setup_minibatches(args, pg)
         self.buf = RolloutBuffer(self.T, self.N, self.device)
         self.other_a = torch.zeros((self.N, 3), dtype=torch.float32, device=self.device)
         self.other_lp = torch.zeros((self.N, 3), dtype=torch.float32, device=self.device)
@@ -224,6 +265,51 @@ class VecTrainer:
             self.surrogate = Surrogate(device=self.device, seed=self.seed, state_dict=sd)
             self.ellipse_params = torch.zeros((self.N, 10), dtype=torch.float32, device=self.device)
         self.env.reset(self.flag, obs_out=self.buf.obs[0])
+
+    STRATA = 8
+
+    def _setup_minibatches(self, args, pg):
+        """Local minibatch size and index sampler (see args_param
+        dp_minibatch / minibatch_sampler)."""
+        W, r = _dist.world_size(pg), _dist.rank(pg)
+        mode = getattr(args, "dp_minibatch", "global")
+        if mode not in ("global", "per_gpu"):
+            raise ValueError("dp_minibatch must be 'global' or 'per_gpu'")
+        sampler = getattr(args, "minibatch_sampler", None)
+        if sampler is None:
+            sampler = "stratified" if (W > 1 and mode == "global") else "uniform"
+        if sampler not in ("uniform", "stratified"):
+            raise ValueError("minibatch_sampler must be 'uniform' or 'stratified'")
+        mb = int(args.mini_batch_size)
+        if W > 1 and mode == "global" and sampler != "stratified":
+            raise ValueError("global-minibatch data parallelism draws stratified minibatches")
+        self.world, self.rank = W, r
+        self.dp_minibatch, self.sampler = mode, sampler
+        self.global_minibatch = mb if mode == "global" else mb * W
+        self.mb_local = mb // W if mode == "global" else mb
+        if sampler == "stratified":
+            S = self.STRATA
+            if S % W or (self.N * W) % S or mb % S or (mode == "global" and mb % W):
+                raise ValueError(f"stratified minibatches need world size | {S}, {S} | num_envs*world and "
+                                 f"{S} | mini_batch_size (got W={W}, num_envs={self.N}, mb={mb})")
+            self.my_strata = list(range(r * (S // W), (r + 1) * (S // W)))
+            self.strata_gen = {}
+            for s_ in self.my_strata:                # the same stream for a block whatever rank owns it
+                g = torch.Generator(device=self.device)
+                g.manual_seed(self.seed * 1000003 + 7919 * (s_ + 1))
+                self.strata_gen[s_] = g
+        for L in (self.pursuer, self.evader):
+            L.mini_batch_size = self.mb_local
+
+    def epoch_perm(self):
+        """One epoch's minibatch order over the local packed table [T*N]
+        (row t*N + j), minibatch-major: the full minibatches of mb_local rows,
+        then the tail (BatchSampler drop_last=False)."""
+        B = self.T * self.N
+        if self.sampler == "uniform":
+            return torch.randperm(B, device=self.device, generator=self.gen)
+        return stratified_epoch_perm(self.T, self.N, self.world, self.rank, self.global_minibatch, self.strata_gen,
+                                     self.STRATA, self.device)
 
     def _broadcast_params(self):
         # the module parameters are views into each learner's flat P
@@ -319,7 +405,7 @@ class VecTrainer:
             buf.pack(adv_n)
 
     def update(self):
-        self.learner.update_packed(self.buf.packed, self.episodes, generator=self.gen)
+        self.learner.update_packed(self.buf.packed, self.episodes, perms=lambda ep: self.epoch_perm())
 
     def finish_iteration(self):
         # next rollout starts from the current observation

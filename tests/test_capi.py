@@ -20,6 +20,11 @@ def test_headers_declare_expected_entry_points():
             "satenv_get_state", "satenv_set_state", "satenv_last_error"} <= env
     assert {"satrl_gae", "satrl_gaussian_sample", "satrl_moments"} <= _declared("satrl_rollout.h")
     assert {"satrl_ppo_rowpass", "satrl_ppo_reduce", "satrl_ppo_adam", "satrl_ppo_layout"} <= _declared("satrl_ppo.h")
+    # the host build exports every env entry point of satenv.h it restates, same signature, satenv_cpu_ prefix
+    cpu = _declared("satenv_cpu.h")
+    assert {n.replace("satenv_", "satenv_cpu_", 1) for n in ("satenv_create", "satenv_destroy", "satenv_num_envs",
+            "satenv_set_params", "satenv_reset", "satenv_step", "satenv_step_autoreset", "satenv_get_state",
+            "satenv_set_state", "satenv_danger_zone", "satenv_check", "satenv_last_error")} == cpu
 
 
 def test_library_exports_every_declared_symbol():
@@ -27,7 +32,8 @@ def test_library_exports_every_declared_symbol():
     if not os.path.exists(L.LIB_PATH):
         L.build()
     lib = L.lib()          # loads with torch's HIP runtime; no device needed
-    declared = _declared("satenv.h") | _declared("satrl_rollout.h") | _declared("satrl_ppo.h")
+    declared = (_declared("satenv.h") | _declared("satenv_cpu.h") | _declared("satrl_rollout.h") |
+                _declared("satrl_ppo.h"))
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(L.exported_symbols()) == declared

@@ -81,3 +81,30 @@ def test_dist_single_process_is_local():
     g = torch.ones(3)
     assert D.average_(g, None) is g and torch.equal(g, torch.ones(3))
     assert D.rank(None) == 0 and D.world_size(None) == 1 and D.env_offset(None, 9) == 0
+
+
+def test_stratified_minibatches_are_sharding_invariant():
+    """satrl.trainer.stratified_epoch_perm: the global minibatches that W = 2,
+    4 and 8 ranks step (each rank mb/W of its own rows, mapped back to global
+    row ids) are exactly the W = 1 minibatches, in order, tail included."""
+    import torch
+    from satrl.trainer import stratified_epoch_perm
+    T, N, mb = 7, 64, 48          # 448 rows, 9 full minibatches of 48 + a 16-row tail
+    def gens():
+        return {s: torch.Generator().manual_seed(1000 + s) for s in range(8)}
+    ref = stratified_epoch_perm(T, N, 1, 0, mb, gens())
+    assert sorted(ref.tolist()) == list(range(T * N))
+    nfull = (T * N // 8) // (mb // 8)
+    for W in (2, 4, 8):
+        n = N // W
+        parts = []
+        for r in range(W):
+            loc = stratified_epoch_perm(T, n, W, r, mb, gens())
+            glob = (loc // n) * N + r * n + loc % n          # local row t*n + j -> global t*N + r*n + j
+            parts.append(glob)
+        m = mb // W
+        for k in range(nfull):
+            got = torch.cat([p[k * m:(k + 1) * m] for p in parts])
+            assert torch.equal(torch.sort(got).values, torch.sort(ref[k * mb:(k + 1) * mb]).values), (W, k)
+        got_tail = torch.cat([p[nfull * m:] for p in parts])
+        assert torch.equal(torch.sort(got_tail).values, torch.sort(ref[nfull * mb:]).values)

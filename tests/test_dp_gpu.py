@@ -182,3 +182,83 @@ def test_rccl_graphed_dp_update_world1():
     assert used, "the DP update did not run from a graph with the RCCL communicator"
     _, ps, ws = _graphed_update(None)
     assert (pd == ps).all() and (wd == ws).all()
+
+
+def _global_mb_args(num_envs, **kw):
+    sys.path.insert(0, PKG_DIR)
+    from satrl.trainer import args_param
+    return args_param(batch_size=num_envs * 24, mini_batch_size=256, hidden_width=64, K_epochs=2, num_envs=num_envs,
+                      horizon=24, max_episode_steps=10, seed=4, rollout_graph_chunk=8, update_graph_group=2,
+                      chkpt_dir="/tmp", **kw)
+
+
+def _global_mb_rank(rank, port, q):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        from satrl.trainer import VecTrainer
+        tr = VecTrainer(_global_mb_args(32), flag=0, d_capture=15000.0, pg=dist.group.WORLD, env_offset=rank * 32)
+        assert tr.mb_local == 128 and tr.global_minibatch == 256 and tr.sampler == "stratified"
+        tr.iteration()
+        torch.cuda.synchronize()
+        q.put((rank, tr.learner.P.cpu().numpy(), float(tr.learner.steps[0].item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_global_minibatch_dp_equals_one_process():
+    """dp_minibatch="global" (SURVEY.md §8e): 2 ranks x 32 envs, each stepping
+    mb/2 = 128 rows of every global minibatch of 256, over a whole iteration
+    (rollout, GAE, global advantage normalisation, 2 epochs x 6 minibatches)
+    == one process x 64 envs with the same stratified sampler and mb 256:
+    the same global minibatches, the same number of Adam steps, parameters
+    within the fused step's bar (the gradient sums and the advantage moments
+    add in another order)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_global_mb_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (P, st) for r, P, st in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert (res[0][0] == res[1][0]).all()
+    sys.path.insert(0, PKG_DIR)
+    from satrl.trainer import VecTrainer
+    tr = VecTrainer(_global_mb_args(64, minibatch_sampler="stratified"), flag=0, d_capture=15000.0)
+    assert tr.mb_local == 256
+    tr.iteration()
+    torch.cuda.synchronize()
+    P1, steps1 = tr.learner.P.cpu().numpy(), float(tr.learner.steps[0].item())
+    assert res[0][1] == steps1 == 2 * (64 * 24 // 256)
+    import numpy as np
+    diff = np.abs(res[0][0] - P1)
+    print(f"global-minibatch DP vs one process: max |param diff| {diff.max():.3e} after {steps1:.0f} Adam steps")
+    assert np.allclose(res[0][0], P1, rtol=1e-5, atol=2e-7 * steps1), diff.max()
+
+
+def test_per_gpu_minibatch_variant_and_labels():
+    """dp_minibatch="per_gpu" keeps the named variant: each rank steps the
+    full mini_batch_size (global minibatch mb * W).  Single-process default:
+    uniform sampler over the local table (the reference's distribution)."""
+    sys.path.insert(0, PKG_DIR)
+    from satrl.trainer import VecTrainer
+    tr = VecTrainer(_global_mb_args(64), flag=0, d_capture=15000.0)
+    assert tr.sampler == "uniform" and tr.mb_local == 256 and tr.global_minibatch == 256
+    tr = VecTrainer(_global_mb_args(64, dp_minibatch="per_gpu"), flag=0, d_capture=15000.0)
+    assert tr.mb_local == 256 and tr.global_minibatch == 256
+    perm = tr.epoch_perm()
+    assert torch.equal(torch.sort(perm).values, torch.arange(64 * 24, device=perm.device))
+    tr = VecTrainer(_global_mb_args(64, minibatch_sampler="stratified"), flag=0, d_capture=15000.0)
+    perm = tr.epoch_perm()
+    assert torch.equal(torch.sort(perm).values, torch.arange(64 * 24, device=perm.device))
+    # every minibatch holds mb/8 rows of each 8-env block
+    blk = (perm % 64) // 8
+    for k in range(64 * 24 // 256):
+        assert torch.equal(torch.bincount(blk[k * 256:(k + 1) * 256], minlength=8),
+                           torch.full((8,), 32, device=perm.device))
