@@ -50,41 +50,93 @@ def parse():
                     help="init the nccl process group even at world size 1 (rehearses the DP update path)")
     ap.add_argument("--surrogate", action="store_true",
                     help="config 5: ImprovedNN surrogate (bf16) evaluated on every env step of the rollout")
+    ap.add_argument("--dp-minibatch", choices=("global", "per_gpu"), default="global",
+                    help="data parallelism: 'global' = --minibatch is the global minibatch, each of N ranks steps "
+                         "minibatch/N of its rows per Adam step (the reference's semantics, SURVEY 8e); 'per_gpu' = "
+                         "every rank steps --minibatch rows (global minibatch N x --minibatch)")
+    ap.add_argument("--profile-tag", default="r2", help="profiles/<tag>_* files the rocprof cross-check fields read")
     return ap.parse_args()
 
 
+def host_cores():
+    """Cores this process may use on the host: its CPU affinity, capped by a
+    cgroup CPU quota and by OMP_NUM_THREADS when set (the GPU box gives a
+    one-GPU job a 16-core share of a larger host).  Returns (cores, how)."""
+    n = len(os.sched_getaffinity(0))
+    how = [f"affinity {n}"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(per))))
+            how.append(f"cgroup quota {q}/{per}")
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+        how.append(f"OMP_NUM_THREADS {os.environ['OMP_NUM_THREADS']}")
+    return max(1, n), ", ".join(how)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def host_env_rate(n, steps, threads, seed=0):
+    """env-steps/s of the product's host build (satenv_cpu_step_autoreset,
+    OpenMP over envs) from reset, U(-1.6, 1.6) f32 actions, Flag 0,
+    d_capture 15000, max_episode_steps 1000."""
+    import torch
+    from satrl.env import VecSatellites
+    env = VecSatellites(n, device="cpu", d_capture=15000.0, max_episode_steps=1000, threads=threads)
+    env.reset(0)
+    g = np.random.default_rng(seed)
+    acts = torch.from_numpy(g.uniform(-1.6, 1.6, (min(steps, 64), 2, n, 3)).astype(np.float32))
+    obs = torch.empty((n, 18), dtype=torch.float32)
+    rew = torch.empty(n, dtype=torch.float32)
+    dn = torch.empty(n, dtype=torch.uint8)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step_autoreset(acts[k % len(acts), 0], acts[k % len(acts), 1], obs, rew, dn)
+    return n * steps / (time.perf_counter() - t0)
+
+
 def cpu_baseline(seconds, n, T, H, mb, epochs):
-    """The same PPO iteration on host cores, from bounded samples of each
-    part, scaled to one iteration (N envs x T steps, K epochs of mb-row
+    """The same PPO iteration on host cores, scaled from bounded samples of
+    each part to one iteration (N envs x T steps, K epochs of mb-row
     minibatches) -> whole-iteration env-steps/s, the unit of ``value``:
-      env step   oracle/satenv_oracle.c (the C restatement), n envs from the
-                 reference reset state with autoreset (Flag 0, U(-1.6,1.6)
-                 f32 actions), chunks of 64 steps until ~`seconds`, OpenMP
-                 over envs;
+      env step   the product's host build (satenv_cpu_*: the kernels' FP64
+                 step source through g++, bit-identical to the glibc
+                 reference and to oracle/satenv_oracle.c), n envs from reset
+                 with autoreset, U(-1.6,1.6) f32 actions, OpenMP over envs,
+                 chunks of 64 steps until ~`seconds`;
       policy     both agents' choose_action on n states and the critic values
                  (oracle/ppo_cpu.py, torch-CPU f32 as ppo_continuous.py);
       GAE        the reference's python reverse loop (oracle.gae_flat) on 2
-                 envs x T, scaled to n envs and divided by the thread count
-                 (envs are independent: perfect parallel assumed);
+                 envs x T, scaled to n envs and divided by the thread count;
       update     oracle/ppo_cpu.py minibatch steps (mb rows, H hidden),
-                 x (n*T/mb)*epochs."""
-    import numpy as np
+                 x (n*T/mb)*epochs.
+    Threads: the host cores this job may use (host_cores()).  Plus the
+    SURVEY 8(d) env-only leg: 4096 envs x 100 steps on 1 thread and on all
+    of them."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import ppo_cpu
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, how = host_cores()
+    steps, t_env = 0, 0.0
     chunk = 64
-    rng = np.random.default_rng(0)
-    pa = rng.uniform(-1.6, 1.6, (chunk, n, 3)).astype(np.float32)
-    ea = rng.uniform(-1.6, 1.6, (chunk, n, 3)).astype(np.float32)
-    ro = O.Rollout(n, d_capture=15000.0, max_episode_steps=1000)
-    steps, dt = 0, 0.0
-    while dt < seconds and steps < 256 * chunk:
-        t0 = time.perf_counter()
-        ro.run(pa, ea, nthreads=threads)
-        dt += time.perf_counter() - t0
+    while t_env < seconds and steps < 256 * chunk:
+        rate = host_env_rate(n, chunk, threads, seed=steps)
+        t_env += n * chunk / rate
         steps += chunk
-    t_env = dt / steps
+    t_env_step = t_env / steps
+    env_only_1 = host_env_rate(4096, 100, 1)
+    env_only_all = host_env_rate(4096, 100, threads)
     t_pol, t_val, t_mb = ppo_cpu.time_learning_side(n, H, mb, threads)
     g = np.random.default_rng(1)
     r = g.standard_normal(T).astype(np.float32)
@@ -94,28 +146,25 @@ def cpu_baseline(seconds, n, T, H, mb, epochs):
     for _ in range(2):
         O.gae_flat(r, vs, vs, dn, dn)
     t_gae_env = (time.perf_counter() - t0) / 2
-    t_iter = (T * (t_env + t_pol) + (T + 1) * t_val + n * t_gae_env / threads
+    t_iter = (T * (t_env_step + t_pol) + (T + 1) * t_val + n * t_gae_env / threads
               + epochs * (n * T // mb) * t_mb)
-    model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    total = os.cpu_count() or threads
     return {"value": n * T / t_iter, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"one PPO iteration ({n} envs x {T} steps, H {H}, {epochs} epochs x mb {mb}) on "
-                      f"{threads} threads of '{model}' (os.cpu_count()={os.cpu_count()}), scaled from samples: "
-                      f"env step = oracle C restatement, {n} envs x {steps} steps with autoreset (Flag 0, "
-                      f"U(-1.6,1.6) actions, d_capture 15000, max_episode_steps 1000); policy/values/update = "
-                      f"oracle/ppo_cpu.py torch-CPU f32 (8 policy steps, 2 value passes, 24 minibatches); GAE = "
-                      f"the reference's python loop on 2 envs x {T}",
+            "cpu_model": cpu_model(), "host_threads_total": total, "cores_how": how,
+            "sample": f"one PPO iteration ({n} envs x {T} steps, H {H}, {epochs} epochs x mb {mb}) on {threads} "
+                      f"threads of '{cpu_model()}' ({how}; the host has {total} hardware threads), scaled from "
+                      f"samples: env step = the product's host build satenv_cpu_step_autoreset, {n} envs x {steps} "
+                      f"steps from reset (Flag 0, U(-1.6,1.6) actions, d_capture 15000, max_episode_steps 1000); "
+                      f"policy/values/update = oracle/ppo_cpu.py torch-CPU f32 (8 policy steps, 2 value passes, "
+                      f"24 minibatches); GAE = the reference's python loop on 2 envs x {T}",
             "iteration_s": t_iter,
-            "env_step_only_env_steps_per_s": n / t_env,
-            "s_per_env_step_batch": t_env, "s_per_policy_step_both_agents": t_pol,
+            "env_step_only_env_steps_per_s": n / t_env_step,
+            "env_only_4096x100": {"threads_1": env_only_1, f"threads_{threads}": env_only_all,
+                                  "per_core": env_only_all / threads,
+                                  "all_host_threads_linear_extrapolation": env_only_all / threads * total},
+            "s_per_env_step_batch": t_env_step, "s_per_policy_step_both_agents": t_pol,
             "s_per_value_pass": t_val, "s_per_update_minibatch": t_mb, "s_gae_per_env_python": t_gae_env,
-            "seconds": dt}
+            "seconds": t_env}
 
 
 def rd_cpu_baseline():
@@ -137,19 +186,21 @@ def rd_cpu_baseline():
 
 
 def workload_name(a, world):
-    """Which BASELINE.json config this run is (configs[1..3]), or a plain description."""
+    """Which BASELINE.json config this run is (configs[1..4]), or a plain description."""
+    gmb = a.minibatch if (world == 1 or a.dp_minibatch == "global") else a.minibatch * world
     desc = (f"num_envs={a.num_envs}/GPU x {world} GPU, hidden={a.hidden}, horizon={a.horizon}, GAE lambda=0.95, "
-            f"minibatch={a.minibatch}, {a.epochs} PPO epochs")
+            f"global minibatch={gmb} ({gmb // world if world > 1 else gmb} rows per GPU per Adam step), "
+            f"{a.epochs} PPO epochs")
     if a.surrogate:
         desc += ", ImprovedNN surrogate bf16 per env-step"
-    if a.horizon == 2048 and a.minibatch == 4096 and a.epochs == 10:
+    if a.horizon == 2048 and gmb == 4096 and a.epochs == 10:
         if world == 1 and a.num_envs == 16384 and a.hidden == 256 and a.surrogate:
             return "BASELINE.json configs[4]: " + desc
         if world == 1 and a.num_envs == 16384 and a.hidden == 256:
             return "BASELINE.json configs[2]: " + desc
         if world == 1 and a.num_envs == 4096 and a.hidden == 64:
             return "BASELINE.json configs[1]: " + desc
-        if world == 8 and a.num_envs == 8192:
+        if world == 8 and a.num_envs == 8192 and a.hidden == 256:
             return "BASELINE.json configs[3]: " + desc
     return desc
 
@@ -176,7 +227,7 @@ def main():
     args = args_param(batch_size=a.num_envs * a.horizon, mini_batch_size=a.minibatch, hidden_width=a.hidden,
                       K_epochs=a.epochs, max_episode_steps=1000, num_envs=a.num_envs, horizon=a.horizon, seed=0,
                       max_train_steps=int(3e6), chkpt_dir="/tmp", surrogate=a.surrogate,
-                      update_graph_group=a.graph_group)
+                      update_graph_group=a.graph_group, dp_minibatch=a.dp_minibatch)
     tr = VecTrainer(args, flag=0, d_capture=a.d_capture, pg=pg, env_offset=rank * a.num_envs)
 
     def barrier():
@@ -205,67 +256,106 @@ def main():
     env_steps = n_total * a.horizon * a.steps
     value = env_steps / elapsed
 
-    # ---- roofline of the dominant kernel (satrl_ppo_rowpass, ~60% of the update):
-    # HIP events around back-to-back launches on the stream it is launched on
-    # (torch's current stream, see satrl._lib.stream_ptr), same inputs as the update.
+    # ---- roofline of the dominant kernel (satrl_ppo_rowpass, ~55% of the update).
+    # Live, in the update's own conditions: eager minibatch steps (rowpass ->
+    # dW2 -> reduce -> Adam, each step's Adam rewriting the weights the next
+    # rowpass streams) with HIP events recorded on the launch stream around
+    # every rowpass; a GPU-side spin queued first lets the host enqueue the
+    # whole run ahead of the GPU, so the kernels run back to back as in the
+    # update's graphs.  (This continues training; it is after the timed region.)
     L = tr.learner
-    st = L.stepper(a.minibatch)
+    mb_local = tr.mb_local
+    st = L.stepper(mb_local)
     src = tr.buf.packed
     g = torch.Generator(device="cuda").manual_seed(1)
-    idx = torch.randperm(src.shape[0], device="cuda", generator=g)[:a.minibatch].contiguous()
-    for _ in range(10):
-        st.rowpass(src, idx)
+    stage = src[torch.randperm(src.shape[0], device="cuda", generator=g)[:mb_local]].contiguous()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    spin = torch.empty(1 << 28, dtype=torch.float32, device="cuda")   # fallback backlog: 1 GiB of fills
+    try:
+        e0.record()
+        torch.cuda._sleep(10 ** 7)
+        e1.record()
+        torch.cuda.synchronize()
+        sleep_cycles_per_ms = 10 ** 7 / e0.elapsed_time(e1)
+    except (RuntimeError, AttributeError):
+        sleep_cycles_per_ms = None
+
+    def backlog(ms):
+        if sleep_cycles_per_ms:
+            torch.cuda._sleep(int(ms * sleep_cycles_per_ms))
+        else:
+            for _ in range(int(ms / 0.2) + 1):
+                spin.fill_(1.0)
+
+    def timed_pairs(n, fn, ahead_ms):
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for k in range(10):
+            fn(k, None)
+        torch.cuda.synchronize()
+        backlog(ahead_ms)
+        for k in range(n):
+            fn(k, evs[k])
+        torch.cuda.synchronize()
+        ts = sorted(x.elapsed_time(y) * 1e3 for x, y in evs)
+        return sum(ts) / n, ts[n // 2]
+
+    rowpass_us, rowpass_med = timed_pairs(a.kernel_iters, lambda k, ev: st.step(stage, None, events=ev), 60.0)
+    rowpass_flop = st.rowpass_flops(a.hidden, mb_local)
+    rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
+    # warm-L2 figure: back-to-back rowpass launches alone (W2/W2T stay in L2)
+    for _ in range(10):
+        st.rowpass(stage, None)
     e0.record()
     for _ in range(a.kernel_iters):
-        st.rowpass(src, idx)
+        st.rowpass(stage, None)
     e1.record()
     torch.cuda.synchronize()
-    rowpass_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
-    rowpass_flop = st.rowpass_flops(a.hidden, a.minibatch)
-    rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
-    # the same kernel's average inside the update's graphs (after each step's
-    # Adam rewrote W2/W2T, so the weights come from MALL, not a warm L2), from
-    # the committed rocprofv3 kernel stats of this command
-    in_update_us = None
-    ks_file = os.path.join(ROOT, "profiles", "r1_bench_kernel_stats.csv")
-    if os.path.exists(ks_file):
+    b2b_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+    # rocprof cross-checks from the committed profiles of this command / the PMC workloads
+    def prof_avg_us(kname):
+        ks_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_bench_kernel_stats.csv")
+        if not os.path.exists(ks_file):
+            return None
         import csv
         with open(ks_file) as f:
             for r in csv.DictReader(f):
-                if "rowpass_kernel<%d" % a.hidden in r["name"].replace(" ", ""):
-                    in_update_us = float(r["avg_ns"]) / 1e3
-    traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", "r1_rowpass_pmc.json")
-    if os.path.exists(pmc_file):
-        with open(pmc_file) as f:
-            pmc = json.load(f)
-        if pmc.get("hidden") == a.hidden and pmc.get("minibatch") == a.minibatch:
-            traffic = pmc["hbm_bytes_per_launch"]
+                if kname in r["name"].replace(" ", ""):
+                    return float(r["avg_ns"]) / 1e3
+        return None
 
-    # ---- env kernel (FP64 step, autoreset): HIP events around eager launches on its stream
+    def pmc(kind, **match):
+        pmc_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_{kind}_pmc.json")
+        if os.path.exists(pmc_file):
+            with open(pmc_file) as f:
+                d = json.load(f)
+            if all(d.get(k) == v for k, v in match.items()):
+                return d["hbm_bytes_per_launch"]
+        return None
+
+    rowpass_prof_us = prof_avg_us("rowpass_kernel<%d" % a.hidden)
+    traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
+
+    # ---- env kernel: in the rollout (live: eager rollout steps -- policy kernel,
+    # then the env step between HIP events -- after the timed region, the
+    # trainer's own envs and policy), and mid-episode under uniform actions
+    # (the sweep below)
+    t_roll = [0]
+
+    def roll_step(k, ev):
+        tr._policy_step(t_roll[0] % a.horizon, events=ev)
+        t_roll[0] += 1
+
+    env_us, env_med = timed_pairs(a.kernel_iters, roll_step, 40.0)
+    env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
+    env_prof_us = prof_avg_us("step_kernel_split<true>")
+    env_traffic = pmc("env", num_envs=a.num_envs)
     env = tr.env
     pa = tr.buf.act[0].clone()
     ea = torch.empty_like(pa).uniform_(-1.6, 1.6)
     obs = torch.empty((a.num_envs, 18), dtype=torch.float32, device="cuda")
     rew = torch.empty(a.num_envs, dtype=torch.float32, device="cuda")
     dn = torch.empty(a.num_envs, dtype=torch.uint8, device="cuda")
-    for _ in range(10):
-        env.step_autoreset(pa, ea, obs, rew, dn)
-    e0.record()
-    for _ in range(a.kernel_iters):
-        env.step_autoreset(pa, ea, obs, rew, dn)
-    e1.record()
-    torch.cuda.synchronize()
-    env_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
-    env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
-    env_traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", "r1_env_pmc.json")
-    if os.path.exists(pmc_file):
-        with open(pmc_file) as f:
-            pmc = json.load(f)
-        if pmc.get("num_envs") == a.num_envs:
-            env_traffic = pmc["hbm_bytes_per_launch"]
 
     # ---- north-star sweep: the env kernel alone at num_envs 4k / 16k / 64k on this GPU
     # (autoreset, U(-1.6,1.6) f32 actions cycled from 64 pre-drawn sets, 256 untimed
@@ -386,7 +476,7 @@ def main():
     flop_per_transition_epoch = 6 * (18 * H + H * H + 3 * H) + 6 * (18 * H + H * H + H)
     upd_flops = a.num_envs * a.horizon * a.epochs * flop_per_transition_epoch
     upd_tfs = upd_flops / (update_ms * 1e-3) / 1e12
-    n_minibatches = a.epochs * ((a.num_envs * a.horizon) // a.minibatch)
+    n_minibatches = a.epochs * ((a.num_envs * a.horizon) // tr.mb_local)
 
     if rank == 0:
         host_baseline = not a.no_cpu_baseline and world == 1          # rank 0 at N = 1 only
@@ -400,7 +490,9 @@ def main():
             "data": "synthetic: reference reset state, random-init (orthogonal, seed 0) policies",
             "config": {"workload": workload_name(a, world),
                        "num_envs_per_gpu": a.num_envs, "num_envs_total": n_total, "horizon": a.horizon,
-                       "hidden": a.hidden, "minibatch_per_gpu": a.minibatch, "epochs": a.epochs,
+                       "hidden": a.hidden, "minibatch_global": tr.global_minibatch,
+                       "minibatch_rows_per_gpu": tr.mb_local, "dp_minibatch": tr.dp_minibatch,
+                       "minibatch_sampler": tr.sampler, "epochs": a.epochs,
                        "d_capture": a.d_capture, "parallelism": f"dp{world}"},
             "ppo_updates_per_s": a.steps / elapsed,
             "rollout_env_steps_per_s": n_total * a.horizon / (rollout_ms * 1e-3),
@@ -413,23 +505,35 @@ def main():
                          "bound": "mfma",
                          "achieved": rowpass_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": rowpass_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
-                         "avg_launch_us": rowpass_us, "flop_per_launch": rowpass_flop,
-                         "in_update_avg_launch_us": in_update_us,
-                         "in_update_frac": (rowpass_flop / (in_update_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS
-                                            if in_update_us else None),
-                         "in_update_source": "profiles/r1_bench_kernel_stats.csv (rocprofv3 average over all "
-                                             "rowpass launches of this command, nearly all inside the update)",
-                         "traffic_source": "profiles/r1_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)",
+                         "avg_launch_us": rowpass_us, "median_launch_us": rowpass_med,
+                         "flop_per_launch": rowpass_flop, "rows_per_launch": mb_local,
+                         "timing": "live, HIP events on the launch stream around each of kernel_iters rowpass "
+                                   "launches inside eager minibatch steps (rowpass -> dW2 -> reduce -> Adam, the "
+                                   "update's conditions), queued behind a GPU spin so they run back to back",
+                         "rocprof_avg_launch_us": rowpass_prof_us,
+                         "rocprof_source": f"profiles/{a.profile_tag}_bench_kernel_stats.csv (rocprofv3 average over "
+                                           "all rowpass launches of this command, nearly all in the update's graphs)",
+                         "back_to_back_avg_launch_us": b2b_us,
+                         "back_to_back_frac": rowpass_flop / (b2b_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS,
+                         "traffic_source": f"profiles/{a.profile_tag}_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
+                                           "bytes/launch)",
                          "note": "f32 MFMA; one net per workgroup of 32 rows, each streams that net's fc2 weights "
                                  "from L2 per phase (DESIGN.md 3.4)"},
-            "roofline_env": {"kernel": "satenv step_kernel<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
+            "roofline_env": {"kernel": "satenv step_kernel_split<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
-                             "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
+                             "avg_launch_us": env_us, "median_launch_us": env_med,
+                             "bytes_per_env_step": ENV_BYTES_PER_STEP, "num_envs": a.num_envs,
+                             "timing": "in_rollout: live, HIP events around the env step of eager rollout steps "
+                                       "(policy kernel -> env step) on the trainer's envs and policy after the "
+                                       "timed region",
+                             "rocprof_avg_launch_us": env_prof_us,
+                             "rocprof_source": f"profiles/{a.profile_tag}_bench_kernel_stats.csv (all launches of "
+                                               "this command: rollout + sweep)",
                              "traffic": env_traffic,
-                             "traffic_source": "profiles/r1_env_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, bytes/launch, "
-                                               "16384 envs mid-episode)",
+                             "traffic_source": f"profiles/{a.profile_tag}_env_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
+                                               "bytes/launch, 16384 envs mid-episode, uniform actions)",
                              "note": "algorithmic bytes; the kernel is FP64 latency bound (DESIGN.md)",
-                             "sweep_num_envs": env_sweep},
+                             "sweep_mid_episode_uniform_actions": env_sweep},
             "roofline_update": {"bound": "mfma", "achieved": upd_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                                 "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
                                 "flop_per_transition_epoch": flop_per_transition_epoch},

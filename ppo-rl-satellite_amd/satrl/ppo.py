@@ -287,7 +287,9 @@ class FusedMinibatch:
         y = H1[lo * mb * H:hi * mb * H].view(nb * S, mb // S, H)
         torch.bmm(z.transpose(1, 2), y, out=self.p2[lo * S * H * H:hi * S * H * H].view(nb * S, H, H))
 
-    def _net_step(self, src, idx, mb, net):
+    def _net_step(self, src, idx, mb, net, events=None):
+        """One minibatch step of one chain; `events` (a pair of torch.cuda.Event,
+        bench only) are recorded around the rowpass launch."""
         L = self.L
         H = L.H
         S = self.S if mb == self.mb else self.splits(H, mb)
@@ -295,7 +297,11 @@ class FusedMinibatch:
             raise _lib.NativeError(f"dW2 split count {S} exceeds the slab capacity {self.max_splits(H)}")
         lib, sp = _lib.lib(), stream_ptr()
         nsq = self.nsq[max(net, 0)]
+        if events is not None:
+            events[0].record()
         H1, dZ2 = self.rowpass(src, idx, mb, net)
+        if events is not None:
+            events[1].record()
         self._dw2(H1, dZ2, mb, S, net)
         if L.pg is None:
             check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
@@ -327,8 +333,11 @@ class FusedMinibatch:
             fn(1)
         cur.wait_stream(self.side)
 
-    def step(self, src, idx, mb=None):
+    def step(self, src, idx, mb=None, events=None):
         mb = self.mb if mb is None else int(mb)
+        if events is not None:
+            self._net_step(src, idx, mb, -1, events)
+            return
         self._chains(lambda net: self._net_step(src, idx, mb, net))
 
     def _group(self, src, ng):

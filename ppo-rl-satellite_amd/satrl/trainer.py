@@ -318,8 +318,9 @@ class VecTrainer:
         self.evader.sync_w2t()
 
     # -- rollout ------------------------------------------------------------------
-    def _policy_step(self, t):
-        """One step of CPPO_main.py:121-147 for all envs (no host sync)."""
+    def _policy_step(self, t, events=None):
+        """One step of CPPO_main.py:121-147 for all envs (no host sync);
+        `events` (bench only): a pair of torch.cuda.Event around the env step."""
         buf = self.buf
         obs_t = buf.obs[t]
         if self.flag == 0:                       # pursuer transitions are stored (CPPO_main.py:141)
@@ -329,7 +330,11 @@ class VecTrainer:
         # both agents act on s (CPPO_main.py:122-123): one fused launch, pursuer = agent 0
         policy_act(self.pursuer.H, obs_t, self.pursuer.P, self.evader.P, 1.6, self.seed, self.env_offset, t,
                    pa, plp, ea, elp, step_base=self.step_base)
+        if events is not None:
+            events[0].record()
         self.env.step_autoreset(pa, ea, obs_out=buf.obs[t + 1], reward_out=buf.rew[t], done_out=buf.done[t])
+        if events is not None:
+            events[1].record()
         if self.surrogate is not None:            # env.ellipse_params of the state the policy sees next
             self.surrogate.env_forward(self.env, out=self.ellipse_params)
 

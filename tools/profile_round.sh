@@ -24,4 +24,6 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
 rm -f "$OUT/bench/run_kernel_trace.csv"
 python3 "$ROOT/tools/summarize_profiles.py" "$OUT" "$TAG" "$OUT/profiles"
+cp "$ROOT/profiles/${TAG}_rowpass_pmc.json" "$ROOT/profiles/${TAG}_env_pmc.json" "$OUT/profiles/" 2>/dev/null || true
+cp "$OUT/profiles/${TAG}_bench_kernel_stats.csv" "$ROOT/profiles/"
 tail -1 "$OUT/bench.json"
