@@ -300,7 +300,26 @@ def main():
         ts = sorted(x.elapsed_time(y) * 1e3 for x, y in evs)
         return sum(ts) / n, ts[n // 2]
 
-    rowpass_us, rowpass_med = timed_pairs(a.kernel_iters, lambda k, ev: st.step(stage, None, events=ev), 60.0)
+    def timed_run(n, fn, ahead_ms):
+        """Average time per call of n back-to-back calls (one event pair over the run)."""
+        for k in range(10):
+            fn(k)
+        torch.cuda.synchronize()
+        backlog(ahead_ms)
+        e0.record()
+        for k in range(n):
+            fn(k)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / n
+
+    # marginal cost of the rowpass on the minibatch chain (whole chain minus the
+    # chain without the rowpass), the headline; plus per-launch event brackets
+    # (each event marker adds its own fence to the stream, so they read high)
+    t_chain = timed_run(a.kernel_iters, lambda k: st.step(stage, None), 60.0)
+    t_rest = timed_run(a.kernel_iters, lambda k: st.step(stage, None, skip_rowpass=True), 40.0)
+    rowpass_us = t_chain - t_rest
+    rowpass_ev_us, rowpass_med = timed_pairs(a.kernel_iters, lambda k, ev: st.step(stage, None, events=ev), 60.0)
     rowpass_flop = st.rowpass_flops(a.hidden, mb_local)
     rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
     # warm-L2 figure: back-to-back rowpass launches alone (W2/W2T stay in L2)
@@ -346,7 +365,13 @@ def main():
         tr._policy_step(t_roll[0] % a.horizon, events=ev)
         t_roll[0] += 1
 
-    env_us, env_med = timed_pairs(a.kernel_iters, roll_step, 40.0)
+    def roll_policy_only(k):
+        tr._policy_step(t_roll[0] % a.horizon, env=False)
+        t_roll[0] += 1
+
+    env_us = (timed_run(a.kernel_iters, lambda k: roll_step(k, None), 40.0)
+              - timed_run(a.kernel_iters, roll_policy_only, 30.0))
+    env_ev_us, env_med = timed_pairs(a.kernel_iters, roll_step, 40.0)
     env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
     env_prof_us = prof_avg_us("step_kernel_split<true>")
     env_traffic = pmc("env", num_envs=a.num_envs)
@@ -505,11 +530,13 @@ def main():
                          "bound": "mfma",
                          "achieved": rowpass_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": rowpass_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
-                         "avg_launch_us": rowpass_us, "median_launch_us": rowpass_med,
-                         "flop_per_launch": rowpass_flop, "rows_per_launch": mb_local,
-                         "timing": "live, HIP events on the launch stream around each of kernel_iters rowpass "
-                                   "launches inside eager minibatch steps (rowpass -> dW2 -> reduce -> Adam, the "
-                                   "update's conditions), queued behind a GPU spin so they run back to back",
+                         "avg_launch_us": rowpass_us, "flop_per_launch": rowpass_flop, "rows_per_launch": mb_local,
+                         "timing": "live, HIP events on the launch stream: kernel_iters minibatch steps (rowpass -> "
+                                   "dW2 -> reduce -> Adam, each Adam rewriting the weights the next rowpass streams, "
+                                   "as in the update) minus the same steps without the rowpass, per launch; queued "
+                                   "behind a GPU spin so the kernels run back to back",
+                         "minibatch_step_us": t_chain,
+                         "event_bracketed_avg_launch_us": rowpass_ev_us, "event_bracketed_median_us": rowpass_med,
                          "rocprof_avg_launch_us": rowpass_prof_us,
                          "rocprof_source": f"profiles/{a.profile_tag}_bench_kernel_stats.csv (rocprofv3 average over "
                                            "all rowpass launches of this command, nearly all in the update's graphs)",
@@ -521,11 +548,12 @@ def main():
                                  "from L2 per phase (DESIGN.md 3.4)"},
             "roofline_env": {"kernel": "satenv step_kernel_split<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
-                             "avg_launch_us": env_us, "median_launch_us": env_med,
-                             "bytes_per_env_step": ENV_BYTES_PER_STEP, "num_envs": a.num_envs,
-                             "timing": "in_rollout: live, HIP events around the env step of eager rollout steps "
-                                       "(policy kernel -> env step) on the trainer's envs and policy after the "
-                                       "timed region",
+                             "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
+                             "num_envs": a.num_envs,
+                             "timing": "in_rollout: live, HIP events: kernel_iters eager rollout steps (policy kernel "
+                                       "-> env step) on the trainer's envs and policy after the timed region, minus "
+                                       "the same steps without the env step, per launch",
+                             "event_bracketed_avg_launch_us": env_ev_us, "event_bracketed_median_us": env_med,
                              "rocprof_avg_launch_us": env_prof_us,
                              "rocprof_source": f"profiles/{a.profile_tag}_bench_kernel_stats.csv (all launches of "
                                                "this command: rollout + sweep)",

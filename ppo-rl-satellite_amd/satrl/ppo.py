@@ -287,9 +287,10 @@ class FusedMinibatch:
         y = H1[lo * mb * H:hi * mb * H].view(nb * S, mb // S, H)
         torch.bmm(z.transpose(1, 2), y, out=self.p2[lo * S * H * H:hi * S * H * H].view(nb * S, H, H))
 
-    def _net_step(self, src, idx, mb, net, events=None):
-        """One minibatch step of one chain; `events` (a pair of torch.cuda.Event,
-        bench only) are recorded around the rowpass launch."""
+    def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False):
+        """One minibatch step of one chain.  Bench-only knobs: `events` (a pair
+        of torch.cuda.Event) recorded around the rowpass launch; skip_rowpass
+        runs the rest of the chain on the last H1/dZ2/slabs (timing only)."""
         L = self.L
         H = L.H
         S = self.S if mb == self.mb else self.splits(H, mb)
@@ -299,7 +300,11 @@ class FusedMinibatch:
         nsq = self.nsq[max(net, 0)]
         if events is not None:
             events[0].record()
-        H1, dZ2 = self.rowpass(src, idx, mb, net)
+        if skip_rowpass:
+            n = 2 * mb * H
+            H1, dZ2 = self.H1[:n], self.dZ2[:n]
+        else:
+            H1, dZ2 = self.rowpass(src, idx, mb, net)
         if events is not None:
             events[1].record()
         self._dw2(H1, dZ2, mb, S, net)
@@ -333,10 +338,10 @@ class FusedMinibatch:
             fn(1)
         cur.wait_stream(self.side)
 
-    def step(self, src, idx, mb=None, events=None):
+    def step(self, src, idx, mb=None, events=None, skip_rowpass=False):
         mb = self.mb if mb is None else int(mb)
-        if events is not None:
-            self._net_step(src, idx, mb, -1, events)
+        if events is not None or skip_rowpass:
+            self._net_step(src, idx, mb, -1, events, skip_rowpass)
             return
         self._chains(lambda net: self._net_step(src, idx, mb, net))
 

@@ -318,9 +318,10 @@ class VecTrainer:
         self.evader.sync_w2t()
 
     # -- rollout ------------------------------------------------------------------
-    def _policy_step(self, t, events=None):
-        """One step of CPPO_main.py:121-147 for all envs (no host sync);
-        `events` (bench only): a pair of torch.cuda.Event around the env step."""
+    def _policy_step(self, t, events=None, env=True):
+        """One step of CPPO_main.py:121-147 for all envs (no host sync).
+        Bench-only knobs: `events` (a pair of torch.cuda.Event) around the env
+        step; env=False skips the env step (timing only)."""
         buf = self.buf
         obs_t = buf.obs[t]
         if self.flag == 0:                       # pursuer transitions are stored (CPPO_main.py:141)
@@ -332,7 +333,8 @@ class VecTrainer:
                    pa, plp, ea, elp, step_base=self.step_base)
         if events is not None:
             events[0].record()
-        self.env.step_autoreset(pa, ea, obs_out=buf.obs[t + 1], reward_out=buf.rew[t], done_out=buf.done[t])
+        if env:
+            self.env.step_autoreset(pa, ea, obs_out=buf.obs[t + 1], reward_out=buf.rew[t], done_out=buf.done[t])
         if events is not None:
             events[1].record()
         if self.surrogate is not None:            # env.ellipse_params of the state the policy sees next
