@@ -54,20 +54,6 @@ int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
 int satrl_ppo_dw2_splits(int H, int mb);
 int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream);
 
-/* H = 256: dW2 = dZ2^T H1 per net (hand-written f32 MFMA, split-K 8, the
- * partial tiles folded in split order by each tile's last-arriving
- * workgroup) AND the W1 / tail slab sums of satrl_ppo_reduce, in one launch:
- * replaces satrl_ppo_dw2 (or the library GEMM) + satrl_ppo_reduce.  p2:
- * scratch [2][8][H][H]; tickets: 32 u32 per handle, zero-initialised once
- * and then only advanced by this call (8 per tile and launch); p1 / pt: the
- * rowpass slabs.  mode 1: G only; mode 3: G, the squared-norm partials nsq
- * in satrl_ppo_reduce's block layout (satrl_ppo_sizes n_norm_blocks
- * entries) and steps[net] += 1, so satrl_ppo_adam follows unchanged.
- * Deterministic: every sum has a fixed order.                            */
-int satrl_ppo_grad(int H, int mb, int net, int mode, const float* H1, const float* dZ2, float* p2,
-                   unsigned* tickets, const float* p1, const float* pt, float* G, double* nsq, double* steps,
-                   void* stream);
-
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
  * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and

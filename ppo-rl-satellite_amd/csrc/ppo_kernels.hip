@@ -962,7 +962,7 @@ __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
 // the W1 and tail parts of reduce (block b of the W1 region, or of the tail
 // after it: b counts from the first W1 block): sums the rowpass slabs into G
 // (mode & 1) or rescales G (world > 1), and adds this thread's squares to
-// (sa, sc).  Shared by reduce_kernel and grad_kernel.
+// (sa, sc).
 __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const RedGeom& g, int b, int mode,
                                                const float* __restrict__ p1, const float* __restrict__ pt,
                                                float4* __restrict__ G4, int world, float4* red, double& sa,
@@ -1047,170 +1047,6 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
       nsq[2 * blockIdx.x] = sa;
       nsq[2 * blockIdx.x + 1] = sc;
       if (blockIdx.x == 0) {
-        if (g.net != 1) steps[0] += 1.0;
-        if (g.net != 0) steps[1] += 1.0;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// grad (H = 256): the fc2 weight gradient dW2 = dZ2^T H1 per net and the
-// rest of reduce in ONE launch, no hipBLASLt call and no W2 slab round trip
-// through a second kernel.
-//   blocks [0, 32 S)   W2: 64x64 output tile T (of 2 nets x 16) x K split s
-//                      (b = s + S T: with round-robin dispatch and S = 8 every
-//                      block of split s is on one XCD, whose L2 then holds the
-//                      2 MB of H1/dZ2 rows the split reads).  4 waves, each a
-//                      32x32 tile on v_mfma_f32_32x32x2_f32 with both operands
-//                      loaded straight from global memory (a 2-row k step is
-//                      two 128-B row segments per operand), 16 k steps in
-//                      flight.  The partial goes out write-through (sc1); the
-//                      tile's last arriver (ticket) folds the S partials in
-//                      split order (sc1 loads), writes G and the tile's
-//                      squared norm.
-//   blocks [32 S, ...) the W1 / tail slab sums of reduce (reduce_w1_tail),
-//                      running beside the MFMA blocks.
-// nsq (mode 2): the reduce layout -- entries [0, nb2) for the W2 region (tile
-// T at T, zeros after), then reduce's W1 / tail blocks -- so satrl_ppo_adam
-// folds the same number of partials either way.
-// ---------------------------------------------------------------------------
-using f16v = __attribute__((ext_vector_type(16))) float;
-constexpr int kGradS = 8;      // K splits of the W2 product at H = 256
-constexpr int kGradU = 16;     // k steps (2 rows each) per load chunk
-
-__device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-template <bool RAGGED>
-__device__ __forceinline__ void grad_w2_block(int b, int mb, int KR, int net_sel, const float* __restrict__ H1g,
-                                              const float* __restrict__ dZ2g, float* __restrict__ p2,
-                                              unsigned* __restrict__ tickets, float* __restrict__ G,
-                                              double* __restrict__ nsq, int mode, int nb2, double* sh) {
-  constexpr int H = 256, TT = H / 64, S = kGradS, U = kGradU;
-  const int s = b % S, T = b / S;
-  const int net = net_sel < 0 ? T / (TT * TT) : net_sel;
-  const int tile = T % (TT * TT);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, half = l >> 5, col = l & 31;
-  const int nw = (tile / TT) * 64 + (w >> 1) * 32, mw = (tile % TT) * 64 + (w & 1) * 32;
-  const int r_begin = s * KR, r_end = min(mb, r_begin + KR);
-  const float* Z = dZ2g + (int64_t)net * mb * H + nw + col;       // A[n][k] = dZ2[row][n]
-  const float* Y = H1g + (int64_t)net * mb * H + mw + col;        // B[k][m] = H1[row][m]
-  const int nsteps = r_end > r_begin ? (r_end - r_begin + 1) >> 1 : 0;
-  const int nch = (nsteps + U - 1) / U;
-  f16v acc0 = {}, acc1 = {};
-  float a0[U], b0[U], a1[U], b1[U];
-  auto load = [&](int c, float (&a)[U], float (&y)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int row = r_begin + 2 * (c * U + u) + half;
-      if constexpr (RAGGED) {
-        const bool ok = row < r_end;
-        const int64_t rr = ok ? row : r_begin;
-        const float za = Z[rr * H], yb = Y[rr * H];
-        a[u] = ok ? za : 0.0f;
-        y[u] = ok ? yb : 0.0f;
-      } else {
-        a[u] = Z[(int64_t)row * H];
-        y[u] = Y[(int64_t)row * H];
-      }
-    }
-  };
-  auto mma = [&](const float (&a)[U], const float (&y)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; u += 2) {
-      acc0 = mfma32(a[u], y[u], acc0);
-      acc1 = mfma32(a[u + 1], y[u + 1], acc1);
-    }
-  };
-  if (nch > 0) load(0, a0, b0);
-  for (int c = 0; c < nch; c += 2) {
-    if (c + 1 < nch) load(c + 1, a1, b1);
-    mma(a0, b0);
-    if (c + 1 < nch) {
-      if (c + 2 < nch) load(c + 2, a0, b0);
-      mma(a1, b1);
-    }
-  }
-  f16v acc = acc0 + acc1;
-  // acc[i] = partial dW2[nw + 8(i/4) + 4 half + i%4][mw + col]
-  float* slab = p2 + ((int64_t)net * S + s) * H * H;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int n = nw + 8 * (i >> 2) + 4 * half + (i & 3);
-    __hip_atomic_store(slab + (int64_t)n * H + mw + col, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // publish: every wave's write-through stores drained, then ONE ticket per block
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned tk = __hip_atomic_fetch_add(tickets + net * TT * TT + tile, 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (int)(tk % S) == S - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // the tile's last arriver: sum the S partials in split order (own from registers)
-  const float* base = p2 + (int64_t)net * S * H * H;
-  double sq = 0.0;
-  float* Gw = G + (int64_t)net * H * H;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int n = nw + 8 * (i >> 2) + 4 * half + (i & 3);
-    const int64_t e = (int64_t)n * H + mw + col;
-    float part[S];
-#pragma unroll
-    for (int q = 0; q < S; ++q)
-      part[q] = q == s ? acc[i] : __hip_atomic_load(base + (int64_t)q * H * H + e, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-    float v = part[0];
-#pragma unroll
-    for (int q = 1; q < S; ++q) v += part[q];
-    if (mode & 1) Gw[e] = v;
-    sq += (double)v * v;
-  }
-  if (mode & 2) {
-    double sa = net == 0 ? sq : 0.0, sc = net == 0 ? 0.0 : sq;
-    block_sum2(sa, sc, sh);
-    if (threadIdx.x == 0) {
-      nsq[2 * T] = sa;
-      nsq[2 * T + 1] = sc;
-    }
-    // zero the W2 entries past the tiles (the reduce layout has nb2 of them)
-    const int ntile = (net_sel < 0 ? 2 : 1) * TT * TT, per = (nb2 - ntile + ntile - 1) / ntile;
-    for (int k = threadIdx.x; k < per; k += blockDim.x) {
-      const int e = ntile + T * per + k;
-      if (e < nb2) { nsq[2 * e] = 0.0; nsq[2 * e + 1] = 0.0; }
-    }
-  }
-}
-
-template <bool RAGGED>
-__global__ void __launch_bounds__(256) grad_kernel(int mb, int KR, int net_sel, RedGeom g, int mode, int nW2,
-                                                   const float* __restrict__ H1g, const float* __restrict__ dZ2g,
-                                                   float* __restrict__ p2, unsigned* __restrict__ tickets,
-                                                   const float* __restrict__ p1, const float* __restrict__ pt,
-                                                   float* __restrict__ G, double* __restrict__ nsq,
-                                                   double* __restrict__ steps) {
-  __shared__ double sh[8];
-  if ((int)blockIdx.x < nW2) {
-    grad_w2_block<RAGGED>(blockIdx.x, mb, KR, net_sel, H1g, dZ2g, p2, tickets, G, nsq, mode, g.nb2, sh);
-    return;
-  }
-  constexpr int H = 256;
-  const Layout L = layout(H);
-  __shared__ float4 red[256];
-  double sa = 0.0, sc = 0.0;
-  const int b = blockIdx.x - nW2;                                 // W1 / tail block (reduce numbering - nb2)
-  reduce_w1_tail(H, L, g, b, mode | 1, p1, pt, reinterpret_cast<float4*>(G), 1, red, sa, sc);
-  if (mode & 2) {
-    block_sum2(sa, sc, sh);
-    if (threadIdx.x == 0) {
-      nsq[2 * (g.nb2 + b)] = sa;
-      nsq[2 * (g.nb2 + b) + 1] = sc;
-      if (b == 0) {
         if (g.net != 1) steps[0] += 1.0;
         if (g.net != 0) steps[1] += 1.0;
       }
@@ -1462,31 +1298,6 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
     hipLaunchKernelGGL(dw2_kernel<128>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
   else
     hipLaunchKernelGGL(dw2_kernel<256>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
-  LAUNCH_CHECK();
-  return 0;
-}
-
-int satrl_ppo_grad(int H, int mb, int net, int mode, const float* H1, const float* dZ2, float* p2,
-                   unsigned* tickets, const float* p1, const float* pt, float* G, double* nsq, double* steps,
-                   void* stream) {
-  if (H != 256 || mb <= 0 || net < -1 || net > 1 || mode < 1 || mode > 3 || !H1 || !dZ2 || !p2 || !tickets ||
-      !p1 || !pt || !G)
-    return -1;
-  if ((mode & 2) && (!nsq || !steps)) return -1;
-  const RedGeom g = geom(H, mb, kGradS, net);
-  const int ntile = (net < 0 ? 2 : 1) * (H / 64) * (H / 64), nW2 = ntile * kGradS;
-  // rows per split: a whole number of 2-row k steps, a multiple of the load chunk when it divides evenly
-  int KR = (mb + kGradS - 1) / kGradS;
-  KR = (KR + 1) & ~1;
-  const bool full = (mb % (kGradS * 2 * kGradU) == 0);
-  const dim3 grid((unsigned)(nW2 + g.nb1 + g.nbt));
-  hipStream_t st = (hipStream_t)stream;
-  if (full)
-    hipLaunchKernelGGL(grad_kernel<false>, grid, dim3(256), 0, st, mb, mb / kGradS, net, g, mode, nW2, H1, dZ2, p2,
-                       tickets, p1, pt, G, nsq, steps);
-  else
-    hipLaunchKernelGGL(grad_kernel<true>, grid, dim3(256), 0, st, mb, KR, net, g, mode, nW2, H1, dZ2, p2, tickets,
-                       p1, pt, G, nsq, steps);
   LAUNCH_CHECK();
   return 0;
 }

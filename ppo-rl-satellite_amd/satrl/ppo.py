@@ -201,12 +201,6 @@ class FusedMinibatch:
         self.lib_gemm = learner.H >= 256
         if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob
             self.lib_gemm = os.environ["SATRL_DW2_LIB"] == "1"
-        # H = 256: satrl_ppo_grad -- the hand-written dW2 (split-K 8, folded in
-        # the same launch by each tile's last workgroup) and reduce's W1/tail
-        # sums in ONE launch, replacing the library GEMM + reduce pair
-        self.fused_grad = learner.H == 256 and os.environ.get("SATRL_GRAD", "1") == "1"
-        if self.fused_grad:
-            self.lib_gemm = False
         self.S = self.splits(learner.H, self.mb)
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
@@ -225,8 +219,6 @@ class FusedMinibatch:
         # S exceeds the full minibatch's never writes past the slabs
         self.p2 = torch.empty(2 * self.max_splits(H) * H * H, **f32)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
-        # per-tile arrival tickets of satrl_ppo_grad (monotonic: S per launch)
-        self.tickets = torch.zeros(64, dtype=torch.int32, device=dev)
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
         # group (one index_select) so rowpass reads them without an index hop
@@ -266,16 +258,12 @@ class FusedMinibatch:
 
     def max_splits(self, H):
         """Upper bound of splits(H, mb) over every mb (the p2 capacity)."""
-        if self.fused_grad:
-            return 8
         if self.lib_gemm:
             return max(self.S, 4)
         return max(self.S, 256 // (2 * (H // 64) ** 2))
 
     def splits(self, H, mb):
         """split-K ways of the dW2 product for a minibatch of mb rows."""
-        if self.fused_grad:
-            return 8
         if self.lib_gemm:
             S = int(os.environ.get("SATRL_DW2_SPLITS", "4"))          # dev A/B knob; 4 measured best
             return S if mb % S == 0 else 1
@@ -319,20 +307,7 @@ class FusedMinibatch:
             H1, dZ2 = self.rowpass(src, idx, mb, net)
         if events is not None:
             events[1].record()
-        if self.fused_grad:
-            single = L.pg is None
-            check(lib.satrl_ppo_grad(H, mb, net, 3 if single else 1, ptr(H1), ptr(dZ2), ptr(self.p2),
-                                     ptr(self.tickets), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
-                                     ptr(nsq) if single else None, ptr(L.steps) if single else None, sp),
-                  "satrl_ppo_grad")
-            if not single:
-                if L.comm is not None:
-                    L.comm.all_reduce_sum_(L.G)
-                else:
-                    _dist.sum_inplace_(L.G, L.pg)
-                check(lib.satrl_ppo_reduce_dp(H, mb, net, _dist.world_size(L.pg), ptr(L.G), ptr(nsq), ptr(L.steps),
-                                              sp), "satrl_ppo_reduce_dp")
-        elif L.pg is None:
+        if L.pg is None:
             self._dw2(H1, dZ2, mb, S, net)
             check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
