@@ -81,7 +81,7 @@ __device__ __forceinline__ void block_sum(Smem& sm, double (&v)[K]) {
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < K; ++k) v[k] = ((sm.red[0][k] + sm.red[1][k]) + sm.red[2][k]) + sm.red[3][k];
-  __syncthreads();
+  __syncthreads();   // LDS-scalar invariant: every wave has read red[] before the next call rewrites it
 }
 
 // Mahalanobis distance of (x, y) to loc under the 2x2 precision P = [[p00, p01], [p01, p11]]
@@ -97,6 +97,8 @@ __device__ double select_kth(Smem& sm, int n, int k, double lx, double ly, doubl
   for (int shift = 56; shift >= 0; shift -= 8) {
     for (int b = threadIdx.x; b < 256; b += kThreads) sm.hist[b] = 0;
     __syncthreads();
+    // invariant: prefix/mask go to registers here, before the barrier that
+    // precedes thread 0's rewrite of them at the end of this pass
     const unsigned long long pre = sm.sel_prefix, msk = sm.sel_mask;
     for (int i = threadIdx.x; i < n; i += kThreads) {
       const double2 q = sm.pts[i];
@@ -446,7 +448,8 @@ __global__ void __launch_bounds__(kThreads) ellipse_kernel(int32_t ndir, const d
   double* o = out + 5 * blockIdx.x;
   const int tid = threadIdx.x;
 
-  // A: gather
+  // A: gather (LDS-scalar invariant: cnt / flag are written only here, before
+  // the barrier below, and are read-only for the rest of the block)
   if (tid == 0) { sm.cnt = 0; sm.flag = 0; }
   __syncthreads();
   for (int d = tid; d < ndir; d += kThreads) {
@@ -573,7 +576,7 @@ __global__ void __launch_bounds__(kThreads) ellipse_kernel(int32_t ndir, const d
       sm.fit[rank] = sm.pts[sm.pick[tid]];
     }
   }
-  if (tid == 0) {
+  if (tid == 0) {   // (invariant: m is written once, read after the barrier, never rewritten)
     int m = 0;
     for (int b = 0; b < kBins; ++b) m += sm.first[b] != INT32_MAX;
     sm.m = m;
