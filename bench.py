@@ -451,6 +451,18 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     env_rk_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+    # propagator 2: solve_ivp RK45 on the CW orbit_ode (satellite_function.py:783-839)
+    env_rk.set_params(propagator=2)
+    env_rk.reset(0)
+    for _ in range(10):
+        env_rk.step_autoreset(pa, ea, obs, rew, dn)
+    e0.record()
+    for _ in range(a.kernel_iters):
+        env_rk.step_autoreset(pa, ea, obs, rew, dn)
+    e1.record()
+    torch.cuda.synchronize()
+    env_rk45_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+    del env_rk
 
     # ---- §8f rank 4: reachable-domain grid (RD_single_pulse.py:40-148), the reference's
     # default 1 x 201 x 201 direction grid for a batch of orbits in one launch
@@ -568,7 +580,11 @@ def main():
             "propagators": {"rk4_j2_state_steps_per_s": a.num_envs * rk_steps / (rk4_ms * 1e-3),
                             "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
                             "env_rk4_cw_avg_launch_us": env_rk_us,
-                            "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6)},
+                            "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6),
+                            "env_rk45_cw_avg_launch_us": env_rk45_us,
+                            "env_rk45_cw_env_steps_per_s": a.num_envs / (env_rk45_us * 1e-6),
+                            "note": "rk4_cw: propagator 1 (RK4, 10 substeps); rk45_cw: propagator 2, the "
+                                    "reference's solve_ivp RK45 on orbit_ode (satellite_function.py:783-839)"},
             "surrogate": {"kernel": "satenv_surrogate (ImprovedNN 5-256-128-64-10, bf16 MFMA 16x16x32, f32 acc)",
                           "in_rollout": bool(a.surrogate), "avg_launch_us": sur_us,
                           "env_steps_per_s": a.num_envs / (sur_us * 1e-6), "bound": "mfma",

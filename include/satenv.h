@@ -6,7 +6,7 @@
  * (qiaobeibei/PPO-RL-Satellite environment.py):
  *   satenv_create / satenv_set_params  <- satellites.__init__   environment.py:26-62
  *   satenv_reset                       <- satellites.reset      environment.py:66-79
- *   satenv_step                        <- satellites.step       environment.py:81-255 (Flag 0, 1)
+ *   satenv_step                        <- satellites.step       environment.py:81-315 (Flag 0, 1, 2)
  *   satenv_step_autoreset              <- the CPPO_main.py:119-153 inner loop around step/reset
  *   satenv_get_state / satenv_set_state<- attribute access (Pursuer_position, fuel_c, dis, ...)
  *   satenv_default_params / satenv_stm <- ctor defaults + Clohessy_Wiltshire.State_transition_matrix
@@ -40,11 +40,14 @@ enum {
     SATENV_ERR_HIP = -2,
     SATENV_ERR_ORBIT_CIRCULAR = -4,  /* calculate_orbital_elements e == 0 (satellite_function.py:251) */
     SATENV_ERR_ORBIT_PARABOLIC = -5, /* 2/r - v^2/mu == 0 (satellite_function.py:253) */
+    SATENV_ERR_STEP_TOO_SMALL = -6,  /* propagator 2: solve_ivp's RK45 stopped (TOO_SMALL_STEP) */
 };
 
 /* numpy scalar type carried by the reference's fuel attributes; bits plane:
  * [1:0] fuel_c type, [3:2] fuel_t type, [4] velocities are int64 (fresh
- * after reset), [5] Flag (0 pursuer training, 1 evader training).        */
+ * after reset), [6:5] Flag (0 pursuer training, 1 evader training, 2
+ * reachable-domain fitting: environment.py:257-315, no danger-zone update,
+ * reward 0; its ellipse fit is satenv_rd_orbits + the grid/fit kernels). */
 enum { SATENV_NUM_PYINT = 0, SATENV_NUM_I64 = 1, SATENV_NUM_F32 = 2, SATENV_NUM_F64 = 3 };
 
 typedef struct satenv_params {
@@ -65,7 +68,12 @@ typedef struct satenv_params {
      * reference's closed-form CW STM (stm[], default); 1 = RK4 on the CW ODE
      * x'' = 2w y' + 3w^2 x, y'' = -2w x', z'' = -w^2 z with rk4_substeps
      * equal steps (optional mode; the reference STM's [1][4] entry is
-     * 4s/w - 3*tau, so the two differ by design).          */
+     * 4s/w - 3*tau, so the two differ by design).
+     * 2 = satellite_function.py:783-839 Numerical_calculation_method: the
+     * CW orbit_ode with omega from r = 35786 km (9.33e-5 rad/s), scipy
+     * solve_ivp RK45 (rtol 1e-3, atol 1e-6, adaptive steps) over the 100-s
+     * step, dense output at t (the reference's commented-out alternative,
+     * environment.py:124-128; cw_omega/rk4_substeps unused).              */
     double cw_omega;           /* w = sqrt(mu / 42164000**3), satellite_function.py:761 */
     int32_t propagator;
     int32_t rk4_substeps;
@@ -158,9 +166,23 @@ typedef struct {
     double f;          /* params['f'], true anomaly of the burn     */
     double delta_max;  /* params['delta_max'], max impulse [m/s]    */
     double mu;         /* params['u'] = 3.986e14                    */
+    double dv_f32;     /* non-zero: params['delta_max'] is an np.float32 scalar (a
+                        * Flag-2 env's fuel_c after an f32 action), so Delta_V
+                        * (:64) and Delta_V ** 2 (:79, :84) are float32 ops   */
 } satenv_rd_orbit;
 int satenv_reachable_domain(int64_t nsets, const satenv_rd_orbit* orbits, int32_t n1, int32_t n2, int32_t n3,
                             double* rf_max, double* rf_min, uint8_t* status, void* stream);
+
+/* Flag 2 (environment.py:293-296): numerical_method_process(R0_c, V0_c,
+ * fuel_c) = RD_single_pulse.Incoming_parameters(calculate_orbital_elements(
+ * 3.986e14, R0_c, V0_c), fuel_c) (real_time_data_process.py:11-110,
+ * RD_single_pulse.py:22-37) for every env of the handle: orbits_out
+ * [N] = (a, e0 = e, f, delta_max = fuel_c, mu = 3.986e14, dv_f32) of the
+ * pursuer's absolute state (relative_state_to_absolute_state :334-343),
+ * ready for satenv_reachable_domain + satenv_ellipse_fit.  status_out i32
+ * [N]: 0, or SATENV_ERR_ORBIT_* where the orbit has no 6-element set (the
+ * reference then indexes data[5] of a 4/5-element list and raises).        */
+int satenv_rd_orbits(satenv_env* h, satenv_rd_orbit* orbits_out, int32_t* status_out, void* stream);
 
 /* curve_fitting.Curve_fitting(RF_max, RF_min)  single_pluse_model/curve_fitting.py:475-576
  * on the dense grids of satenv_reachable_domain (same rf_max / rf_min /

@@ -76,6 +76,8 @@ def lib():
         L.orc_rk4_j2_step.argtypes = [dp, C.c_double, dp]
         L.orc_rk4_j2_propagate.argtypes = [dp, C.c_double, C.c_int32]
         L.orc_cw_rk4.argtypes = [dp, C.c_double, C.c_double, C.c_int32, dp]
+        L.orc_cw_rk45.argtypes = [dp, C.c_double, dp, ip]
+        L.orc_cw_rk45.restype = C.c_int32
         L.orc_reachable_domain.argtypes = [C.POINTER(OrcRdParams), dp, dp, C.POINTER(C.c_uint8)]
         L.orc_reachable_domain.restype = C.c_int64
         _lib = L
@@ -117,6 +119,18 @@ def cw_rk4(x, w, t, nsub):
     return y
 
 
+def cw_rk45(x, t):
+    """Numerical_calculation_method.numerical_calculation(t) of one craft
+    (satellite_function.py:783-839): (state after t seconds, nfev)."""
+    y = np.zeros(6)
+    nfev = np.zeros(1, dtype=np.int32)
+    rc = lib().orc_cw_rk45(_dp(np.ascontiguousarray(x, dtype=np.float64)), float(t), _dp(y),
+                           nfev.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc:
+        raise ValueError(f"orc_cw_rk45: {rc}")
+    return y, int(nfev[0])
+
+
 def stm(t=100.0):
     out = np.zeros(36)
     lib().orc_stm(float(t), _dp(out))
@@ -125,13 +139,16 @@ def stm(t=100.0):
 
 class OrcRdParams(C.Structure):
     _fields_ = [("a", C.c_double), ("e0", C.c_double), ("f", C.c_double), ("delta_max", C.c_double),
-                ("mu", C.c_double), ("n1", C.c_int32), ("n2", C.c_int32), ("n3", C.c_int32)]
+                ("mu", C.c_double), ("n1", C.c_int32), ("n2", C.c_int32), ("n3", C.c_int32),
+                ("dv_f32", C.c_int32)]
 
 
-def reachable_domain_grid(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14):
+def reachable_domain_grid(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14, dv_f32=False):
     """RD_single_pulse.py:40-148 over the whole direction grid: returns
-    (rf_max [n][3], rf_min [n][3], status [n] u8) with n = n1*(n2+1)*(n3+1)."""
-    p = OrcRdParams(float(a), float(e0), float(f), float(delta_max), float(mu), int(n1), int(n2), int(n3))
+    (rf_max [n][3], rf_min [n][3], status [n] u8) with n = n1*(n2+1)*(n3+1).
+    dv_f32: delta_max is an np.float32 scalar (Delta_V in float32)."""
+    p = OrcRdParams(float(a), float(e0), float(f), float(delta_max), float(mu), int(n1), int(n2), int(n3),
+                    int(bool(dv_f32)))
     n = int(n1) * (int(n2) + 1) * (int(n3) + 1)
     mx = np.zeros((n, 3))
     mn = np.zeros((n, 3))
@@ -140,10 +157,10 @@ def reachable_domain_grid(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14
     return mx, mn, st
 
 
-def reachable_domain(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14):
+def reachable_domain(a, e0, f, delta_max, n1=1, n2=200, n3=200, mu=3.986e14, dv_f32=False):
     """The RF_max / RF_min point lists Reachable_Domain hands to Curve_fitting
     (RD_single_pulse.py:138-140), in the reference's loop order."""
-    mx, mn, st = reachable_domain_grid(a, e0, f, delta_max, n1, n2, n3, mu)
+    mx, mn, st = reachable_domain_grid(a, e0, f, delta_max, n1, n2, n3, mu, dv_f32)
     if (st == 2).any():
         raise ValueError("gama - f outside the theta branches of RD_single_pulse.py:87-90")
     keep = st == 1

@@ -182,6 +182,169 @@ void orc_cw_rk4(const double x[6], double w, double t, int32_t nsub, double y[6]
     memcpy(y, s, sizeof(s));
 }
 
+/* ---- satellite_function.py:783-839 Numerical_calculation_method ---------
+ * numerical_calculation(t): orbit_ode (:796-821, omega from r = 35786 km, J2
+ * = 0, Tmax = 0) integrated by scipy.integrate.solve_ivp(method='RK45',
+ * t_eval=arange(0, t+50, 50)) with its defaults rtol 1e-3, atol 1e-6;
+ * the result is solution.y[:, -1], the dense output at t_eval[-1] = t.
+ * scipy 1.15.3 (scipy/integrate/_ivp/rk.py, common.py; not part of the
+ * reference) restated: select_initial_step, RungeKutta._step_impl,
+ * rk_step, RK45's tableau and RkDenseOutput.  numpy/OpenBLAS (SkylakeX,
+ * 0.3.29) orderings probed in the build container:
+ *   np.dot(K[:s].T, a)  (dgemv_n, 6 rows): rows 0-3 fma(a0,x0, a1*x1) ->
+ *     fma a2, a3 -> + fma(a4,x4, a5*x5) -> + a6*x6 (blocks 4/2/1); rows 4-5
+ *     a fma chain from a0*x0
+ *   K.T.dot(P), np.dot(Q, p) with >= 2 columns (dgemm): fma chain
+ *   np.dot(Q, p) with one column (dgemv_t): (q0p0 + q2p2) + (q1p1 + q3p3)
+ *   np.linalg.norm (ddot): fma chain from x0*x0                            */
+static const double CW45_W2X = 0x1.8729f82d726ffp-13;    /* 2 * omega          */
+static const double CW45_W3 = 0x1.c044ec3d320a8p-26;     /* 3 * omega ** 2     */
+static const double CW45_WSQ = 0x1.2ad89d7e215c5p-27;    /* omega ** 2         */
+
+static void cw_ode_rhs(const double X[6], double f[6]) {  /* orbit_ode :816-820 (+ a_T = 0, + pJ2 = 0) */
+    f[0] = X[3]; f[1] = X[4]; f[2] = X[5];
+    f[3] = ((CW45_W2X * X[4]) + (CW45_W3 * X[0])) + 0.0;
+    f[4] = ((-CW45_W2X) * X[3]) + 0.0;
+    f[5] = ((-CW45_WSQ) * X[2]) + 0.0;
+}
+static double rms6(const double v[6]) {                   /* common.norm */
+    double t = v[0] * v[0];
+    for (int j = 1; j < 6; ++j) t = fma(v[j], v[j], t);
+    return sqrt(t) / 2.449489742783178;                    /* / x.size ** 0.5 */
+}
+static double rk_gemv(const double K[7][6], const double* a, int s, int i) {   /* np.dot(K[:s].T, a[:s])[i] */
+    if (i >= 4) {
+        double t = K[0][i] * a[0];
+        for (int j = 1; j < s; ++j) t = fma(K[j][i], a[j], t);
+        return t;
+    }
+    if (s == 1) return K[0][i] * a[0];
+    double t = fma(K[0][i], a[0], K[1][i] * a[1]);
+    if (s == 2) return t;
+    if (s == 3) return t + K[2][i] * a[2];
+    t = fma(K[3][i], a[3], fma(K[2][i], a[2], t));
+    int j = 4;
+    if (s - j >= 2) { t = t + fma(K[j][i], a[j], K[j + 1][i] * a[j + 1]); j += 2; }
+    if (s - j >= 1) t = t + K[j][i] * a[j];
+    return t;
+}
+static const double RK45_A[6][5] = {
+    {0, 0, 0, 0, 0},
+    {1.0 / 5, 0, 0, 0, 0},
+    {3.0 / 40, 9.0 / 40, 0, 0, 0},
+    {44.0 / 45, -56.0 / 15, 32.0 / 9, 0, 0},
+    {19372.0 / 6561, -25360.0 / 2187, 64448.0 / 6561, -212.0 / 729, 0},
+    {9017.0 / 3168, -355.0 / 33, 46732.0 / 5247, 49.0 / 176, -5103.0 / 18656}};
+static const double RK45_B[6] = {35.0 / 384, 0, 500.0 / 1113, 125.0 / 192, -2187.0 / 6784, 11.0 / 84};
+static const double RK45_E[7] = {-71.0 / 57600, 0, 71.0 / 16695, -71.0 / 1920, 17253.0 / 339200, -22.0 / 525,
+                                 1.0 / 40};
+static const double RK45_P[7][4] = {
+    {1, -8048581381.0 / 2820520608, 8663915743.0 / 2820520608, -12715105075.0 / 11282082432},
+    {0, 0, 0, 0},
+    {0, 131558114200.0 / 32700410799, -68118460800.0 / 10900136933, 87487479700.0 / 32700410799},
+    {0, -1754552775.0 / 470086768, 14199869525.0 / 1410260304, -10690763975.0 / 1880347072},
+    {0, 127303824393.0 / 49829197408, -318862633887.0 / 49829197408, 701980252875.0 / 199316789632},
+    {0, -282668133.0 / 205662961, 2019193451.0 / 616988883, -1453857185.0 / 822651844},
+    {0, 40617522.0 / 29380423, -110615467.0 / 29380423, 69997945.0 / 29380423}};
+
+int orc_cw_rk45(const double x0[6], double tb, double y_out[6], int32_t* nfev_out) {
+    const double rtol = 1e-3, atol = 1e-6;
+    double y[6], f[6], K[7][6], scale[6], v[6];
+    int nfev = 0;
+    memcpy(y, x0, sizeof(y));
+    cw_ode_rhs(y, f); ++nfev;
+    /* select_initial_step (common.py:109-133), t0 = 0, direction 1, order 4 */
+    double h_abs;
+    {
+        const double L = fabs(tb - 0.0);
+        for (int i = 0; i < 6; ++i) scale[i] = atol + fabs(y[i]) * rtol;
+        for (int i = 0; i < 6; ++i) v[i] = y[i] / scale[i];
+        const double d0 = rms6(v);
+        for (int i = 0; i < 6; ++i) v[i] = f[i] / scale[i];
+        const double d1 = rms6(v);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (0.01 * d0) / d1;
+        if (L < h0) h0 = L;                                         /* min(h0, interval_length) */
+        double y1[6], f1[6];
+        for (int i = 0; i < 6; ++i) y1[i] = y[i] + (h0 * 1.0) * f[i];
+        cw_ode_rhs(y1, f1); ++nfev;
+        for (int i = 0; i < 6; ++i) v[i] = (f1[i] - f[i]) / scale[i];
+        const double d2 = rms6(v) / h0;
+        double h1;
+        if (d1 <= 1e-15 && d2 <= 1e-15) h1 = (1e-6 < h0 * 1e-3) ? h0 * 1e-3 : 1e-6;   /* max(1e-6, h0*1e-3) */
+        else h1 = pow(0.01 / ((d2 > d1) ? d2 : d1), 1.0 / 5);
+        h_abs = 100 * h0;                                           /* min(100*h0, h1, L, inf) */
+        if (h1 < h_abs) h_abs = h1;
+        if (L < h_abs) h_abs = L;
+    }
+    double t = 0.0, t_old = 0.0, y_old[6];
+    while (!(t - tb >= 0)) {                                        /* OdeSolver.step until finished */
+        const double min_step = 10 * fabs(nextafter(t, INFINITY) - t);
+        double h_cur = h_abs < min_step ? min_step : h_abs;
+        int accepted = 0, rejected = 0;
+        double h = 0.0, t_new = t, y_new[6];
+        while (!accepted) {
+            if (h_cur < min_step) { *nfev_out = nfev; return -6; }  /* TOO_SMALL_STEP */
+            h = h_cur * 1.0;
+            t_new = t + h;
+            if (1.0 * (t_new - tb) > 0) t_new = tb;
+            h = t_new - t;
+            h_cur = fabs(h);
+            /* rk_step (rk.py:62-73) */
+            memcpy(K[0], f, sizeof(f));
+            for (int s = 1; s < 6; ++s) {
+                double ys[6];
+                for (int i = 0; i < 6; ++i) ys[i] = y[i] + rk_gemv(K, RK45_A[s], s, i) * h;
+                cw_ode_rhs(ys, K[s]); ++nfev;
+            }
+            for (int i = 0; i < 6; ++i) y_new[i] = y[i] + h * rk_gemv(K, RK45_B, 6, i);
+            cw_ode_rhs(y_new, K[6]); ++nfev;
+            for (int i = 0; i < 6; ++i) {
+                const double ay = fabs(y[i]), an = fabs(y_new[i]);
+                scale[i] = atol + (ay > an ? ay : an) * rtol;      /* np.maximum (finite states) */
+            }
+            for (int i = 0; i < 6; ++i) v[i] = (rk_gemv(K, RK45_E, 7, i) * h) / scale[i];
+            const double en = rms6(v);
+            if (en < 1) {
+                double factor;
+                if (en == 0) factor = 10;
+                else { factor = 0.9 * pow(en, -0.2); if (!(factor < 10)) factor = 10; }   /* min(MAX_FACTOR, .) */
+                if (rejected && !(factor < 1)) factor = 1;                                 /* min(1, factor) */
+                h_cur *= factor;
+                accepted = 1;
+            } else {
+                double fac = 0.9 * pow(en, -0.2);
+                if (!(fac > 0.2)) fac = 0.2;                                               /* max(MIN_FACTOR, .) */
+                h_cur *= fac;
+                rejected = 1;
+            }
+        }
+        t_old = t;
+        memcpy(y_old, y, sizeof(y));
+        t = t_new;
+        memcpy(y, y_new, sizeof(y));
+        memcpy(f, K[6], sizeof(f));
+        h_abs = h_cur;
+    }
+    /* RkDenseOutput at t_eval[-1] == t (x == 1, p == 1): Q = K.T.dot(P) then
+     * y = h * np.dot(Q, p) + y_old; np.dot's kernel depends on how many
+     * t_eval points (multiples of 50 up to t) the last step holds */
+    const double hd = t - t_old;
+    int m = 0;
+    for (double te = 0.0; te <= tb; te += 50.0) if (te > t_old || t_old == 0.0) ++m;   /* (t_old, t]; all in step 1 */
+    for (int i = 0; i < 6; ++i) {
+        double q[4];
+        for (int c = 0; c < 4; ++c) {
+            double a = K[0][i] * RK45_P[0][c];
+            for (int j = 1; j < 7; ++j) a = fma(K[j][i], RK45_P[j][c], a);
+            q[c] = a;
+        }
+        const double sum = (m == 1) ? (q[0] + q[2]) + (q[1] + q[3]) : ((q[0] + q[1]) + q[2]) + q[3];
+        y_out[i] = hd * sum + y_old[i];
+    }
+    *nfev_out = nfev;
+    return 0;
+}
+
 /* ---- satellite_function.py:161-255 calculate_orbital_elements ---------- */
 int orc_orbital_elements(double miu, const double R0[3], const double V0[3], double out[6]) {
     const double r_norm = norm3(R0), v_norm = norm3(V0), r_dot_v = dot3(R0, V0);
@@ -488,8 +651,15 @@ int64_t orc_reachable_domain(const orc_rd_params* p, double* rf_max, double* rf_
     const double sq = sqrt(u / p0);
     int64_t d = 0, reach = 0;
     for (int32_t jj = 1; jj <= p->n1; ++jj) {
-        const double dV = -p->delta_max + (2 * p->delta_max * jj) / p->n1;   /* :64 */
-        const double dV2 = sq2(dV);
+        double dV2;
+        if (p->dv_f32) {                                                      /* np.float32 fuel_c */
+            const float d = (float)p->delta_max;
+            const float dV = -d + ((2.0f * d) * (float)jj) / (float)p->n1;    /* :64 */
+            dV2 = (double)(dV * dV);                                          /* float32 ** 2 */
+        } else {
+            const double dV = -p->delta_max + (2 * p->delta_max * jj) / p->n1;   /* :64 */
+            dV2 = sq2(dV);
+        }
         for (int32_t i = 0; i <= p->n2; ++i) {
             const double gama = (ORC_2PI * i) / p->n2;                        /* :66 */
             const double g = gama - f;
@@ -623,7 +793,7 @@ int orc_step(const orc_params* p, orc_env* e, const float pa_in[3], const float 
     const double dis_prev = norm3(rel);                            /* :89 */
     int p_zero = 0, e_zero = 0;
     const int flag = e->flag;
-    if (flag == 0) {
+    if (flag != 1) {                                               /* Flag 0; Flag 2 :262-276 */
         if (e->dis < p->d_range && e->dz != 0) {                   /* :91-97 */
             add_dv(e->Ev, ea, e->vel_int);
             p_zero = 1;
@@ -648,7 +818,12 @@ int orc_step(const orc_params* p, orc_env* e, const float pa_in[3], const float 
     double xc[6] = {e->Pp[0], e->Pp[1], e->Pp[2], e->Pv[0], e->Pv[1], e->Pv[2]};
     double xt[6] = {e->Ep[0], e->Ep[1], e->Ep[2], e->Ev[0], e->Ev[1], e->Ev[2]};
     double yc[6], yt[6];
-    if (p->propagator == 1) {                       /* optional RK4 on the CW ODE */
+    if (p->propagator == 2) {                       /* optional solve_ivp RK45, :783-839 */
+        int32_t nf;
+        const int rc = orc_cw_rk45(xc, 100.0, yc, &nf);
+        const int rt = orc_cw_rk45(xt, 100.0, yt, &nf);
+        if (rc || rt) return rc ? rc : rt;
+    } else if (p->propagator == 1) {                /* optional RK4 on the CW ODE */
         orc_cw_rk4(xc, p->cw_omega, 100.0, p->rk4_substeps, yc);
         orc_cw_rk4(xt, p->cw_omega, 100.0, p->rk4_substeps, yt);
     } else {
@@ -662,6 +837,11 @@ int orc_step(const orc_params* p, orc_env* e, const float pa_in[3], const float 
     for (int k = 0; k < 3; ++k) rel[k] = e->Pp[k] - e->Ep[k];
     e->dis = norm3(rel);
     make_obs(e, obs);
+    if (flag == 2) {                       /* :298-315: reward 0, no danger-zone update */
+        *reward = 0.0;
+        *done = (e->dis <= p->d_capture || episode_count >= p->max_episode_steps) ? 1 : 0;
+        return 0;
+    }
     if (e->dis <= p->d_capture) {                                   /* :139-142, :221-225 */
         *reward = (flag == 0) ? p->win_reward : -150.0; *done = 1; return 0;
     }
@@ -739,7 +919,7 @@ int orc_step_planes(const orc_params* p, int64_t n, double* f64, int32_t* i32, c
         e.fuel_c = f64[12 * n + i]; e.fuel_t = f64[13 * n + i]; e.dis = f64[14 * n + i];
         const int32_t b = i32[2 * n + i];
         e.dz = i32[i];
-        e.fuel_c_mode = b & 3; e.fuel_t_mode = (b >> 2) & 3; e.vel_int = (b >> 4) & 1; e.flag = (b >> 5) & 1;
+        e.fuel_c_mode = b & 3; e.fuel_t_mode = (b >> 2) & 3; e.vel_int = (b >> 4) & 1; e.flag = (b >> 5) & 3;
         double obs[18], r;
         int32_t d;
         err |= (orc_step(p, &e, pa + 3 * i, ea + 3 * i, episode_count[i], obs, &r, &d) != 0);
@@ -750,7 +930,7 @@ int orc_step_planes(const orc_params* p, int64_t n, double* f64, int32_t* i32, c
         }
         f64[12 * n + i] = e.fuel_c; f64[13 * n + i] = e.fuel_t; f64[14 * n + i] = e.dis;
         i32[i] = e.dz; i32[n + i] = episode_count[i];
-        i32[2 * n + i] = (e.fuel_c_mode & 3) | ((e.fuel_t_mode & 3) << 2) | ((e.vel_int & 1) << 4) | ((e.flag & 1) << 5);
+        i32[2 * n + i] = (e.fuel_c_mode & 3) | ((e.fuel_t_mode & 3) << 2) | ((e.vel_int & 1) << 4) | ((e.flag & 3) << 5);
     }
     return err ? -1 : 0;
 }

@@ -41,7 +41,7 @@ typedef struct {
     double R_cw[3], V_cw[3];
     double stm[36];       /* row-major 6x6, satellite_function.py:766-773 */
     double cw_omega;      /* mean motion of the STM (satellite_function.py:761) */
-    int32_t propagator;   /* 0: closed-form STM (reference), 1: RK4 on the CW ODE */
+    int32_t propagator;   /* 0: closed-form STM (reference), 1: RK4 on the CW ODE, 2: solve_ivp RK45 */
     int32_t rk4_substeps; /* RK4 steps per 100-s env step (propagator 1)         */
 } orc_params;
 
@@ -71,11 +71,18 @@ void orc_rk4_j2_propagate(double rv[6], double h, int32_t steps);
  * z'' = -w^2 z over t seconds in nsub equal steps (propagator 1; the
  * RungeKutta stage combination of the script above)                      */
 void orc_cw_rk4(const double x[6], double w, double t, int32_t nsub, double y[6]);
+/* satellite_function.py:783-839 Numerical_calculation_method: the CW
+ * orbit_ode (omega from r = 35786 km) by scipy solve_ivp RK45 (rtol 1e-3,
+ * atol 1e-6) over (0, t), result = the dense output at t (t a multiple of
+ * 50, the t_eval spacing).  Returns 0, or -6 (scipy's TOO_SMALL_STEP);
+ * *nfev = solve_ivp's function evaluations.                              */
+int  orc_cw_rk45(const double x[6], double t, double y[6], int32_t* nfev);
 
 /* reachable-domain direction grid, RD_single_pulse.py:40-148 (params :9-20) */
 typedef struct {
     double a, e0, f, delta_max, mu;
     int32_t n1, n2, n3;
+    int32_t dv_f32;   /* delta_max is an np.float32 scalar: Delta_V and Delta_V ** 2 in float32 */
 } orc_rd_params;
 /* fills n1*(n2+1)*(n3+1) directions; returns the number with status 1 */
 int64_t orc_reachable_domain(const orc_rd_params* p, double* rf_max, double* rf_min, uint8_t* status);

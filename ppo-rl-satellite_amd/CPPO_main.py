@@ -10,8 +10,8 @@ import argparse
 import numpy as np
 
 from satrl.env import satellites
-from satrl.trainer import (VecTrainer, args_param, test_network, train_evader_network,  # noqa: F401
-                           train_pursuer_network)
+from satrl.trainer import (VecTrainer, args_param, test_network, train_elliptical_network,  # noqa: F401
+                           train_evader_network, train_pursuer_network)
 
 
 def main():
@@ -20,6 +20,7 @@ def main():
     g.add_argument("--test", action="store_true", help="Sign == 1 (the reference default)")
     g.add_argument("--train-pursuer", action="store_true", help="Sign == 0, pursuer part")
     g.add_argument("--train-evader", action="store_true", help="Sign == 0, evader part")
+    g.add_argument("--train-ellipse", action="store_true", help="Sign == 2: train_elliptical_network (Flag 2)")
     g.add_argument("--vec", action="store_true", help="vectorised engine iterations")
     ap.add_argument("--chkpt-dir", default="model_file/one_layer")
     ap.add_argument("--episodes", type=int, default=None)
@@ -47,6 +48,8 @@ def main():
         train_pursuer_network(args, env, show_picture=False, pre_train=True, d_capture=15000, max_episodes=a.episodes)
     elif a.train_evader:
         train_evader_network(args, env, show_picture=False, pre_train=False, d_capture=15000, max_episodes=a.episodes)
+    elif a.train_ellipse:                                    # CPPO_main.py:342-343
+        train_elliptical_network(args, env, epsiodes=a.episodes or 500, d_capture=0)
     else:
         test_network(args, env, show_pictures=False, d_capture=20000)
 

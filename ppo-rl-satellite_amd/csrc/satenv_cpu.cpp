@@ -33,7 +33,7 @@ int fail(int code, const std::string& msg) {
 }
 
 bool params_ok(const satenv_params* p) {
-  return (p->propagator == 0 || p->propagator == 1) && p->rk4_substeps >= 1;
+  return p->propagator >= 0 && p->propagator <= 2 && p->rk4_substeps >= 1;
 }
 
 }  // namespace
@@ -62,7 +62,8 @@ void step_env(satenv_cpu_env* h, const StepIO& io, int64_t i, bool autoreset, do
   int32_t* i32 = h->i32.data();
   double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0;
   Lane L;
-  step_begin(prm, h->n, f64, i32, io, i, autoreset, L);
+  step_begin<true>(prm, h->n, f64, i32, io, i, autoreset, L);
+  if (L.err) note_error(h, L.err);
   if (!L.terminal) {
     int cnt = 0;
     const int rc = danger_zone(prm, L.k[0], L.k[1], L.k[2], L.k[3], L.k[4], L.k[5], L.k[6], L.k[7], L.k[8],
@@ -102,7 +103,7 @@ const char* satenv_cpu_last_error(void) { return g_last_error.c_str(); }
 
 int satenv_cpu_create(satenv_cpu_env** out, int64_t num_envs, const satenv_params* p, int device) {
   if (!out || !p || num_envs <= 0 || device < 0) return fail(SATENV_ERR_ARG, "satenv_cpu_create: bad arguments");
-  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_cpu_create: propagator must be 0/1, rk4_substeps >= 1");
+  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_cpu_create: propagator must be 0/1/2, rk4_substeps >= 1");
   satenv_cpu_env* h = new satenv_cpu_env();
   h->n = num_envs;
   h->threads = device > 0 ? device : omp_get_max_threads();
@@ -127,7 +128,7 @@ int satenv_cpu_num_envs(const satenv_cpu_env* h, int64_t* n) {
 
 int satenv_cpu_set_params(satenv_cpu_env* h, const satenv_params* p) {
   if (!h || !p) return fail(SATENV_ERR_ARG, "satenv_cpu_set_params: null");
-  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_cpu_set_params: propagator must be 0/1, rk4_substeps >= 1");
+  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_cpu_set_params: propagator must be 0/1/2, rk4_substeps >= 1");
   const int32_t flag = h->prm.flag;
   h->prm = *p;
   h->prm.flag = flag;
@@ -137,7 +138,7 @@ int satenv_cpu_set_params(satenv_cpu_env* h, const satenv_params* p) {
 int satenv_cpu_reset(satenv_cpu_env* h, int32_t flag, const uint8_t* env_mask, float* obs_out, double* obs64_out,
                      void* /*stream*/) {
   if (!h) return fail(SATENV_ERR_ARG, "satenv_cpu_reset: null handle");
-  if (flag != 0 && flag != 1) return fail(SATENV_ERR_ARG, "satenv_cpu_reset: only Flag 0/1 are on the hot path");
+  if (flag < 0 || flag > 2) return fail(SATENV_ERR_ARG, "satenv_cpu_reset: Flag must be 0, 1 or 2");
   h->prm.flag = flag;
   const int64_t n = h->n;
   double* f64 = h->f64.data();

@@ -35,7 +35,7 @@
 static inline long long __double_as_longlong(double x) { long long v; std::memcpy(&v, &x, 8); return v; }
 static inline double __longlong_as_double(long long v) { double x; std::memcpy(&x, &v, 8); return x; }
 using std::acos; using std::atan; using std::cos; using std::fabs; using std::fma; using std::pow; using std::rint;
-using std::sin; using std::sqrt; using std::trunc;
+using std::sin; using std::sqrt; using std::trunc; using std::nextafter;
 #endif
 
 #include "satenv.h"
@@ -49,13 +49,13 @@ constexpr double kEpsMch = 2.220446049250313e-16;
 // numpy scalar type of the reference's fuel attributes (environment.py:106-107)
 enum : int { kPyInt = 0, kI64 = 1, kF32 = 2, kF64 = 3 };
 
-// per-env int "bits" plane: [1:0] fuel_c mode, [3:2] fuel_t mode, [4] vel_int, [5] flag
+// per-env int "bits" plane: [1:0] fuel_c mode, [3:2] fuel_t mode, [4] vel_int, [6:5] flag (0/1/2)
 SATENV_HD int fc_mode(int b) { return b & 3; }
 SATENV_HD int ft_mode(int b) { return (b >> 2) & 3; }
 SATENV_HD int vel_int(int b) { return (b >> 4) & 1; }
-SATENV_HD int env_flag(int b) { return (b >> 5) & 1; }
+SATENV_HD int env_flag(int b) { return (b >> 5) & 3; }
 SATENV_HD int make_bits(int fc, int ft, int vi, int flag) {
-  return (fc & 3) | ((ft & 3) << 2) | ((vi & 1) << 4) | ((flag & 1) << 5);
+  return (fc & 3) | ((ft & 3) << 2) | ((vi & 1) << 4) | ((flag & 3) << 5);
 }
 
 using Params = satenv_params;   // include/satenv.h
@@ -546,6 +546,164 @@ SATENV_HD void cw_rk4(double (&s)[6], double w, double t, int nsub) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) s[k] = o[k];
   }
+}
+
+// ---------------------------------------------------------------------------
+// Propagator 2: satellite_function.py:783-839 Numerical_calculation_method.
+// numerical_calculation(t) integrates orbit_ode (:796-821: the CW equations
+// with omega from r = 35786 km, J2 = 0, Tmax = 0) by scipy's solve_ivp RK45
+// (rtol 1e-3, atol 1e-6, t_eval = arange(0, t + 50, 50)) and keeps the
+// dense output at t.  scipy 1.15.3's select_initial_step, _step_impl,
+// rk_step, the RK45 tableau and RkDenseOutput, restated with the
+// numpy/OpenBLAS summation orders the reference executes (the oracle's
+// orc_cw_rk45 documents the probes; it matches the captured solve_ivp
+// outputs bit for bit).  The constants are the reference's python values
+// of 2*omega, 3*omega**2, omega**2.  Returns 0, or -6 when scipy would
+// stop with TOO_SMALL_STEP.
+// ---------------------------------------------------------------------------
+constexpr double kCw45W2x = 0x1.8729f82d726ffp-13;   // 2 * omega
+constexpr double kCw45W3 = 0x1.c044ec3d320a8p-26;    // 3 * omega ** 2
+constexpr double kCw45Wsq = 0x1.2ad89d7e215c5p-27;   // omega ** 2
+
+SATENV_HD void cw45_rhs(const double (&X)[6], double (&f)[6]) {   // orbit_ode :816-820 (+ a_T + pJ2 = +0)
+  f[0] = X[3]; f[1] = X[4]; f[2] = X[5];
+  f[3] = ((kCw45W2x * X[4]) + (kCw45W3 * X[0])) + 0.0;
+  f[4] = ((-kCw45W2x) * X[3]) + 0.0;
+  f[5] = ((-kCw45Wsq) * X[2]) + 0.0;
+}
+SATENV_HD double rms6(const double (&v)[6]) {                      // common.norm (ddot fma chain)
+  double t = v[0] * v[0];
+#pragma unroll
+  for (int j = 1; j < 6; ++j) t = fma(v[j], v[j], t);
+  return sqrt(t) / 2.449489742783178;
+}
+// np.dot(K[:s].T, a[:s])[i] (OpenBLAS dgemv_n, 6 rows: blocks of 4/2/1
+// columns for rows 0-3, a fma chain for the tail rows 4-5)
+SATENV_HD double rk_gemv(const double (&K)[7][6], const double* a, int s, int i) {
+  if (i >= 4) {
+    double t = K[0][i] * a[0];
+#pragma unroll
+    for (int j = 1; j < 7; ++j)
+      if (j < s) t = fma(K[j][i], a[j], t);
+    return t;
+  }
+  if (s == 1) return K[0][i] * a[0];
+  double t = fma(K[0][i], a[0], K[1][i] * a[1]);
+  if (s == 2) return t;
+  if (s == 3) return t + K[2][i] * a[2];
+  t = fma(K[3][i], a[3], fma(K[2][i], a[2], t));
+  int j = 4;
+  if (s - j >= 2) { t = t + fma(K[j][i], a[j], K[j + 1][i] * a[j + 1]); j += 2; }
+  if (s - j >= 1) t = t + K[j][i] * a[j];
+  return t;
+}
+
+SATENV_HD int cw_rk45(double (&y)[6], double tb) {
+  // RK45 tableau (rk.py:380-404), python int/int divisions = correctly rounded doubles
+  constexpr double A[6][5] = {{0, 0, 0, 0, 0},
+                              {1.0 / 5, 0, 0, 0, 0},
+                              {3.0 / 40, 9.0 / 40, 0, 0, 0},
+                              {44.0 / 45, -56.0 / 15, 32.0 / 9, 0, 0},
+                              {19372.0 / 6561, -25360.0 / 2187, 64448.0 / 6561, -212.0 / 729, 0},
+                              {9017.0 / 3168, -355.0 / 33, 46732.0 / 5247, 49.0 / 176, -5103.0 / 18656}};
+  constexpr double B[6] = {35.0 / 384, 0, 500.0 / 1113, 125.0 / 192, -2187.0 / 6784, 11.0 / 84};
+  constexpr double E[7] = {-71.0 / 57600, 0, 71.0 / 16695, -71.0 / 1920, 17253.0 / 339200, -22.0 / 525, 1.0 / 40};
+  constexpr double P[7][4] = {
+      {1, -8048581381.0 / 2820520608, 8663915743.0 / 2820520608, -12715105075.0 / 11282082432},
+      {0, 0, 0, 0},
+      {0, 131558114200.0 / 32700410799, -68118460800.0 / 10900136933, 87487479700.0 / 32700410799},
+      {0, -1754552775.0 / 470086768, 14199869525.0 / 1410260304, -10690763975.0 / 1880347072},
+      {0, 127303824393.0 / 49829197408, -318862633887.0 / 49829197408, 701980252875.0 / 199316789632},
+      {0, -282668133.0 / 205662961, 2019193451.0 / 616988883, -1453857185.0 / 822651844},
+      {0, 40617522.0 / 29380423, -110615467.0 / 29380423, 69997945.0 / 29380423}};
+  constexpr double rtol = 1e-3, atol = 1e-6;
+  double f[6], K[7][6], sc[6], v[6];
+  cw45_rhs(y, f);
+  double h_abs;
+  {  // select_initial_step (common.py:109-133): t0 = 0, direction 1, order 4
+    const double L = fabs(tb - 0.0);
+    for (int i = 0; i < 6; ++i) sc[i] = atol + fabs(y[i]) * rtol;
+    for (int i = 0; i < 6; ++i) v[i] = y[i] / sc[i];
+    const double d0 = rms6(v);
+    for (int i = 0; i < 6; ++i) v[i] = f[i] / sc[i];
+    const double d1 = rms6(v);
+    double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (0.01 * d0) / d1;
+    if (L < h0) h0 = L;
+    double y1[6], f1[6];
+    for (int i = 0; i < 6; ++i) y1[i] = y[i] + (h0 * 1.0) * f[i];
+    cw45_rhs(y1, f1);
+    for (int i = 0; i < 6; ++i) v[i] = (f1[i] - f[i]) / sc[i];
+    const double d2 = rms6(v) / h0;
+    double h1;
+    if (d1 <= 1e-15 && d2 <= 1e-15) h1 = (1e-6 < h0 * 1e-3) ? h0 * 1e-3 : 1e-6;
+    else h1 = pow(0.01 / ((d2 > d1) ? d2 : d1), 1.0 / 5);
+    h_abs = 100 * h0;                                               // min(100*h0, h1, L, max_step)
+    if (h1 < h_abs) h_abs = h1;
+    if (L < h_abs) h_abs = L;
+  }
+  double t = 0.0, t_old = 0.0, y_old[6];
+  while (!(t - tb >= 0)) {                                          // OdeSolver.step until 'finished'
+    const double min_step = 10 * fabs(nextafter(t, (double)INFINITY) - t);
+    double hc = h_abs < min_step ? min_step : h_abs;
+    bool accepted = false, rejected = false;
+    double h = 0.0, t_new = t, yn[6];
+    while (!accepted) {                                             // _step_impl (rk.py:111-164)
+      if (hc < min_step) return -6;
+      t_new = t + hc * 1.0;
+      if (1.0 * (t_new - tb) > 0) t_new = tb;
+      h = t_new - t;
+      hc = fabs(h);
+      for (int i = 0; i < 6; ++i) K[0][i] = f[i];                   // rk_step (rk.py:62-73)
+#pragma unroll
+      for (int s = 1; s < 6; ++s) {
+        double ys[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) ys[i] = y[i] + rk_gemv(K, A[s], s, i) * h;
+        cw45_rhs(ys, K[s]);
+      }
+      for (int i = 0; i < 6; ++i) yn[i] = y[i] + h * rk_gemv(K, B, 6, i);
+      cw45_rhs(yn, K[6]);
+      for (int i = 0; i < 6; ++i) {
+        const double ay = fabs(y[i]), an = fabs(yn[i]);
+        sc[i] = atol + (ay > an ? ay : an) * rtol;
+      }
+      for (int i = 0; i < 6; ++i) v[i] = (rk_gemv(K, E, 7, i) * h) / sc[i];
+      const double en = rms6(v);
+      if (en < 1) {
+        double factor = 10;                                         // MAX_FACTOR
+        if (en != 0) { factor = 0.9 * pow(en, -0.2); if (!(factor < 10)) factor = 10; }
+        if (rejected && !(factor < 1)) factor = 1;
+        hc *= factor;
+        accepted = true;
+      } else {
+        double fac = 0.9 * pow(en, -0.2);
+        if (!(fac > 0.2)) fac = 0.2;                                // max(MIN_FACTOR, .)
+        hc *= fac;
+        rejected = true;
+      }
+    }
+    t_old = t;
+    for (int i = 0; i < 6; ++i) { y_old[i] = y[i]; y[i] = yn[i]; f[i] = K[6][i]; }
+    t = t_new;
+    h_abs = hc;
+  }
+  // RkDenseOutput at t_eval[-1] = t (x = 1): Q = K.T.dot(P) (dgemm: fma
+  // chains), y = h * np.dot(Q, p) + y_old, where np.dot is dgemv_t when the
+  // last step holds one t_eval point and dgemm when it holds more
+  const double hd = t - t_old;
+  int m = 0;
+  for (double te = 0.0; te <= tb; te += 50.0) m += (te > t_old || t_old == 0.0) ? 1 : 0;
+  for (int i = 0; i < 6; ++i) {
+    double q[4];
+    for (int c = 0; c < 4; ++c) {
+      double a = K[0][i] * P[0][c];
+      for (int j = 1; j < 7; ++j) a = fma(K[j][i], P[j][c], a);
+      q[c] = a;
+    }
+    const double sum = (m == 1) ? (q[0] + q[2]) + (q[1] + q[3]) : ((q[0] + q[1]) + q[2]) + q[3];
+    y[i] = hd * sum + y_old[i];
+  }
+  return 0;
 }
 
 }  // namespace satenv

@@ -30,7 +30,7 @@ namespace {
 thread_local std::string g_last_error;
 
 bool params_ok(const satenv_params* p) {
-  return (p->propagator == 0 || p->propagator == 1) && p->rk4_substeps >= 1;
+  return p->propagator >= 0 && p->propagator <= 2 && p->rk4_substeps >= 1;
 }
 
 int fail(int code, const std::string& msg) {
@@ -62,14 +62,15 @@ __device__ __forceinline__ void wave_stats(double* stats, double fin, double fin
 }
 
 // one lane per env, the count's four solves one after another (64-lane blocks)
-template <bool AUTORESET>
+template <bool AUTORESET, bool RK45 = false>
 __global__ void __launch_bounds__(64) step_kernel(const Params prm, int64_t n, double* __restrict__ f64,
                                                   int32_t* __restrict__ i32, StepIO io) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0, cap = 0.0;
   if (i < n) {
     Lane L;
-    step_begin(prm, n, f64, i32, io, i, AUTORESET, L);
+    step_begin<RK45>(prm, n, f64, i32, io, i, AUTORESET, L);
+    if (L.err) atomicCAS(io.err, 0, L.err);
     cap = L.cap;
     if (!L.terminal) {
       int cnt = 0;
@@ -92,7 +93,7 @@ __global__ void __launch_bounds__(64) step_kernel(const Params prm, int64_t n, d
 // latency bound: 16384 envs are only 256 waves).  Bit-identical to
 // step_kernel: every problem runs the same hybrd1.
 constexpr int kSplitEnvs = 64;
-template <bool AUTORESET>
+template <bool AUTORESET, bool RK45 = false>
 __global__ void __launch_bounds__(256) step_kernel_split(const Params prm, int64_t n, double* __restrict__ f64,
                                                          int32_t* __restrict__ i32, StepIO io) {
   __shared__ double sA[4][kSplitEnvs], sSt[4][kSplitEnvs], sDvm[4][kSplitEnvs], sX[4][kSplitEnvs];
@@ -107,7 +108,8 @@ __global__ void __launch_bounds__(256) step_kernel_split(const Params prm, int64
   if (w == 0) {
     bool on[2] = {false, false};
     if (live) {
-      step_begin(prm, n, f64, i32, io, i, AUTORESET, L);
+      step_begin<RK45>(prm, n, f64, i32, io, i, AUTORESET, L);
+      if (L.err) atomicCAS(io.err, 0, L.err);
       cap = L.cap;
       if (!L.terminal) {
         rc = lane_setup(prm, L, z);                                      // :150, :317-332
@@ -253,8 +255,14 @@ __device__ __forceinline__ RdDir rd_dir(const satenv_rd_orbit& o, int n1, int n2
   const int jj = d / per + 1, rem = d - (jj - 1) * per;
   const int i = rem / (n3 + 1), j = rem - i * (n3 + 1);
   RdDir r;
-  const double dV = -o.delta_max + (2.0 * o.delta_max * jj) / n1;   // :64
-  r.dV2 = dV * dV;
+  if (o.dv_f32 != 0.0) {                                            // np.float32 delta_max: f32 ops
+    const float d = (float)o.delta_max;
+    const float dV = -d + ((2.0f * d) * (float)jj) / (float)n1;      // :64
+    r.dV2 = (double)(dV * dV);                                      // Delta_V ** 2 (float32 square)
+  } else {
+    const double dV = -o.delta_max + (2.0 * o.delta_max * jj) / n1;   // :64
+    r.dV2 = dV * dV;
+  }
   r.gama = (kTwoPi * i) / n2;                                       // :66
   r.alpha = -kPi / 2 + (kPi * j) / n3;                              // :68
   r.g = r.gama - o.f;
@@ -345,6 +353,31 @@ __global__ void __launch_bounds__(kRdBlock) rd_kernel(const satenv_rd_orbit* __r
 #pragma unroll
     for (int c = 0; c < 3; ++c) { omx[c] = mx * P[c]; omn[c] = mn * P[c]; }
   }
+}
+
+// Flag 2: the Incoming_parameters orbit of every env (include/satenv.h
+// satenv_rd_orbits): real_time_data_process.calculate_orbital_elements
+// (:11-105, the same element set as satellite_function's, orbital_elements)
+// of the pursuer's absolute state, delta_max = fuel_c with its numpy type
+__global__ void __launch_bounds__(256) rd_orbits_kernel(const Params prm, int64_t n, const double* __restrict__ f64,
+                                                        const int32_t* __restrict__ i32,
+                                                        satenv_rd_orbit* __restrict__ out,
+                                                        int32_t* __restrict__ status) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Elements E;
+  const int rc = orbital_elements(3.986e14, prm.R_cw[0] + f64[0 * n + i], prm.R_cw[1] + f64[1 * n + i],
+                                  prm.R_cw[2] + f64[2 * n + i], prm.V_cw[0] + f64[3 * n + i],
+                                  prm.V_cw[1] + f64[4 * n + i], prm.V_cw[2] + f64[5 * n + i], E);
+  satenv_rd_orbit o;
+  o.a = rc ? 0.0 : E.a;                                            // Incoming_parameters :29-33
+  o.e0 = rc ? 0.0 : E.e;
+  o.f = rc ? 0.0 : E.f;
+  o.delta_max = f64[12 * n + i];
+  o.mu = 3.986e14;                                                 // RD_single_pulse params['u']
+  o.dv_f32 = fc_mode(i32[kPlaneBits * n + i]) == kF32 ? 1.0 : 0.0;
+  out[i] = o;
+  status[i] = rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -497,7 +530,7 @@ int satenv_default_params(satenv_params* p) {
 
 int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, int device) {
   if (!out || !p || num_envs <= 0) return fail(SATENV_ERR_ARG, "satenv_create: bad arguments");
-  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_create: propagator must be 0/1, rk4_substeps >= 1");
+  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_create: propagator must be 0/1/2, rk4_substeps >= 1");
   HIP_TRY(hipSetDevice(device));
   satenv_env* h = new satenv_env();
   h->n = num_envs;
@@ -541,7 +574,7 @@ int satenv_num_envs(const satenv_env* h, int64_t* n) {
 
 int satenv_set_params(satenv_env* h, const satenv_params* p) {
   if (!h || !p) return fail(SATENV_ERR_ARG, "satenv_set_params: null");
-  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_set_params: propagator must be 0/1, rk4_substeps >= 1");
+  if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_set_params: propagator must be 0/1/2, rk4_substeps >= 1");
   h->prm = *p;
   return SATENV_OK;
 }
@@ -549,7 +582,7 @@ int satenv_set_params(satenv_env* h, const satenv_params* p) {
 int satenv_reset(satenv_env* h, int32_t flag, const uint8_t* env_mask, float* obs_out, double* obs64_out,
                  void* stream) {
   if (!h) return fail(SATENV_ERR_ARG, "satenv_reset: null handle");
-  if (flag != 0 && flag != 1) return fail(SATENV_ERR_ARG, "satenv_reset: only Flag 0/1 are on the hot path");
+  if (flag < 0 || flag > 2) return fail(SATENV_ERR_ARG, "satenv_reset: Flag must be 0, 1 or 2");
   h->prm.flag = flag;
   hipLaunchKernelGGL(reset_kernel, dim3(grid_for(h->n, 256)), dim3(256), 0, (hipStream_t)stream, h->prm, h->n,
                      h->f64, h->i32, flag, env_mask, obs_out, obs64_out);
@@ -561,7 +594,10 @@ int satenv_step(satenv_env* h, const float* pa, const float* ea, const int32_t* 
                 double* obs64_out, double* reward_out, uint8_t* done_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step: null argument");
   StepIO io{pa, ea, episode_count, obs_out, obs64_out, reward_out, nullptr, done_out, nullptr, h->err};
-  if (h->split)
+  if (h->prm.propagator == 2)   // the RK45 instantiation (its registers stay out of the STM kernels)
+    hipLaunchKernelGGL((step_kernel_split<false, true>), dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0,
+                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
+  else if (h->split)
     hipLaunchKernelGGL(step_kernel_split<false>, dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0, (hipStream_t)stream,
                        h->prm, h->n, h->f64, h->i32, io);
   else
@@ -575,7 +611,10 @@ int satenv_step_autoreset(satenv_env* h, const float* pa, const float* ea, float
                           uint8_t* done_out, double* stats_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step_autoreset: null argument");
   StepIO io{pa, ea, nullptr, obs_out, nullptr, nullptr, reward_out, done_out, stats_out, h->err};
-  if (h->split)
+  if (h->prm.propagator == 2)   // the RK45 instantiation (its registers stay out of the STM kernels)
+    hipLaunchKernelGGL((step_kernel_split<true, true>), dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0,
+                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
+  else if (h->split)
     hipLaunchKernelGGL(step_kernel_split<true>, dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0, (hipStream_t)stream,
                        h->prm, h->n, h->f64, h->i32, io);
   else
@@ -649,6 +688,14 @@ int satenv_reachable_domain(int64_t nsets, const satenv_rd_orbit* orbits, int32_
     return fail(SATENV_ERR_ARG, "satenv_reachable_domain: grid too large");
   hipLaunchKernelGGL(rd_kernel, dim3((unsigned)(nsets * tiles)), dim3(kRdBlock), 0, (hipStream_t)stream, orbits, n1,
                      n2, n3, (int32_t)ndir, (int32_t)tiles, rf_max, rf_min, status);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_rd_orbits(satenv_env* h, satenv_rd_orbit* orbits_out, int32_t* status_out, void* stream) {
+  if (!h || !orbits_out || !status_out) return fail(SATENV_ERR_ARG, "satenv_rd_orbits: null argument");
+  hipLaunchKernelGGL(rd_orbits_kernel, dim3(grid_for(h->n, 256)), dim3(256), 0, (hipStream_t)stream, h->prm, h->n,
+                     h->f64, h->i32, orbits_out, status_out);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

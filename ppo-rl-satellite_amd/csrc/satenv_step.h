@@ -73,12 +73,17 @@ struct Lane {
   int dz, count, flag, fcm, ftm;
   bool p_zero;
   float pa[3];
-  bool terminal;          // capture or timeout: reward/done set, no count (:139-147 return first)
+  int err;                // propagator 2: scipy's TOO_SMALL_STEP (-6), else 0
+  bool terminal;          // reward/done final, no count: capture or timeout (:139-147 return first), or Flag 2
   double reward;
   bool done;
   double cap;
 };
 
+// kRk45: the instantiation that carries propagator 2 (solve_ivp RK45); the
+// default kernels leave it out so its registers do not cost the STM path
+// occupancy
+template <bool kRk45 = false>
 SATENV_HD void step_begin(const Params& prm, int64_t n, const double* __restrict__ f64,
                                            const int32_t* __restrict__ i32, const StepIO& io, int64_t i,
                                            bool autoreset, Lane& L) {
@@ -104,7 +109,7 @@ SATENV_HD void step_begin(const Params& prm, int64_t n, const double* __restrict
   }
   L.dis_prev = norm3(k[0] - k[6], k[1] - k[7], k[2] - k[8]);             // :89
   bool p_zero = false, e_zero = false, move_p = true, move_e = true;
-  if (L.flag == 0) {
+  if (L.flag != 1) {                                                      // Flag 0 and Flag 2 (:262-276)
     if (L.dis < prm.d_range && L.dz != 0) { move_p = false; p_zero = true; }   // :91-97
   } else {
     if (L.dz == 0) { move_e = false; e_zero = true; }                         // :194-198
@@ -118,7 +123,25 @@ SATENV_HD void step_begin(const Params& prm, int64_t n, const double* __restrict
   fuel_sub(L.fuel_c, L.fcm, p_zero, (fabsf(L.pa[0]) + fabsf(L.pa[1])) + fabsf(L.pa[2]));   // :106
   fuel_sub(L.fuel_t, L.ftm, e_zero, (fabsf(ea[0]) + fabsf(ea[1])) + fabsf(ea[2]));         // :107
 
-  if (prm.propagator == 1) {                                              // optional: RK4 on the CW ODE
+  L.err = 0;
+  bool propagated = false;
+  if constexpr (kRk45) {
+    if (prm.propagator == 2) {                                            // optional: solve_ivp RK45 (:783-839)
+#pragma unroll 1
+      for (int craft = 0; craft < 2; ++craft) {
+        double x[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) x[c] = k[6 * craft + c];
+        const int rc = cw_rk45(x, 100.0);
+        if (rc) L.err = rc;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) k[6 * craft + c] = x[c];
+      }
+      propagated = true;
+    }
+  }
+  if (propagated) {
+  } else if (prm.propagator == 1) {                                       // optional: RK4 on the CW ODE
 #pragma unroll
     for (int craft = 0; craft < 2; ++craft) {
       double x[6];
@@ -149,12 +172,15 @@ SATENV_HD void step_begin(const Params& prm, int64_t n, const double* __restrict
   L.cap = 0.0;
   L.terminal = true;
   L.done = true;
-  if (L.dis <= prm.d_capture) {                                           // :139-142, :221-225
-    L.reward = L.flag == 0 ? prm.win_reward : -150.0;
+  if (L.dis <= prm.d_capture) {                                           // :139-142, :221-225, :303-306
+    L.reward = L.flag == 0 ? prm.win_reward : (L.flag == 1 ? -150.0 : 0.0);
     L.cap = 1.0;
-  } else if (L.count >= prm.max_episode_steps) {                         // :144-147, :227-231
-    L.reward = L.flag == 0 ? prm.burn_reward : prm.win_reward;
-  } else {
+  } else if (L.count >= prm.max_episode_steps) {                         // :144-147, :227-231, :308-311
+    L.reward = L.flag == 0 ? prm.burn_reward : (L.flag == 1 ? prm.win_reward : 0.0);
+  } else if (L.flag == 2) {                                               // :313-315: reward 0, not done,
+    L.reward = 0.0;                                                       // no danger-zone update (the
+    L.done = false;                                                       // ellipse fit and the surrogate
+  } else {                                                                // training run outside the kernel)
     L.terminal = false;
     L.done = false;
   }

@@ -82,6 +82,7 @@ _SIGS = {
     "satenv_surrogate": ([_vp, _vp, _vp, _vp], C.c_int),
     "satenv_surrogate_mlp": ([_i64, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_ellipse_fit": ([_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_rd_orbits": ([_vp, _vp, _vp, _vp], C.c_int),
     "satenv_cpu_last_error": ([], C.c_char_p),
     "satenv_cpu_create": ([C.POINTER(_vp), _i64, C.POINTER(SatenvParams), C.c_int], C.c_int),
     "satenv_cpu_destroy": ([_vp], C.c_int),

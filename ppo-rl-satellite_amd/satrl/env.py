@@ -145,6 +145,14 @@ class VecSatellites:
     def _push_params(self):
         check(self._fn("set_params")(self._h, C.byref(self._p)), self._api + "set_params")
 
+    def set_params(self, **fields):
+        """Update satenv_params fields (e.g. propagator=2) and push them."""
+        for k, v in fields.items():
+            if not hasattr(self._p, k):
+                raise AttributeError(f"satenv_params has no field {k!r}")
+            setattr(self._p, k, v)
+        self._push_params()
+
     @property
     def d_capture(self):
         return self._p.d_capture
@@ -257,34 +265,28 @@ class VecSatellites:
 
 
 def pack_bits(fuel_c_mode, fuel_t_mode, vel_int, flag):
-    return (int(fuel_c_mode) & 3) | ((int(fuel_t_mode) & 3) << 2) | ((int(vel_int) & 1) << 4) | ((int(flag) & 1) << 5)
+    return (int(fuel_c_mode) & 3) | ((int(fuel_t_mode) & 3) << 2) | ((int(vel_int) & 1) << 4) | ((int(flag) & 3) << 5)
 
 
 def unpack_bits(b):
     b = int(b)
-    return dict(fuel_c_mode=b & 3, fuel_t_mode=(b >> 2) & 3, vel_int=(b >> 4) & 1, flag=(b >> 5) & 1)
+    return dict(fuel_c_mode=b & 3, fuel_t_mode=(b >> 2) & 3, vel_int=(b >> 4) & 1, flag=(b >> 5) & 3)
 
 
 def _typed(v, mode):
     return [int(v), np.int64(v), np.float32(v), np.float64(v)][mode]
 
 
-class _EllipseFittingNet:
-    """The part of real_time_data_process.network_method_train (:127-139) the
-    env step can observe: ``net`` = an ImprovedNN built on the CPU (its
-    forward is commented out in the step, environment.py:158)."""
-
-    def __init__(self):
-        from .surrogate import ImprovedNN
-        self.net = ImprovedNN()
-
-
 class satellites:  # noqa: N801  (reference class name)
-    """Drop-in for ``environment.satellites`` (environment.py:8), Flag 0/1.
+    """Drop-in for ``environment.satellites`` (environment.py:8), Flag 0/1/2.
 
     Same keywords as environment.py:26-28; ``args.max_episode_steps`` is
     required as in environment.py:46.  State lives on the GPU; the public
-    attributes are read back on access.
+    attributes are read back on access.  Flag 2 (environment.py:257-315):
+    the kernel steps the state (no danger-zone update, reward 0), the
+    ellipse_params come from the reachable-domain grid and ellipse-fit
+    kernels (satrl.reachable), and the env's network_method_train takes its
+    step on the CPU like the reference's.
     """
 
     def __init__(self, Pursuer_position=np.array([2000, 2000, 1000]), Pursuer_vector=np.array([1.71, 1.14, 1.3]),
@@ -306,7 +308,9 @@ class satellites:  # noqa: N801  (reference class name)
         # (real_time_data_process.py:129) draws its default init from torch's
         # global CPU generator: draw the same numbers, so agents constructed
         # after a seeded env get the reference's weights
-        self.trian_elliptical_fitting = _EllipseFittingNet()
+        from .surrogate import network_method_train
+        self.trian_elliptical_fitting = network_method_train(pretrain=False,
+                                                             save_dir=getattr(args, "ellipse_save_dir", None))
         dev = self._v.device
         self._pa = torch.empty((1, ACT_DIM), dtype=torch.float32, device=dev)
         self._ea = torch.empty((1, ACT_DIM), dtype=torch.float32, device=dev)
@@ -379,8 +383,8 @@ class satellites:  # noqa: N801  (reference class name)
     # API ------------------------------------------------------------------------
     def reset(self, Flag):
         """environment.py:66-79: returns the int64 observation."""
-        if Flag not in (0, 1):
-            raise NotImplementedError("Flag 2 (reachable-domain training) is outside the accelerated path")
+        if Flag not in (0, 1, 2):
+            raise ValueError(f"Flag must be 0, 1 or 2 (environment.py:36), got {Flag!r}")
         self._v.reset(Flag, obs64_out=self._obs)
         return self._obs[0].cpu().numpy().astype(np.int64)
 
@@ -397,7 +401,28 @@ class satellites:  # noqa: N801  (reference class name)
         done = bool(self._d.item())
         if done:
             r = int(r)          # terminal rewards are python ints in the reference
+        if self.Flag == 2:
+            self._flag2_fit()
+            r = 0               # environment.py:298-315 return the literal 0
         return obs, r, done
+
+    def _flag2_fit(self):
+        """environment.py:293-301: ellipse_params = numerical_method_process(
+        R0_c, V0_c, fuel_c) on the GPU grid + fit kernels, then one step of
+        the env's ellipse-fitting network."""
+        from . import reachable as RD
+        if self._v.host:
+            raise _lib.NativeError("Flag 2's reachable-domain grid and ellipse fit run on the GPU kernels; the host "
+                                   "build steps Flag 0/1 only")
+        orbits, status = RD.env_orbits(self._v)
+        if int(status.item()) != 0:
+            # real_time_data_process.py:109 -> RD_single_pulse.py:32 indexes data[5] of a 4/5-element list
+            raise IndexError("list index out of range (the pursuer's orbit has no 6-element set, "
+                             f"satenv code {int(status.item())})")
+        ell, _ = RD.reachable_ellipses(orbits, RD.params["N1"], RD.params["N2"], RD.params["N3"])
+        self.ellipse_params = ell[0].cpu().numpy()
+        R0_c, V0_c = self.relative_state_to_absolute_state(self.Pursuer_position, self.Pursuer_vector)
+        self.trian_elliptical_fitting.train(R0_c, V0_c, self.fuel_c, self.ellipse_params)
 
     @staticmethod
     def relative_state_to_absolute_state(R0, V0):

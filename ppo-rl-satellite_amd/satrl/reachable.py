@@ -39,9 +39,10 @@ params = {
 UNREACHABLE, REACHABLE, THETA_UNDEFINED = 0, 1, 2
 
 
-def orbits_tensor(a, e0, f, delta_max, mu=3.986e14, device="cuda"):
-    """[nsets][5] f64 rows (a, e0, f, delta_max, mu) = satenv_rd_orbit; scalars broadcast."""
-    cols = np.broadcast_arrays(*[np.asarray(v, dtype=np.float64) for v in (a, e0, f, delta_max, mu)])
+def orbits_tensor(a, e0, f, delta_max, mu=3.986e14, device="cuda", dv_f32=0.0):
+    """[nsets][6] f64 rows (a, e0, f, delta_max, mu, dv_f32) = satenv_rd_orbit;
+    scalars broadcast.  dv_f32 != 0: delta_max is an np.float32 scalar."""
+    cols = np.broadcast_arrays(*[np.asarray(v, dtype=np.float64) for v in (a, e0, f, delta_max, mu, dv_f32)])
     arr = np.stack([c.reshape(-1) for c in cols], axis=1)
     return torch.tensor(arr, dtype=torch.float64, device=device)
 
@@ -51,8 +52,8 @@ def reachable_domain_grid(orbits, n1=1, n2=200, n3=200, stream=None):
     [nsets][ndir] u8) with ndir = n1*(n2+1)*(n3+1), direction order of the
     reference loops (jj, i, j).  Entries with status != 1 are zero."""
     _lib.require_cuda(orbits, torch.float64, None, "orbits")
-    if orbits.dim() != 2 or orbits.shape[1] != 5 or not orbits.is_contiguous():
-        raise ValueError("orbits must be a contiguous [nsets][5] f64 tensor")
+    if orbits.dim() != 2 or orbits.shape[1] != 6 or not orbits.is_contiguous():
+        raise ValueError("orbits must be a contiguous [nsets][6] f64 tensor (satenv_rd_orbit)")
     nsets = orbits.shape[0]
     ndir = int(n1) * (int(n2) + 1) * (int(n3) + 1)
     dev = orbits.device
@@ -120,7 +121,8 @@ def Reachable_Domain(device="cuda"):
     """RD_single_pulse.Reachable_Domain (:40-148) on the module `params`:
     the [2][5] ellipse array of Curve_fitting (:140)."""
     p = params
-    orbits = orbits_tensor(p["a"], p["e0"], p["f"], p["delta_max"], p["u"], device)
+    orbits = orbits_tensor(p["a"], p["e0"], p["f"], p["delta_max"], p["u"], device,
+                           dv_f32=isinstance(p["delta_max"], np.float32))
     ell, info = reachable_ellipses(orbits, p["N1"], p["N2"], p["N3"])
     info = info.cpu().numpy()
     if (info < 0).any():
@@ -133,3 +135,41 @@ def Incoming_parameters(data, delta_max, device="cuda"):
     params["a"], params["i"], params["e0"], params["f"] = data[0], data[2], data[1], data[5]
     params["delta_max"] = delta_max
     return np.array(Reachable_Domain(device))
+
+
+def env_orbits(env, stream=None):
+    """Flag 2's Incoming_parameters orbit of every env of a VecSatellites
+    (environment.py:293-296 -> real_time_data_process.py:107-110):
+    ([N][6] f64 satenv_rd_orbit rows, status [N] i32: 0 or the
+    SATENV_ERR_ORBIT_* of an orbit without a 6-element set)."""
+    n = env.num_envs
+    orbits = torch.empty((n, 6), dtype=torch.float64, device=env.device)
+    status = torch.empty(n, dtype=torch.int32, device=env.device)
+    check(_lib.lib().satenv_rd_orbits(env._h, ptr(orbits), ptr(status), stream_ptr(stream)), "satenv_rd_orbits")
+    return orbits, status
+
+
+def env_ellipse_params(env, chunk=512, n1=None, n2=None, n3=None, stream=None):
+    """numerical_method_process for every env (the Flag-2 ellipse_params,
+    environment.py:296): [N][2][5] f64 ellipses and info [N][2] i32 (see
+    ellipse_fit; rows of envs without a 6-element orbit are NaN with info
+    SATENV_ERR_ORBIT_*).  The 201 x 201 direction grids of `chunk` envs at a
+    time (2 x 0.97 MB of points per env) go through the grid and fit kernels
+    without leaving the GPU."""
+    p = params
+    n1 = p["N1"] if n1 is None else n1
+    n2 = p["N2"] if n2 is None else n2
+    n3 = p["N3"] if n3 is None else n3
+    orbits, status = env_orbits(env, stream)
+    n = env.num_envs
+    ell = torch.full((n, 2, 5), float("nan"), dtype=torch.float64, device=env.device)
+    info = torch.empty((n, 2), dtype=torch.int32, device=env.device)
+    for s0 in range(0, n, chunk):
+        s1 = min(n, s0 + chunk)
+        e, i = reachable_ellipses(orbits[s0:s1].contiguous(), n1, n2, n3, stream)
+        ell[s0:s1] = e
+        info[s0:s1] = i
+    bad = status != 0
+    ell[bad] = float("nan")
+    info[bad] = status[bad].unsqueeze(1).expand(-1, 2)
+    return ell, info

@@ -12,6 +12,7 @@ accumulation whose activations never leave registers (surrogate_device.h).
 Inference semantics: no dropout (the reference constructs the net fresh in
 training mode, so its dropout would make the output random).
 """
+import numpy as np
 import torch
 
 from . import _lib
@@ -95,3 +96,121 @@ def bf16_reference(net, x):
         if i < 3:
             h = q(torch.relu(h))
     return h
+
+
+# ---------------------------------------------------------------------------
+# Flag 2: the ellipse-fitting network trainer the env owns
+# (environment.py:49, :298-301; real_time_data_process.py:127-183)
+# ---------------------------------------------------------------------------
+class ImprovedNNDropout(ImprovedNN):
+    """ImprovedNN with model.py:14's Dropout(0.2) after fc1 and fc2, as the
+    reference trains it (the module is in training mode)."""
+
+    def __init__(self):
+        super().__init__()
+        self.dropout = torch.nn.Dropout(0.2)
+
+    def forward(self, x):
+        x = self.dropout(torch.relu(self.fc1(x)))
+        x = self.dropout(torch.relu(self.fc2(x)))
+        x = torch.relu(self.fc3(x))
+        return self.fc4(x)
+
+
+def rtp_orbital_elements(miu, R0, V0):
+    """real_time_data_process.calculate_orbital_elements (:11-105) on host
+    arrays: [a, e, i, omega, Omega, f] (ellipse/hyperbola), [a, i, u, Omega]
+    (circular) or [p, i, omega, Omega, f] (parabolic), numpy semantics."""
+    R0 = np.asarray(R0)
+    V0 = np.asarray(V0)
+    r_norm = np.linalg.norm(R0)
+    v_norm = np.linalg.norm(V0)
+    r_dot_v = np.dot(R0, V0)
+    en = 2 / r_norm - v_norm ** 2 / miu
+    a = 1 / abs(en) if en != 0 else None
+    E = (v_norm ** 2 / miu - 1 / r_norm) * R0 - r_dot_v / miu * V0
+    e = np.linalg.norm(E)
+    H = np.cross(R0, V0)
+    h = np.linalg.norm(H)
+    p = h ** 2 / miu
+    Z, X, Y = np.array([0, 0, 1]), np.array([1, 0, 0]), np.array([0, 1, 0])
+    N = np.cross(Z, H)
+    n = np.linalg.norm(N)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        i = np.arccos(np.dot(Z, H) / h)
+        if e != 0:
+            omega = np.arccos(np.dot(N, E) / n / e) if (n != 0 and e != 0) else 0.0
+            if np.dot(Z, E) < 0:
+                omega = 2 * np.pi - omega
+        else:
+            u = np.arccos(np.dot(N, R0) / n / r_norm)
+            if np.dot(R0, Z) < 0:
+                u = 2 * np.pi - u
+        Omega = np.arccos(np.dot(X, N) / n) if n != 0 else 0.0
+        if np.dot(Y, N) < 0:
+            Omega = 2 * np.pi - Omega
+        if e != 0:
+            f = np.arccos(np.dot(E, R0) / e / r_norm)
+            if r_dot_v < 0:
+                f = 2 * np.pi - f
+    if en != 0:
+        return [a, e, i, omega, Omega, f] if e != 0 else [a, i, u, Omega]
+    return [p, i, omega, Omega, f]
+
+
+class network_method_train:  # noqa: N801  (reference class name)
+    """Drop-in for real_time_data_process.network_method_train (:127-183):
+    one Adam step (lr 1e-3, StepLR 10 / 0.1) of ImprovedNN on the
+    StandardScaler-transformed (input, target) of the current step.  A
+    one-row StandardScaler maps every finite value to 0, so the reference
+    trains the net towards f(0) = 0 whatever the ellipse is; the step runs
+    on torch's CPU like the reference's, drawing ImprovedNN's init and the
+    dropout masks from the same global generator in the same order.
+
+    Divergence by necessity: every 10th step the reference saves MLPNet2.pth
+    to the author's absolute path (/mnt/datab/...), which raises anywhere
+    else; here it goes to `save_dir` (None: not saved)."""
+
+    def __init__(self, pretrain=False, pretrained_path=None, save_dir=None):
+        from sklearn.preprocessing import StandardScaler
+        self.net = ImprovedNNDropout()
+        if pretrain:
+            if pretrained_path is None:
+                raise FileNotFoundError("pretrain=True needs pretrained_path (MLPNet.pth; the reference's path is "
+                                        "an absolute one on the author's machine)")
+            sd = torch.load(pretrained_path, map_location="cpu", weights_only=True)
+            self.net.load_state_dict(sd)
+        self.criterion = torch.nn.MSELoss()
+        self.optimizer = torch.optim.Adam(self.net.parameters(), lr=0.001)
+        self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=10, gamma=0.1)
+        self.count = 0
+        self.loss = []
+        self.all_loss = []
+        self.save_dir = save_dir
+        self.input_scaler = StandardScaler()
+        self.output_scaler = StandardScaler()
+
+    def train(self, R0, V0, fuel, target):
+        target = self.output_scaler.fit_transform(np.asarray(target).reshape(1, -1))
+        target = torch.tensor(target.reshape(10), dtype=torch.float32)
+        orbit_data = rtp_orbital_elements(3.986e14, R0, V0)
+        x = orbit_data[:3] + orbit_data[5:]
+        x.append(fuel)
+        x = self.input_scaler.fit_transform(np.array(x).reshape(1, -1)).reshape(5)
+        x = torch.tensor(x, dtype=torch.float32)
+        self.optimizer.zero_grad()
+        predictions = self.net(x)
+        loss = self.criterion(predictions, target)
+        self.loss.append(loss)
+        self.all_loss.append(loss)
+        loss.backward()
+        self.optimizer.step()
+        self.count += 1
+        if self.count == 10:
+            self.scheduler.step()
+            self.count = 0
+            print("loss: ", sum(self.loss) / 10)
+            self.loss = []
+            if self.save_dir is not None:
+                import os
+                torch.save(self.net.state_dict(), os.path.join(self.save_dir, "MLPNet2.pth"))

@@ -191,6 +191,35 @@ def test_network(args, env, show_pictures=False, d_capture=0):
             return epsiode_reward
 
 
+def train_elliptical_network(args, env, epsiodes=200, d_capture=0):
+    """CPPO_main.py:284-322: Flag-2 episodes with the trained pursuer and an
+    untrained evader acting; each env step fits the reachable-domain
+    ellipse (GPU grid + fit kernels) and trains the env's ImprovedNN.  Note
+    the reference never resets epsiode_count between episodes (:287, :301),
+    so every episode after the first ends at its first step's timeout test."""
+    env.d_capture = d_capture
+    args.state_dim = env.observation_space.shape[0]
+    args.action_dim = env.action_space.shape[0]
+    args.max_action = float(env.action_space[0][1])
+    pursuer_agent = PPO_continuous(args, "pursuer")
+    evader_agent = PPO_continuous(args, "evader")
+    pursuer_agent.load_checkpoint()
+    epsiode_count = 0
+    for _ in range(epsiodes):
+        s = env.reset(2)
+        while True:
+            epsiode_count += 1
+            pa, _ = pursuer_agent.choose_action(s)
+            ea, _ = evader_agent.choose_action(s)
+            if args.policy_dist == "Beta":
+                pa = 2 * (pa - 0.5) * args.max_action
+                ea = 2 * (ea - 0.5) * args.max_action
+            s_, r, done = env.step(pa, ea, epsiode_count)
+            s = s_
+            if done:
+                break
+
+
 # ---------------------------------------------------------------------------
 # vectorised engine
 # ---------------------------------------------------------------------------

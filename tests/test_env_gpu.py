@@ -298,3 +298,60 @@ def test_autoreset_block_geometries_vs_oracle(satrl_env, oracle, n):
     exact but for listed libm ties)."""
     ties, counted = _locked_autoreset_rollout(satrl_env, oracle, n, 24, n, 15000.0, 10, f"autoreset n={n}")
     assert ties <= max(2, counted // 20000), (ties, counted)
+
+
+def test_env_rk45_cw_mode_vs_reference_solve_ivp(satrl_env):
+    """propagator 2 (satellite_function.py:783-839: the CW orbit_ode by
+    scipy solve_ivp RK45, dense output at the 100-s step) on the GPU vs the
+    reference's own numerical_calculation(100) outputs (cw_ode.npz), zero
+    actions.  The step-size control calls pow(err, -0.2) (OCML here, glibc in
+    the reference), so the bar is rel 1e-13 of the state's scale; the count
+    of bitwise-equal states is printed."""
+    import test_host_build as H
+    g = golden("cw_ode")
+    a = list(g["t"]).index(100.0)
+    n, f, i32, want = H._cw_ode_pairs(g, a)
+    env = satrl_env.VecSatellites(n, d_capture=0.0, max_episode_steps=1000, propagator=2)
+    env.set_state(f.cuda(), i32.cuda())
+    z = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+    env.step(z, z, torch.ones(n, dtype=torch.int32, device="cuda"))
+    assert env.check_errors() == 0
+    got = env.get_state()[0][0:12].cpu().numpy()
+    scale = np.maximum(np.abs(want).max(axis=0, keepdims=True), 1e-300)
+    err = (np.abs(got - want) / scale).max()
+    exact = int((got == want).all(axis=0).sum())
+    print(f"propagator 2 vs solve_ivp: {exact}/{n} env pairs bitwise, worst rel {err:.2e}")
+    assert err <= 1e-13
+
+
+def test_env_rk45_cw_mode_rollout_vs_oracle(satrl_env, oracle):
+    """propagator 2 inside the full step (gating, fuel, terminal logic,
+    danger-zone count, reward): step-locked to the oracle, done exact,
+    obs rel 1e-12, reward 1e-9."""
+    n, T = 24, 40
+    rng = np.random.default_rng(19)
+    pa = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    ea = rng.uniform(-1.6, 1.6, (T, n, 3)).astype(np.float32)
+    env = satrl_env.VecSatellites(n, d_capture=15000.0, max_episode_steps=30, propagator=2)
+    env.reset(0)
+    orc = [oracle.OracleEnv(15000.0, 30, propagator=2) for _ in range(n)]
+    for o in orc:
+        o.reset(0)
+    cnt = np.zeros(n, dtype=np.int32)
+    obs64 = torch.empty((n, 18), dtype=torch.float64, device="cuda")
+    for t in range(T):
+        cnt += 1
+        _, r, d = env.step(torch.tensor(pa[t], device="cuda"), torch.tensor(ea[t], device="cuda"),
+                           torch.tensor(cnt, device="cuda"), obs64_out=obs64)
+        obs = obs64.cpu().numpy(); r = r.cpu().numpy(); d = d.cpu().numpy()
+        for i, o in enumerate(orc):
+            oo, orr, od = o.step(pa[t, i], ea[t, i], int(cnt[i]))
+            assert np.allclose(obs[i], oo, rtol=1e-12, atol=1e-9), (t, i)
+            assert bool(d[i]) == od, (t, i)
+            assert abs(r[i] - orr) <= 1e-9 * max(1.0, abs(orr)), (t, i, r[i], orr)
+            if od:
+                o.reset(0)
+                cnt[i] = 0
+        if d.any():
+            env.reset(0, mask=torch.tensor(d.astype(np.uint8), device="cuda"))
+    assert env.check_errors() == 0

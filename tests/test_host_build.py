@@ -59,6 +59,41 @@ def test_host_step_bitexact_vs_reference(name):
     assert np.array_equal(r.numpy(), d["r_glibc"])
 
 
+def _cw_ode_pairs(g, a):
+    """env k = (pursuer x0[2k], evader x0[2k+1]) of cw_ode.npz case a"""
+    x0, out = g["x0"], g["out"][a]
+    n = (len(x0) + 1) // 2
+    ip = np.arange(n) * 2
+    ie = np.minimum(ip + 1, len(x0) - 1)
+    f = np.zeros((15, n))
+    f[0:6] = x0[ip].T
+    f[6:12] = x0[ie].T
+    f[12:14] = 320.0
+    f[14] = np.inf
+    i32 = np.zeros((3, n), np.int32)
+    from satrl.env import pack_bits
+    i32[2] = pack_bits(0, 0, 0, 0)
+    want = np.concatenate([out[ip].T, out[ie].T])
+    return n, torch.from_numpy(f), torch.from_numpy(i32), want
+
+
+def test_host_propagator2_is_the_reference_solve_ivp():
+    """propagator 2 (satellite_function.py:783-839, solve_ivp RK45 over the
+    100-s step) in the host build: zero actions, every captured state pair
+    propagated bit for bit like the reference's numerical_calculation(100)."""
+    from satrl.env import VecSatellites
+    g = golden("cw_ode")
+    a = list(g["t"]).index(100.0)
+    n, f, i32, want = _cw_ode_pairs(g, a)
+    env = VecSatellites(n, device="cpu", d_capture=0.0, max_episode_steps=1000, propagator=2)
+    env.set_state(f, i32)
+    z = torch.zeros((n, 3), dtype=torch.float32)
+    env.step(z, z, torch.ones(n, dtype=torch.int32))
+    assert env.check_errors() == 0
+    fa, _ = env.get_state()
+    assert np.array_equal(fa[0:12].numpy(), want)
+
+
 def test_host_danger_zone_counts_exact():
     import ctypes as C
     from satrl import _lib

@@ -274,3 +274,18 @@ def test_curve_fitting_golden_pairs(oracle):
             scale = max(abs(ref[j][2]), abs(ref[j][3]))
             assert np.abs(ell[j][:2] - ref[j][:2]).max() < 1e-3 * scale, (r, j)
             assert np.allclose(np.sort(np.abs(ell[j][2:4])), np.sort(np.abs(ref[j][2:4])), rtol=1e-3), (r, j)
+
+
+def test_cw_rk45_restatement_bitexact(oracle):
+    """satellite_function.py:783-839 Numerical_calculation_method (scipy
+    solve_ivp RK45 on orbit_ode) captured from the reference
+    (tests/golden/capture_cw_ode.py): the C restatement reproduces
+    solution.y[:, -1] bit for bit and solve_ivp's function-evaluation count,
+    for t = 100 (the env step), 600 (the reference's commented-out call),
+    50 and 1000 s, incl. the all-zero state (h0 = 1e-6, error 0 -> x10 steps)."""
+    g = golden("cw_ode")
+    for a, t in enumerate(g["t"]):
+        for i, x in enumerate(g["x0"]):
+            y, nfev = oracle.cw_rk45(x, t)
+            assert np.array_equal(y, g["out"][a, i]), (t, i)
+            assert nfev == g["nfev"][a, i], (t, i, nfev)

@@ -62,6 +62,14 @@ if probe:
             print(f"  {names[k]:>14}: {int(np.median(d[0::2])):7d} | {int(np.median(d[1::2])):7d}")
         tot = b[:, 7, w, 1] - b[:, 0, w, 1]
         print(f"  {'total':>14}: {int(np.median(tot[0::2])):7d} | {int(np.median(tot[1::2])):7d}")
+    # timeline: each stamp's shader-clock time after the workgroup's wave-0
+    # start, median over workgroups, both stamped waves side by side
+    print("timeline (cycles after wave 0's start; actor wave0/waveNW2 | critic wave0/waveNW2)")
+    for k in order:
+        v0 = b[:, k, 0, 1] - b[:, 0, 0, 1]
+        v1 = b[:, k, 1, 1] - b[:, 0, 0, 1]
+        print(f"  stamp {k:2d}: {int(np.median(v0[0::2])):7d} / {int(np.median(v1[0::2])):7d} | "
+              f"{int(np.median(v0[1::2])):7d} / {int(np.median(v1[1::2])):7d}")
     cyc = (b[:, 7, 0, 1] - b[:, 0, 0, 1]).astype(np.float64)
     wall = (b[:, 7, 0, 0] - b[:, 0, 0, 0]).astype(np.float64) / 100e6
     print("shader clock over a workgroup's span (median GHz):", round(float(np.median(cyc / wall)) / 1e9, 3))
