@@ -334,6 +334,9 @@ struct Pursuer { double u, dv2, e, f0, p, r, sf0, X, sq; };
 // count can advance all four of an env's solves in one hybrdN<4>
 struct RfSolve { bool ok; double vx0, vy0, dvm, st, ct; double A[2], ag[2]; };
 
+constexpr double kSinHalfPi = 1.0;                        // sin(np.pi / 2), = -sin(-np.pi / 2)
+constexpr double kCosHalfPi = 0x1.1a62633145c07p-54;      // cos(+-np.pi / 2) = 6.123233995736766e-17
+
 SATENV_HD void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
   const double d = f_c - P.f0;
   const double sd = sin(d);
@@ -344,8 +347,13 @@ SATENV_HD void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
   q.ag[0] = kPi / 2;
   q.ag[1] = -kPi / 2;
   if (!q.ok) return;
-  const double beta = atan(0.0 / sd);                                            // tan(fai)=0, :469
-  const double sb = sin(beta), cb = cos(beta);
+  // beta = atan(0 / sd) (tan(fai) = 0, :469): for a finite non-zero sd the
+  // quotient is a signed zero, and atan / sin / cos of +-0 are exact (+-0,
+  // +-0, 1) in every IEEE libm, so the three calls drop off the chain
+  const double q0 = 0.0 / sd;
+  double sb, cb;
+  if (q0 == 0.0) { sb = q0; cb = 1.0; }
+  else { const double beta = atan(q0); sb = sin(beta); cb = cos(beta); }
   q.dvm = sqrt(P.dv2 - P.u * pow2(P.X) * pow2(sb) / P.p);                        // :470
   double theta = 0.0;
   if ((-kTwoPi <= d && d < -kPi) || (0.0 <= d && d < kPi)) theta = acos(cos(d) * 1.0);          // :473
@@ -355,30 +363,37 @@ SATENV_HD void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
   q.vy0 = P.sq * P.X * cb;                                                       // :519
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    double sg, cg;
-    sincos(q.ag[k], &sg, &cg);
+    // sincos(+-pi/2): the values OCML and glibc both return (the guesses are
+    // constants; test_env_gpu / test_oracle_golden check the identity)
+    const double sg = k == 0 ? kSinHalfPi : -kSinHalfPi, cg = kCosHalfPi;
     const double v1x = q.vx0 + q.dvm * cg, v1y = q.vy0 + q.dvm * sg;
     const double h = P.r * v1y;
     q.A[k] = (2.0 * P.u * (1.0 - q.ct)) / (h * v1y) - v1x * q.st / v1y;          // :560
   }
 }
 
+// rf of one solution alpha (:525-530 / :543-548), before abs and sort
+SATENV_HD double rf_one(const Pursuer& P, const RfSolve& q, double al) {
+  double sa, ca;
+  sincos(al, &sa, &ca);
+  const double vx = q.vx0 + q.dvm * ca, vy = q.vy0 + q.dvm * sa;                 // :525-528
+  const double hm = P.r * vy;
+  return pow2(hm) / (P.u * (1.0 - q.ct) + hm * vy * q.ct - hm * vx * q.st);     // :530
+}
+
+// abs and sort of the two rf values (:549-554); (0, 0) when temp1 < 0 (:477)
+SATENV_HD void rf_sort(bool ok, double rf0, double rf1, double& rmax, double& rmin) {
+  if (!ok) { rmax = 0.0; rmin = 0.0; return; }
+  rmax = fabs(rf0);
+  rmin = fabs(rf1);
+  if (rmax < rmin) { const double t = rmin; rmin = rmax; rmax = t; }
+}
+
 // rf from the two solutions, abs and sort (:525-530, :549-556)
 SATENV_HD void rf_finish(const Pursuer& P, const RfSolve& q, double al0, double al1, double& rmax,
                                           double& rmin) {
   if (!q.ok) { rmax = 0.0; rmin = 0.0; return; }
-  double rf[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    double sa, ca;
-    sincos(k == 0 ? al0 : al1, &sa, &ca);
-    const double vx = q.vx0 + q.dvm * ca, vy = q.vy0 + q.dvm * sa;               // :525-528
-    const double hm = P.r * vy;
-    rf[k] = pow2(hm) / (P.u * (1.0 - q.ct) + hm * vy * q.ct - hm * vx * q.st);   // :530
-  }
-  rmax = fabs(rf[0]);
-  rmin = fabs(rf[1]);
-  if (rmax < rmin) { const double t = rmin; rmin = rmax; rmax = t; }            // :549-554
+  rf_sort(true, rf_one(P, q, al0), rf_one(P, q, al1), rmax, rmin);
 }
 
 // self.Delta_V_c ** 2 by numpy scalar type
@@ -393,22 +408,24 @@ SATENV_HD double fuel_sq(double fuel, int mode) {
 // the two rf_extreme_point set-ups (up to four fsolve problems, z.q[c].A[k]
 // with guess z.q[c].ag[k], live when z.q[c].ok) and the target radii;
 // dz_finish takes the four solutions and returns the count.  Returns 0 or
-// <0 (a non-6-element orbit branch).
+// <0 (a non-6-element orbit branch).  The pieces (dz_elements, dz_pursuer,
+// dz_lat, rf_setup, dz_target_radii, rf_one / rf_sort) are what the
+// multi-wave env kernel spreads over waves; composed in this order they are
+// dz_setup / dz_finish, operation for operation.
 struct DzCtx { Pursuer P; RfSolve q[2]; double r_ft1, r_ft2; };
 
-SATENV_HD int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
-                                        double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
-                                        double Ev1, double Ev2, double fuel, int fmode, DzCtx& z) {
-  const double u = 3.986e14;                                // Time_window_of_danger_zone default u
-  Elements C, T;
-  int rc = orbital_elements(u, prm.R_cw[0] + Pp0, prm.R_cw[1] + Pp1, prm.R_cw[2] + Pp2, prm.V_cw[0] + Pv0,
-                            prm.V_cw[1] + Pv1, prm.V_cw[2] + Pv2, C);
-  if (rc) return rc;
-  rc = orbital_elements(u, prm.R_cw[0] + Ep0, prm.R_cw[1] + Ep1, prm.R_cw[2] + Ep2, prm.V_cw[0] + Ev0,
-                        prm.V_cw[1] + Ev1, prm.V_cw[2] + Ev2, T);
-  if (rc) return rc;
-  Pursuer& P = z.P;
-  P.u = u;
+constexpr double kDzMu = 3.986e14;                           // Time_window_of_danger_zone default u
+
+// the chaser's (which = 0) or the target's (1) element set from the relative state
+SATENV_HD int dz_elements(const Params& prm, double X0, double X1, double X2, double V0, double V1, double V2,
+                          Elements& out) {
+  return orbital_elements(kDzMu, prm.R_cw[0] + X0, prm.R_cw[1] + X1, prm.R_cw[2] + X2, prm.V_cw[0] + V0,
+                          prm.V_cw[1] + V1, prm.V_cw[2] + V2, out);
+}
+
+// Time_window_of_danger_zone attributes of the chaser (:54-58, :82-86)
+SATENV_HD void dz_pursuer(const Elements& C, double fuel, int fmode, Pursuer& P) {
+  P.u = kDzMu;
   P.dv2 = fuel_sq(fuel, fmode);
   P.e = C.e;
   P.f0 = C.f;
@@ -418,8 +435,12 @@ SATENV_HD int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, do
   P.X = 1.0 + C.e * cf0;
   P.p = C.a * (1.0 - pow2(C.e));                                                 // :58
   P.r = P.p / P.X;                                                               // :57 (a(1-e^2)/(1+e cos f0))
-  P.sq = sqrt(u / P.p);
-  // :317-339 latitudinal angles
+  P.sq = sqrt(kDzMu / P.p);
+}
+
+// :317-339 latitudinal angles u_c1, u_c2 = u_c1 + pi, u_t1, u_t2 = u_t1 + pi
+SATENV_HD void dz_lat(const Elements& C, const Elements& T, double& u_c1, double& u_c2, double& u_t1,
+                      double& u_t2) {
   double s_it, c_it, s_ic, c_ic, s_d, c_d;
   sincos(T.i, &s_it, &c_it);
   sincos(C.i, &s_ic, &c_ic);
@@ -428,13 +449,39 @@ SATENV_HD int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, do
   double temp1 = (s_it * s_d) / (c_it * s_ic - s_it * c_ic * c_d);
   double temp2 = (s_ic * s_dn) / (c_ic * s_it - s_ic * c_it * c_dn);
   if (temp1 != temp1 || temp2 != temp2) { temp1 = 1.0; temp2 = 1.0; }         // :331-332
-  const double u_c1 = atan(temp1), u_c2 = kPi + u_c1;
-  const double u_t1 = atan(temp2), u_t2 = u_t1 + kPi;
-  rf_setup(P, u_c1 - C.omega, z.q[0]);                                           // rf_extreme_point('orbit_c1')
-  rf_setup(P, u_c2 - C.omega, z.q[1]);                                           // ('orbit_c2')
+  u_c1 = atan(temp1);
+  u_c2 = kPi + u_c1;
+  u_t1 = atan(temp2);
+  u_t2 = u_t1 + kPi;
+}
+
+// :363-365 target radii, cross-wired as in the reference (r_ft1 from f_t2)
+SATENV_HD void dz_target_radii(const Elements& T, double u_t1, double u_t2, double& r_ft1, double& r_ft2) {
   const double pt = T.a * (1.0 - pow2(T.e));
-  z.r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                             // :363 (cross-wired f_t2)
-  z.r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                             // :365
+  r_ft1 = pt / (1.0 + T.e * cos(u_t2 - T.omega));                               // :363 (cross-wired f_t2)
+  r_ft2 = pt / (1.0 + T.e * cos(u_t1 - T.omega));                               // :365
+}
+
+// the count from the two (rmax, rmin) pairs and the target radii (:367-372)
+SATENV_HD int dz_count(double mx1, double mn1, double mx2, double mn2, double r_ft1, double r_ft2) {
+  const bool in1 = (mn1 <= r_ft1 && r_ft1 <= mx1), in2 = (mn2 <= r_ft2 && r_ft2 <= mx2);
+  return (in1 && in2) ? 2 : ((in1 || in2) ? 1 : 0);
+}
+
+SATENV_HD int dz_setup(const Params& prm, double Pp0, double Pp1, double Pp2, double Pv0,
+                                        double Pv1, double Pv2, double Ep0, double Ep1, double Ep2, double Ev0,
+                                        double Ev1, double Ev2, double fuel, int fmode, DzCtx& z) {
+  Elements C, T;
+  int rc = dz_elements(prm, Pp0, Pp1, Pp2, Pv0, Pv1, Pv2, C);
+  if (rc) return rc;
+  rc = dz_elements(prm, Ep0, Ep1, Ep2, Ev0, Ev1, Ev2, T);
+  if (rc) return rc;
+  dz_pursuer(C, fuel, fmode, z.P);
+  double u_c1, u_c2, u_t1, u_t2;
+  dz_lat(C, T, u_c1, u_c2, u_t1, u_t2);
+  rf_setup(z.P, u_c1 - C.omega, z.q[0]);                                         // rf_extreme_point('orbit_c1')
+  rf_setup(z.P, u_c2 - C.omega, z.q[1]);                                         // ('orbit_c2')
+  dz_target_radii(T, u_t1, u_t2, z.r_ft1, z.r_ft2);
   return 0;
 }
 
@@ -443,8 +490,7 @@ SATENV_HD int dz_finish(const DzCtx& z, const double (&al)[4]) {
   double mx1, mn1, mx2, mn2;
   rf_finish(z.P, z.q[0], al[0], al[1], mx1, mn1);
   rf_finish(z.P, z.q[1], al[2], al[3], mx2, mn2);
-  const bool in1 = (mn1 <= z.r_ft1 && z.r_ft1 <= mx1), in2 = (mn2 <= z.r_ft2 && z.r_ft2 <= mx2);
-  return (in1 && in2) ? 2 : ((in1 || in2) ? 1 : 0);
+  return dz_count(mx1, mn1, mx2, mn2, z.r_ft1, z.r_ft2);
 }
 
 // the whole count in one lane (the four solves one after another)

@@ -44,6 +44,19 @@ int fail(int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(SATENV_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
   } while (0)
 
+#ifdef SATENV_PHASE_PROBE
+// development-only phase stamps of step_kernel_wide (tools/env_phase_probe.py),
+// never in the shipped build: [workgroup][stamp][wave][s_memtime]
+__device__ unsigned long long g_env_probe[1024][8][4];
+#define ENV_PROBE(k)                                                                  \
+  do {                                                                                \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                                 \
+      g_env_probe[blockIdx.x][k][threadIdx.x >> 6] = clock64();                       \
+  } while (0)
+#else
+#define ENV_PROBE(k) do {} while (0)
+#endif
+
 // wave-level reduction of the per-step stats, one f64 atomic per wave and counter
 __device__ __forceinline__ void wave_stats(double* stats, double fin, double fin_ret, double rew, double cap) {
 #pragma unroll
@@ -147,6 +160,186 @@ __global__ void __launch_bounds__(256) step_kernel_split(const Params prm, int64
     step_end(prm, n, f64, i32, io, i, AUTORESET, L, fin, fin_ret, rew_acc);
   }
   if (w == 0 && io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
+}
+
+// 64 envs per 4-wave workgroup with the whole per-env chain spread over the
+// waves, not only the four solves (step_kernel_split keeps the rest of the
+// chain in wave 0).  Between barriers, per env:
+//   I   wave 0: step_begin (state, actions, fuel, propagation, terminal tests)
+//   II  wave 0: chaser elements | wave 1: target elements | wave 2: the
+//       count-independent reward terms (three cosine similarities, pv4)
+//   II' wave 0 also: the chaser's set-up (dz_pursuer) for both waves of III
+//   III wave 0: latitudinal angles, rf_setup('orbit_c1') | wave 1: the same
+//       angles, rf_setup('orbit_c2') | wave 2: the angles, the target radii
+//   IV  wave w: fsolve problem w (rf_extreme_point w>>1, guess w&1) and the
+//       rf value of its solution
+//   V   wave 0: sort, count, reward, outputs, autoreset, state write-back
+// Every value is computed by the functions dz_setup / dz_finish /
+// step_reward are composed of, in the same order, so the kernel is
+// bit-identical to step_kernel_split (and to the host build where the libm
+// agrees); only the schedule differs.  Phases II-IV each shorten wave 0's
+// dependent FP64 chain (OCML acos/atan/sincos latency) by running next to it.
+template <int E>
+struct WideSmem {
+  double k[12][E];          // state after the propagation
+  float pa[3][E];
+  int live[E];              // bit 0: count needed (non-terminal), bit 1: pursuer frozen (p_zero)
+  double fuel[E];
+  int fcm[E];
+  double C[6][E], T[6][E];
+  int rc[2][E];
+  double rt[4][E];          // reward terms
+  double P[9][E];                    // the chaser's Pursuer set-up (dz_pursuer), from phase II
+  double qA[4][E], qAg[4][E], qSt[2][E], qCt[2][E], qDvm[2][E],
+      qVx0[2][E], qVy0[2][E];
+  int qOk[2][E];
+  double rft[2][E];
+  double rf[4][E];
+};
+
+template <int E>
+__device__ __forceinline__ void put_elements(double (*dst)[E], int lane, const Elements& el) {
+  dst[0][lane] = el.a; dst[1][lane] = el.e; dst[2][lane] = el.i;
+  dst[3][lane] = el.omega; dst[4][lane] = el.Omega; dst[5][lane] = el.f;
+}
+template <int E>
+__device__ __forceinline__ Elements get_elements(const double (*src)[E], int lane) {
+  Elements el;
+  el.a = src[0][lane]; el.e = src[1][lane]; el.i = src[2][lane];
+  el.omega = src[3][lane]; el.Omega = src[4][lane]; el.f = src[5][lane];
+  return el;
+}
+
+// ENVS envs per workgroup (lanes >= ENVS of each wave idle): fewer envs per
+// wave put more waves, i.e. more independent dependency chains, on each SIMD
+// when N is small (the step is latency bound there); 64 at large N
+template <bool AUTORESET, int ENVS>
+__global__ void __launch_bounds__(256) step_kernel_wide(const Params prm, int64_t n, double* __restrict__ f64,
+                                                        int32_t* __restrict__ i32, StepIO io) {
+  __shared__ WideSmem<ENVS> sm;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool env_lane = lane < ENVS;
+  const int64_t i = (int64_t)blockIdx.x * ENVS + lane;
+  const bool in_range = env_lane && i < n;
+  Lane L;
+  double fin = 0.0, fin_ret = 0.0, rew_acc = 0.0, cap = 0.0;
+  ENV_PROBE(0);
+  // ---- I -------------------------------------------------------------------
+  if (w == 0) {
+    int live = 0;
+    if (in_range) {
+      step_begin(prm, n, f64, i32, io, i, AUTORESET, L);
+      if (L.err) atomicCAS(io.err, 0, L.err);
+      cap = L.cap;
+      live = L.terminal ? 0 : (1 | (L.p_zero ? 2 : 0));
+#pragma unroll
+      for (int c = 0; c < 12; ++c) sm.k[c][lane] = L.k[c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) sm.pa[c][lane] = L.pa[c];
+      sm.fuel[lane] = L.fuel_c;
+      sm.fcm[lane] = L.fcm;
+    }
+    if (env_lane) sm.live[lane] = live;
+  }
+  ENV_PROBE(1);
+  __syncthreads();
+  const int live = env_lane ? sm.live[lane] : 0;
+  // ---- II ------------------------------------------------------------------
+  if (live & 1) {
+    if (w <= 1) {
+      Elements E;
+      const int o = 6 * w;                                    // chaser: Pp/Pv, target: Ep/Ev
+      const int rc = dz_elements(prm, sm.k[o][lane], sm.k[o + 1][lane], sm.k[o + 2][lane], sm.k[o + 3][lane],
+                                 sm.k[o + 4][lane], sm.k[o + 5][lane], E);
+      put_elements<ENVS>(w == 0 ? sm.C : sm.T, lane, E);
+      sm.rc[w][lane] = rc;
+      if (w == 0 && rc == 0) {                                  // the chaser's set-up, off phase III's path
+        Pursuer P;
+        dz_pursuer(E, sm.fuel[lane], sm.fcm[lane], P);
+        sm.P[0][lane] = P.u; sm.P[1][lane] = P.dv2; sm.P[2][lane] = P.e; sm.P[3][lane] = P.f0;
+        sm.P[4][lane] = P.p; sm.P[5][lane] = P.r; sm.P[6][lane] = P.sf0; sm.P[7][lane] = P.X;
+        sm.P[8][lane] = P.sq;
+      }
+    } else if (w == 2) {
+      double k[12], t[4];
+      float pa[3];
+#pragma unroll
+      for (int c = 0; c < 12; ++c) k[c] = sm.k[c][lane];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pa[c] = sm.pa[c][lane];
+      reward_terms(k, pa, (live & 2) != 0, t);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sm.rt[c][lane] = t[c];
+    }
+  }
+  ENV_PROBE(2);
+  __syncthreads();
+  // ---- III -----------------------------------------------------------------
+  const bool ok_el = (live & 1) && sm.rc[0][lane] == 0 && sm.rc[1][lane] == 0;
+  if (ok_el && w <= 2) {
+    const Elements C = get_elements<ENVS>(sm.C, lane), T = get_elements<ENVS>(sm.T, lane);
+    double u_c1, u_c2, u_t1, u_t2;
+    dz_lat(C, T, u_c1, u_c2, u_t1, u_t2);
+    if (w <= 1) {
+      Pursuer P;
+      P.u = sm.P[0][lane]; P.dv2 = sm.P[1][lane]; P.e = sm.P[2][lane]; P.f0 = sm.P[3][lane];
+      P.p = sm.P[4][lane]; P.r = sm.P[5][lane]; P.sf0 = sm.P[6][lane]; P.X = sm.P[7][lane];
+      P.sq = sm.P[8][lane];
+      RfSolve q;
+      rf_setup(P, (w == 0 ? u_c1 : u_c2) - C.omega, q);         // rf_extreme_point('orbit_c1' / 'orbit_c2')
+      sm.qOk[w][lane] = q.ok ? 1 : 0;
+      sm.qA[2 * w][lane] = q.A[0]; sm.qA[2 * w + 1][lane] = q.A[1];
+      sm.qAg[2 * w][lane] = q.ag[0]; sm.qAg[2 * w + 1][lane] = q.ag[1];
+      sm.qSt[w][lane] = q.st; sm.qCt[w][lane] = q.ct; sm.qDvm[w][lane] = q.dvm;
+      sm.qVx0[w][lane] = q.vx0; sm.qVy0[w][lane] = q.vy0;
+    } else {
+      double r1, r2;
+      dz_target_radii(T, u_t1, u_t2, r1, r2);
+      sm.rft[0][lane] = r1; sm.rft[1][lane] = r2;
+    }
+  }
+  ENV_PROBE(3);
+  __syncthreads();
+  // ---- IV: problem w = (rf_extreme_point c = w >> 1, guess k = w & 1) ------
+  if (ok_el) {
+    const int c = w >> 1;
+    if (sm.qOk[c][lane]) {
+      RfSolve q;
+      q.ok = true;
+      q.st = sm.qSt[c][lane]; q.ct = sm.qCt[c][lane]; q.dvm = sm.qDvm[c][lane];
+      q.vx0 = sm.qVx0[c][lane]; q.vy0 = sm.qVy0[c][lane];
+      const double al = hybrd1(sm.qA[w][lane], q.st, q.dvm, sm.qAg[w][lane]);
+      Pursuer P;
+      P.u = kDzMu;
+      P.r = sm.P[5][lane];
+      sm.rf[w][lane] = rf_one(P, q, al);
+    }
+  }
+  ENV_PROBE(4);
+  __syncthreads();
+  ENV_PROBE(5);
+  // ---- V -------------------------------------------------------------------
+  if (w == 0 && in_range) {
+    if (!L.terminal) {
+      int cnt = 0;
+      const int rc = sm.rc[0][lane] ? sm.rc[0][lane] : sm.rc[1][lane];
+      if (rc) {
+        atomicCAS(io.err, 0, rc);
+      } else {
+        double mx1, mn1, mx2, mn2;
+        rf_sort(sm.qOk[0][lane] != 0, sm.rf[0][lane], sm.rf[1][lane], mx1, mn1);
+        rf_sort(sm.qOk[1][lane] != 0, sm.rf[2][lane], sm.rf[3][lane], mx2, mn2);
+        cnt = dz_count(mx1, mn1, mx2, mn2, sm.rft[0][lane], sm.rft[1][lane]);
+      }
+      double t[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] = sm.rt[c][lane];
+      step_reward_terms(prm, L, cnt, t);
+    }
+    step_end(prm, n, f64, i32, io, i, AUTORESET, L, fin, fin_ret, rew_acc);
+  }
+  if (w == 0 && io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
+  ENV_PROBE(6);
 }
 
 __global__ void __launch_bounds__(256) reset_kernel(const Params prm, int64_t n, double* __restrict__ f64,
@@ -330,8 +523,7 @@ __global__ void __launch_bounds__(kRdBlock) rd_kernel(const satenv_rd_orbit* __r
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const double ag = s == 0 ? kPi / 2 : -kPi / 2;                           // :93, :109
-      double sgs, cgs;
-      sincos(ag, &sgs, &cgs);
+      const double sgs = s == 0 ? kSinHalfPi : -kSinHalfPi, cgs = kCosHalfPi;   // sincos(ag)
       const double v1x = vx0 + dvm * cgs, v1y = vy0 + dvm * sgs;
       const double h = r0 * v1y;                                                // :98
       const double A = (2.0 * o.mu * (1.0 - ct)) / (h * v1y) - v1x * st / v1y; // :152
@@ -465,24 +657,68 @@ struct satenv_env {
   double* f64 = nullptr;
   int32_t* i32 = nullptr;
   int32_t* err = nullptr;
-  int split = 1;   // step_kernel_split (1) or the one-lane step_kernel (0)
+  int split = 2;   // step_kernel_wide (2), step_kernel_split (1) or the one-lane step_kernel (0)
 };
 
 namespace {
 
 int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
-// env-step kernel choice (SATENV_STEP_SPLIT=0 forces the one-lane kernel: dev A/B)
+// env-step kernel choice (dev A/B: SATENV_STEP_SPLIT=0 the one-lane kernel,
+// 1 the four-solve split kernel, 2 the wide kernel)
 int pick_split(int64_t n) {
   (void)n;
   const char* e = std::getenv("SATENV_STEP_SPLIT");
-  if (e && e[0] == '0') return 0;
-  return 1;
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] - '0';
+  return 2;
+}
+
+// envs per workgroup of the wide kernel (dev A/B: SATENV_WIDE_ENVS = 16/32/64)
+int wide_envs(int64_t n) {
+  const char* e = std::getenv("SATENV_WIDE_ENVS");
+  if (e) {
+    const int v = std::atoi(e);
+    if (v == 16 || v == 32 || v == 64) return v;
+  }
+  return 64;
+}
+
+template <bool AR>
+void launch_step(satenv_env* h, const StepIO& io, void* stream) {
+  const dim3 grid(grid_for(h->n, kSplitEnvs));
+  if (h->prm.propagator == 2)   // the RK45 instantiation (its registers stay out of the STM kernels)
+    hipLaunchKernelGGL((step_kernel_split<AR, true>), grid, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
+                       h->i32, io);
+  else if (h->split == 2) {
+    const int envs = wide_envs(h->n);
+    const dim3 gw(grid_for(h->n, envs));
+    if (envs == 16)
+      hipLaunchKernelGGL((step_kernel_wide<AR, 16>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
+                         h->i32, io);
+    else if (envs == 32)
+      hipLaunchKernelGGL((step_kernel_wide<AR, 32>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
+                         h->i32, io);
+    else
+      hipLaunchKernelGGL((step_kernel_wide<AR, 64>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
+                         h->i32, io);
+  }
+  else if (h->split == 1)
+    hipLaunchKernelGGL(step_kernel_split<AR>, grid, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64, h->i32,
+                       io);
+  else
+    hipLaunchKernelGGL(step_kernel<AR>, dim3(grid_for(h->n, 64)), dim3(64), 0, (hipStream_t)stream, h->prm, h->n,
+                       h->f64, h->i32, io);
 }
 
 }  // namespace
 
 extern "C" {
+
+#ifdef SATENV_PHASE_PROBE
+int satenv_probe_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_env_probe), sizeof(g_env_probe)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char* satenv_last_error(void) { return g_last_error.c_str(); }
 int satenv_abi_version(void) { return SATENV_ABI_VERSION; }
@@ -594,15 +830,7 @@ int satenv_step(satenv_env* h, const float* pa, const float* ea, const int32_t* 
                 double* obs64_out, double* reward_out, uint8_t* done_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step: null argument");
   StepIO io{pa, ea, episode_count, obs_out, obs64_out, reward_out, nullptr, done_out, nullptr, h->err};
-  if (h->prm.propagator == 2)   // the RK45 instantiation (its registers stay out of the STM kernels)
-    hipLaunchKernelGGL((step_kernel_split<false, true>), dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0,
-                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
-  else if (h->split)
-    hipLaunchKernelGGL(step_kernel_split<false>, dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0, (hipStream_t)stream,
-                       h->prm, h->n, h->f64, h->i32, io);
-  else
-    hipLaunchKernelGGL(step_kernel<false>, dim3(grid_for(h->n, 64)), dim3(64), 0, (hipStream_t)stream, h->prm, h->n,
-                       h->f64, h->i32, io);
+  launch_step<false>(h, io, stream);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }
@@ -611,15 +839,7 @@ int satenv_step_autoreset(satenv_env* h, const float* pa, const float* ea, float
                           uint8_t* done_out, double* stats_out, void* stream) {
   if (!h || !pa || !ea) return fail(SATENV_ERR_ARG, "satenv_step_autoreset: null argument");
   StepIO io{pa, ea, nullptr, obs_out, nullptr, nullptr, reward_out, done_out, stats_out, h->err};
-  if (h->prm.propagator == 2)   // the RK45 instantiation (its registers stay out of the STM kernels)
-    hipLaunchKernelGGL((step_kernel_split<true, true>), dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0,
-                       (hipStream_t)stream, h->prm, h->n, h->f64, h->i32, io);
-  else if (h->split)
-    hipLaunchKernelGGL(step_kernel_split<true>, dim3(grid_for(h->n, kSplitEnvs)), dim3(256), 0, (hipStream_t)stream,
-                       h->prm, h->n, h->f64, h->i32, io);
-  else
-    hipLaunchKernelGGL(step_kernel<true>, dim3(grid_for(h->n, 64)), dim3(64), 0, (hipStream_t)stream, h->prm, h->n,
-                       h->f64, h->i32, io);
+  launch_step<true>(h, io, stream);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

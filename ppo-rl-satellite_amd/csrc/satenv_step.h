@@ -186,29 +186,41 @@ SATENV_HD void step_begin(const Params& prm, int64_t n, const double* __restrict
   }
 }
 
-// non-terminal reward with the new danger-zone count (:150, :161-175, :251)
-SATENV_HD void step_reward(const Params& prm, Lane& L, int cnt) {
-  const double* k = L.k;
+// the count-independent reward terms 1*pv1, 0.6*pv2, 0.2*pv3, 2*pv4 (:166-175)
+SATENV_HD void reward_terms(const double (&k)[12], const float (&pa)[3], bool p_zero, double (&t)[4]) {
   const double r0 = k[0] - k[6], r1 = k[1] - k[7], r2 = k[2] - k[8];
-  L.dz = cnt;
-  double r = (L.dis < L.dis_prev) ? 1.0 : -1.0;                          // :161-164
-  r += (prm.d_capture <= L.dis && L.dis <= 4 * prm.d_capture) ? -1.0 : -2.0;
-  r += (L.dz == 0) ? -1.0 : L.dz * 0.5;
   const double pv1 = cos_sim(k[0], k[1], k[2], k[6], k[7], k[8]);       // reward_of_action3
   const double pv2 = cos_sim(k[3], k[4], k[5], k[9], k[10], k[11]);     // reward_of_action1
   const double pv3 = cos_sim(r0, r1, r2, k[3], k[4], k[5]);             // reward_of_action2
   double pv4 = 0.0;                                                      // reward_of_action4, :388
-  const float* pa = L.pa;
-  if (!L.p_zero && pa[0] != 0.0f && pa[1] != 0.0f && pa[2] != 0.0f) {
+  if (!p_zero && pa[0] != 0.0f && pa[1] != 0.0f && pa[2] != 0.0f) {
     const double nr = norm3(r0, r1, r2);
     const float na = norm3f(pa[0], pa[1], pa[2]);
     pv4 = -dot3(r0 / nr, r1 / nr, r2 / nr, (double)(pa[0] / na), (double)(pa[1] / na), (double)(pa[2] / na));
   }
-  r += 1 * pv1;
-  r += 0.6 * pv2;
-  r += 0.2 * pv3;
-  r += 2 * pv4;
+  t[0] = 1 * pv1;
+  t[1] = 0.6 * pv2;
+  t[2] = 0.2 * pv3;
+  t[3] = 2 * pv4;
+}
+
+// non-terminal reward with the new danger-zone count (:150, :161-175, :251)
+SATENV_HD void step_reward_terms(const Params& prm, Lane& L, int cnt, const double (&t)[4]) {
+  L.dz = cnt;
+  double r = (L.dis < L.dis_prev) ? 1.0 : -1.0;                          // :161-164
+  r += (prm.d_capture <= L.dis && L.dis <= 4 * prm.d_capture) ? -1.0 : -2.0;
+  r += (L.dz == 0) ? -1.0 : L.dz * 0.5;
+  r += t[0];
+  r += t[1];
+  r += t[2];
+  r += t[3];
   L.reward = L.flag == 0 ? r : -r;                                        // :251
+}
+
+SATENV_HD void step_reward(const Params& prm, Lane& L, int cnt) {
+  double t[4];
+  reward_terms(L.k, L.pa, L.p_zero, t);
+  step_reward_terms(prm, L, cnt, t);
 }
 
 SATENV_HD void step_end(const Params& prm, int64_t n, double* __restrict__ f64,

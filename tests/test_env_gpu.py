@@ -78,6 +78,14 @@ def test_straight_line_sincos_is_the_library_sincos(satrl_env):
         res.append((s.cpu().numpy().view(np.int64), c.cpu().numpy().view(np.int64)))
     (s0, c0), (s1, c1) = res
     assert np.array_equal(s0, s1) and np.array_equal(c0, c1)
+    # the fsolve guesses' sincos(+-pi/2) are constants in the kernels
+    # (satenv_device.h kSinHalfPi / kCosHalfPi): the library's values
+    xs = torch.tensor([np.pi / 2, -np.pi / 2], dtype=torch.float64, device="cuda")
+    s = torch.empty(2, dtype=torch.float64, device="cuda")
+    c = torch.empty(2, dtype=torch.float64, device="cuda")
+    _lib.check(_lib.lib().satenv_sincos(2, _lib.ptr(xs), _lib.ptr(s), _lib.ptr(c), 1, _lib.stream_ptr()),
+               "satenv_sincos")
+    assert s.tolist() == [1.0, -1.0] and c.tolist() == [float.fromhex("0x1.1a62633145c07p-54")] * 2
 
 
 def test_danger_zone_counts(satrl_env, oracle):

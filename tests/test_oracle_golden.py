@@ -289,3 +289,12 @@ def test_cw_rk45_restatement_bitexact(oracle):
             y, nfev = oracle.cw_rk45(x, t)
             assert np.array_equal(y, g["out"][a, i]), (t, i)
             assert nfev == g["nfev"][a, i], (t, i, nfev)
+
+
+def test_guess_sincos_constants_are_glibc():
+    """satenv_device.h's kSinHalfPi / kCosHalfPi (the fsolve guesses +-pi/2
+    of satellite_function.py:516/:534 and RD_single_pulse.py:93/:109) are
+    what glibc (the host build, the reference) returns."""
+    import math
+    assert math.sin(math.pi / 2) == 1.0 and math.sin(-math.pi / 2) == -1.0
+    assert math.cos(math.pi / 2) == math.cos(-math.pi / 2) == float.fromhex("0x1.1a62633145c07p-54")
