@@ -24,14 +24,13 @@ thread_local std::string g_err;
 
 #ifdef SATRL_PHASE_PROBE
 // development-only phase stamps (tools/_probe/phase_probe.py), never in the
-// shipped build: [workgroup][stamp][wave 0 | wave NW/2][s_memrealtime, s_memtime]
-__device__ unsigned long long g_probe[4096][16][2][2];
+// shipped build: [workgroup][stamp][wave][s_memrealtime, s_memtime]
+__device__ unsigned long long g_probe[512][16][16][2];
 #define PHASE_PROBE(k)                                                        \
   do {                                                                        \
-    if (threadIdx.x == 0 || threadIdx.x == blockDim.x / 2) {                  \
-      const int pw_ = threadIdx.x == 0 ? 0 : 1;                               \
-      g_probe[blockIdx.x][k][pw_][0] = wall_clock64();                        \
-      g_probe[blockIdx.x][k][pw_][1] = clock64();                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) {                        \
+      g_probe[blockIdx.x][k][threadIdx.x >> 6][0] = wall_clock64();           \
+      g_probe[blockIdx.x][k][threadIdx.x >> 6][1] = clock64();                \
     }                                                                         \
   } while (0)
 #else
@@ -521,6 +520,12 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
   const int rb = net_sel < 0 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, n0 = w * (H / NW);
   const int r0 = rb * R;
   auto& S = sm.S;
+#ifdef SATRL_PHASE_PROBE
+  if (threadIdx.x == 0 && blockIdx.x < 512) {   // placement: XCC_ID and HW_ID (SE/SH/CU) of the workgroup
+    g_probe[blockIdx.x][15][0][0] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    g_probe[blockIdx.x][15][0][1] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
+#endif
   PHASE_PROBE(0);
   // the head's output-layer bias / log_std (uniform: scalar loads issued now,
   // long landed when the head runs)

@@ -47,45 +47,22 @@ torch.cuda.synchronize()
 
 if probe:
     lib = _L.lib()
-    buf = np.zeros((4096, 16, 2, 2), dtype=np.uint64)
+    buf = np.zeros((512, 16, 16, 2), dtype=np.uint64)
     lib.satrl_probe_read.argtypes = [C.c_void_p]
     assert lib.satrl_probe_read(buf.ctypes.data) == 0
-    nwg = 2 * (mb // 32)
-    b = buf[:nwg].astype(np.int64)
+    b = buf.astype(np.int64)                     # [wg][stamp][wave][realtime, shader clock]
     order = [0, 8, 9, 10, 11, 1, 2, 3, 4, 5, 6, 7]
-    names = ["gather issue", "S ready+w3", "fc1 mfma", "tanh h1 store", "barrier", "B fc2", "C fwd",
-             "C head", "C tail", "D dH1", "E dW1"]
-    for w in (0, 1):
-        print(f"wave {'0' if w == 0 else 'NW/2'}: phase cycles (median over workgroups, actor | critic)")
-        for k in range(len(order) - 1):
-            d = b[:, order[k + 1], w, 1] - b[:, order[k], w, 1]
-            print(f"  {names[k]:>14}: {int(np.median(d[0::2])):7d} | {int(np.median(d[1::2])):7d}")
-        tot = b[:, 7, w, 1] - b[:, 0, w, 1]
-        print(f"  {'total':>14}: {int(np.median(tot[0::2])):7d} | {int(np.median(tot[1::2])):7d}")
-    # timeline: each stamp's shader-clock time after the workgroup's wave-0
-    # start, median over workgroups, both stamped waves side by side
-    print("timeline (cycles after wave 0's start; actor wave0/waveNW2 | critic wave0/waveNW2)")
-    for k in order:
-        v0 = b[:, k, 0, 1] - b[:, 0, 0, 1]
-        v1 = b[:, k, 1, 1] - b[:, 0, 0, 1]
-        print(f"  stamp {k:2d}: {int(np.median(v0[0::2])):7d} / {int(np.median(v1[0::2])):7d} | "
-              f"{int(np.median(v0[1::2])):7d} / {int(np.median(v1[1::2])):7d}")
+    t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
+    print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
+          "(median over workgroups), waves 0..15; actor rows then critic rows")
+    for net, sl in (("actor", slice(0, None, 2)), ("critic", slice(1, None, 2))):
+        print(f"  {net}")
+        for k in order:
+            v = b[sl, k, :, 1] - t0[sl, None]
+            print(f"    stamp {k:2d}: " + " ".join(f"{int(x):6d}" for x in np.median(v, axis=0)))
     cyc = (b[:, 7, 0, 1] - b[:, 0, 0, 1]).astype(np.float64)
     wall = (b[:, 7, 0, 0] - b[:, 0, 0, 0]).astype(np.float64) / 100e6
     print("shader clock over a workgroup's span (median GHz):", round(float(np.median(cyc / wall)) / 1e9, 3))
-    rt = b[:, 0, 0, 0]
-    print("start spread (realtime ticks, 100 MHz):", int(rt.max() - rt.min()),
-          " end spread:", int(b[:, 7, 0, 0].max() - b[:, 7, 0, 0].min()),
-          " kernel span:", int(b[:, 7, 0, 0].max() - rt.min()))
-    # where the tail comes from: end times (ticks after the first start) by
-    # XCD (round-robin dispatch: blockIdx % 8; the actor on even ones) and
-    # the start of phase B / D (stamps 1 and 5) per XCD
-    end = b[:, 7, 0, 0] - rt.min()
-    for name, k in (("start B", 1), ("start D", 5), ("end", 7)):
-        v = b[:, k, 0, 0] - rt.min()
-        print(f"  {name:>8} by XCD (median / max ticks):",
-              " ".join(f"{int(np.median(v[x::8]))}/{int(v[x::8].max())}" for x in range(8)))
-    print("  slowest 8 workgroups:", [(int(i), int(end[i])) for i in np.argsort(end)[-8:]])
 
 # event timings of each launch of one minibatch step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
