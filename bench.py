@@ -373,7 +373,7 @@ def main():
               - timed_run(a.kernel_iters, roll_policy_only, 30.0))
     env_ev_us, env_med = timed_pairs(a.kernel_iters, roll_step, 40.0)
     env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
-    env_prof_us = prof_avg_us("step_kernel_split<true>")
+    env_prof_us = prof_avg_us("step_kernel_wide<true;64>")
     env_traffic = pmc("env", num_envs=a.num_envs)
     env = tr.env
     pa = tr.buf.act[0].clone()
@@ -558,7 +558,7 @@ def main():
                                            "bytes/launch)",
                          "note": "f32 MFMA; one net per workgroup of 32 rows, each streams that net's fc2 weights "
                                  "from L2 per phase (DESIGN.md 3.4)"},
-            "roofline_env": {"kernel": "satenv step_kernel_split<autoreset> (hand-written HIP, FP64)", "bound": "hbm",
+            "roofline_env": {"kernel": "satenv step_kernel_wide<autoreset, 64> (hand-written HIP, FP64)", "bound": "hbm",
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
                              "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
                              "num_envs": a.num_envs,

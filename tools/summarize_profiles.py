@@ -62,7 +62,7 @@ def main():
         f_kb, nf = pmc_per_dispatch(fetch, "step_kernel", "FETCH_SIZE", last=40)
         w_kb, nw = pmc_per_dispatch(write, "step_kernel", "WRITE_SIZE", last=40)
         n = 16384
-        res = {"kernel": "satenv step_kernel<true>", "num_envs": n, "dispatches": [nf, nw],
+        res = {"kernel": "satenv step_kernel_wide<true, 64>", "num_envs": n, "dispatches": [nf, nw],
                "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
                "fetch_bytes_per_env_raw": f_kb * 1024.0 / n, "write_bytes_per_env": w_kb * 1024.0 / n,
                "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
