@@ -52,6 +52,8 @@ if probe:
     assert lib.satrl_probe_read(buf.ctypes.data) == 0
     b = buf.astype(np.int64)                     # [wg][stamp][wave][realtime, shader clock]
     order = [0, 8, 9, 10, 11, 1, 2, 3, 4, 5, 6, 7]
+    if os.environ.get("SATRL_ROWPASS", "") != "classic":   # the pipelined kernel's stamps
+        order = [0, 8, 1, 9, 2, 10, 3, 11, 4, 12, 5, 7]
     t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
     print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
           "(median over workgroups), waves 0..15; actor rows then critic rows")
@@ -60,9 +62,23 @@ if probe:
         for k in order:
             v = b[sl, k, :, 1] - t0[sl, None]
             print(f"    stamp {k:2d}: " + " ".join(f"{int(x):6d}" for x in np.median(v, axis=0)))
-    cyc = (b[:, 7, 0, 1] - b[:, 0, 0, 1]).astype(np.float64)
-    wall = (b[:, 7, 0, 0] - b[:, 0, 0, 0]).astype(np.float64) / 100e6
-    print("shader clock over a workgroup's span (median GHz):", round(float(np.median(cyc / wall)) / 1e9, 3))
+    if os.environ.get("PROBE_RAW"):
+        for wg in (0, 1, 100):
+            print(f"raw wg {wg}: stamp: realtime ticks rel / clock rel (waves 0, 4, 8, 15)")
+            rt0 = b[wg, 0, :, 0].min()
+            ck0 = b[wg, 0, :, 1].min()
+            for k in order:
+                print(f"   {k:2d}: " + "  ".join(f"{int(b[wg, k, w_, 0] - rt0):6d}/{int(b[wg, k, w_, 1] - ck0):7d}"
+                                             for w_ in (0, 4, 8, 15)))
+    nwg = 2 * (mb // 32)
+    st = b[:nwg, 0, :, 0].min(axis=1)
+    en = b[:nwg, 7, :, 0].max(axis=1)
+    cyc = (b[:nwg, 7, :, 1].max(axis=1) - b[:nwg, 0, :, 1].min(axis=1)).astype(np.float64)
+    wall = (en - st).astype(np.float64) / 100e6
+    print("workgroup span: median %.2f us, max %.2f us; shader clock over it (median GHz) %.3f" %
+          (np.median(wall) * 1e6, wall.max() * 1e6, float(np.median(cyc / wall)) / 1e9))
+    print("start spread %.2f us, end spread %.2f us, kernel span %.2f us" %
+          ((st.max() - st.min()) / 100.0, (en.max() - en.min()) / 100.0, (en.max() - st.min()) / 100.0))
 
 # event timings of each launch of one minibatch step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
