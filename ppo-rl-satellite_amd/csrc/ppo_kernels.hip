@@ -720,403 +720,6 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
 }
 
 // ---------------------------------------------------------------------------
-// rowpass, software-pipelined (H = 256): the same per-row work as
-// rowpass_kernel, but the workgroup's 16 waves form two row groups (waves
-// 0-7: rows 0-15, waves 8-15: rows 16-31; every wave owns 32 columns = two
-// 16-column tiles for its group's 16 rows) that run the phases offset by
-// one stage, so one group's MFMA phase overlaps the other's non-MFMA phase:
-//   stage   1      2      3          4          5          6
-//   group 0 A      B      C          D          E          -
-//   group 1 A      (W2)   B          C          D          E
-// Stages end at workgroup barriers; C's two internal syncs are group-local
-// (LDS counter).  The MFMA sequence of every output element, the output
-// layer's tile-by-tile partials and their sum (out_sum over 16 tiles) are
-// those of mlp_forward, so the forward -- logp, the head -- is bitwise the
-// rollout policy kernel's.  The row sums over the workgroup's 32 rows
-// (tail, [dW1|db1] and head partials) are group 0's 16 rows + group 1's 16
-// rows in that order: fixed, deterministic.
-// ---------------------------------------------------------------------------
-#ifndef SATRL_ROWPASS_PIPE
-#define SATRL_ROWPASS_PIPE 1
-#endif
-
-struct PipeSmem {
-  static constexpr int H = 256, LDA = H + 4, LDS_S = 36;
-  float S[2][16][LDS_S] __attribute__((aligned(16)));   // [s | 1 | 0..] per group row
-  float h1s[2][16][LDA] __attribute__((aligned(16)));   // tanh(fc1): B's operand, E's derivative
-  float dzs[2][16][LDA] __attribute__((aligned(16)));   // dZ2: D's operand
-  float b2w3[4][H];                                     // fc2 bias, output-layer weights of the net
-  float osum[2][16][16][3];                             // [group][column tile][row][output]
-  float ax[2][16][8];
-  float dz3s[2][16][4];
-  float tp0[4 * H];                                     // group 0's tail column sums
-  float hp0[8];                                         // group 0's head partials
-  float pw0[H][20];                                     // group 0's [dW1 | db1]
-  float hcs[3][3];
-  int gsync[2];
-};
-
-// the 8 waves of one row group meet; LDS writes before it are visible after.
-// The wait is bounded (~2^20 sleeps, tens of ms): a broken schedule ends the
-// kernel with wrong numbers for the tests to catch, never a hung GPU.
-__device__ __forceinline__ void group_sync(int* ctr, int& epoch) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  epoch += 8;
-  for (int spin = 0; spin < (1 << 20); ++spin) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= epoch) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// a workgroup barrier that orders LDS only: the stage boundaries hand over
-// nothing through global memory (H1, dZ2 and the slabs are read by later
-// launches), so outstanding W2 prefetches and result stores stay in flight
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-__global__ void __launch_bounds__(1024, 4) rowpass_pipe_kernel(int mb, const float* __restrict__ src,
-                                                              const int64_t* __restrict__ idx,
-                                                              const float* __restrict__ P,
-                                                              const float* __restrict__ W2T, float epsilon,
-                                                              float ent_coef, float max_action, float* __restrict__ H1g,
-                                                              float* __restrict__ dZ2g, float* __restrict__ ptail,
-                                                              float* __restrict__ pw1, int net_sel) {
-  constexpr int H = 256, LDA = H + 4, CT = 2, LDS_S = 36, NT = 1024;
-  const Layout L = layout(H);
-  __shared__ PipeSmem sm;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
-  const int g = w >> 3, v = w & 7, n0 = 32 * v;                    // row group, wave in group, first column
-  const int net = net_sel < 0 ? (int)(blockIdx.x & 1) : net_sel;
-  const int rb = net_sel < 0 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
-  const int r0 = rb * 32, gr0 = r0 + 16 * g;                       // first row of the block / of the group
-  const int gvalid = mb - gr0;                                     // valid rows of the group (may be <= 0)
-  int epoch = 0;
-  PHASE_PROBE(0);
-  if (tid < 2) sm.gsync[tid] = 0;
-  float hb3[3], hls[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) { hb3[d] = P[L.b3a + d]; hls[d] = P[L.ls + d]; }
-  const float hb3c = P[L.b3c];
-
-  // ---- stage 1 (both groups): A -------------------------------------------
-  float4 bw1[CT][2];
-  {
-    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
-      bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
-      bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lg < 2) {
-        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
-        bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
-      } else if (lg == 2) {
-        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
-      }
-    }
-  }
-  for (int q = tid; q < 32 * 26; q += NT) {                        // the block's 32 rows
-    const int r = q / 26, c = q % 26, row = r0 + r, gg = r >> 4, rr = r & 15;
-    const float x = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
-    if (c < 18) sm.S[gg][rr][c] = x; else sm.ax[gg][rr][c - 18] = x;
-  }
-  if (tid < 3) {
-    const float ls = tid == 0 ? hls[0] : (tid == 1 ? hls[1] : hls[2]);
-    const float sd = expf(ls), var = sd * sd;
-    sm.hcs[0][tid] = var;
-    sm.hcs[1][tid] = logf(sd);
-    sm.hcs[2][tid] = 1.0f / var;
-  }
-  for (int q = tid; q < 32 * (LDS_S - 18); q += NT) {
-    const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18), gg = r >> 4, rr = r & 15;
-    sm.S[gg][rr][c] = (c == 18 && r0 + r < mb) ? 1.0f : 0.0f;        // bias column of W1aug, zero pad
-  }
-  {                                                                // b2 | W3 rows of the net -> LDS (read in C)
-    const int q = tid >> 8, n = tid & (H - 1);
-    float x;
-    if (q == 0) x = P[L.b2 + net * H + n];
-    else if (net == 0) x = P[L.W3a + (q - 1) * H + n];
-    else x = q == 1 ? P[L.W3c + n] : 0.0f;
-    sm.b2w3[q][n] = x;
-  }
-  lds_barrier();
-  f4 acc[1][CT];
-  float h1[1][CT][4];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_chunk<LDS_S, 1, CT>(&sm.S[g][li][8 * lg], bw1, acc);
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int n = n0 + 16 * t + li;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float h = tanh_f32(acc[0][t][j]);                      // fc1 + tanh
-      h1[0][t][j] = h;
-      sm.h1s[g][4 * lg + j][n] = h;
-    }
-    acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-  }
-  store_rows<16, CT>(H1g + ((int64_t)net * mb + gr0) * H, H, n0, gvalid, h1);
-  // the first W2 chunks of this group's B go out now (group 1 then waits a stage)
-  WPre<CT> pre;
-  mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, pre);
-  PHASE_PROBE(8);
-  lds_barrier();
-  PHASE_PROBE(1);
-
-  // phase B of this group: Z2 = H1 W2^T
-  auto phase_B = [&]() {
-    mfma_rows<H, LDA, H, 1, CT, true, true>(&sm.h1s[g][0][0], P + L.W2 + (int64_t)net * H * H, n0, acc, &pre);
-  };
-
-  // phase C of this group: fc2 tanh, output layer, loss head, dZ2 (-> h1s[g]), tail sums
-  float d2v[1][CT][4];
-  auto phase_C = [&]() {
-    int* gctr = &sm.gsync[g];
-    float b2v[CT], w3[CT][3];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int n = n0 + 16 * t + li;
-      b2v[t] = sm.b2w3[0][n];
-      w3[t][0] = sm.b2w3[1][n]; w3[t][1] = sm.b2w3[2][n]; w3[t][2] = sm.b2w3[3][n];
-    }
-    // output-layer partials per column tile, as mlp_forward forms them
-    {
-      float p[CT][3][4];
-#pragma unroll
-      for (int t = 0; t < CT; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float h = tanh_f32(acc[0][t][j] + b2v[t]);        // fc2 + tanh
-          acc[0][t][j] = h;
-#pragma unroll
-          for (int q = 0; q < 3; ++q) p[t][q][j] = fmaf(h, w3[t][q], 0.0f);
-        }
-      float ps[CT * 3 * 4];
-#pragma unroll
-      for (int t = 0; t < CT; ++t)
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) ps[(t * 3 + q) * 4 + j] = p[t][q][j];
-      if (net == 0) {
-        row16_sum_n<CT * 3 * 4>(ps);
-      } else {
-        float p0[CT * 4];
-#pragma unroll
-        for (int t = 0; t < CT; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) p0[t * 4 + j] = ps[(t * 3) * 4 + j];
-        row16_sum_n<CT * 4>(p0);
-#pragma unroll
-        for (int t = 0; t < CT; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) ps[(t * 3) * 4 + j] = p0[t * 4 + j];
-      }
-      if (li == 0) {
-#pragma unroll
-        for (int t = 0; t < CT; ++t)
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            if (q >= (net == 0 ? 3 : 1)) break;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) sm.osum[g][2 * v + t][4 * lg + j][q] = ps[(t * 3 + q) * 4 + j];
-          }
-      }
-    }
-    group_sync(gctr, epoch);
-    // ---- the loss head: lanes 0-15 of the group's first wave, one row each
-    if (v == 0 && l < 16) {
-      const int r = l, row = gr0 + r;
-      float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
-      if (row < mb) {
-        const float inv = 1.0f / (float)mb;
-        if (net == 0) {
-          float th[3], mu[3], dv[3], var[3], logp[3];
-#pragma unroll
-          for (int d = 0; d < 3; ++d) {
-            float od = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) od += sm.osum[g][k][r][d];
-            th[d] = tanh_f32(od + hb3[d]);
-            mu[d] = max_action * th[d];
-            var[d] = sm.hcs[0][d];
-            dv[d] = sm.ax[g][r][d] - mu[d];
-            logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - sm.hcs[1][d]) - kLogSqrt2Pi;
-          }
-          const float lsum = (logp[0] + logp[1]) + logp[2];
-          const float lold = (sm.ax[g][r][3] + sm.ax[g][r][4]) + sm.ax[g][r][5];
-          const float ratio = expf(lsum - lold);
-          const float adv = sm.ax[g][r][6];
-          const float s1 = ratio * adv;
-          const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
-          const float s2 = cr * adv;
-          const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);   // torch.min tie split
-          const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-          const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
-          const float dmin = -inv;
-          const float dratio = dmin * g1 * adv + dmin * g2 * adv * inside;
-          const float dlsum = dratio * ratio;
-#pragma unroll
-          for (int d = 0; d < 3; ++d) {
-            const float dvv = dv[d] * sm.hcs[2][d];
-            const float dmu = dlsum * dvv;
-            dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
-            dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
-          }
-        } else {
-          float od = 0.0f;
-#pragma unroll
-          for (int k = 0; k < 16; ++k) od += sm.osum[g][k][r][0];
-          const float vc = od + hb3c;
-          dz[3] = 2.0f * inv * (vc - sm.ax[g][r][7]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sm.dz3s[g][r][q] = dz[q];
-      float red[7] = {dz[0], dz[1], dz[2], dls[0], dls[1], dls[2], dz[3]};
-      row16_sum_n<7>(red);                                         // the group's 16 rows, in lane 0
-      if (r == 0) {
-        if (g == 0) {
-#pragma unroll
-          for (int q = 0; q < 7; ++q) sm.hp0[q] = red[q];
-        } else {
-          float* tp = ptail + (int64_t)rb * L.tail;                // rows 0-15 + rows 16-31
-          if (net == 0) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-              tp[5 * H + q] = sm.hp0[q] + red[q];                  // b3a
-              tp[5 * H + 4 + q] = sm.hp0[3 + q] + red[3 + q];      // log_std
-            }
-            tp[5 * H + 3] = 0.0f;
-            tp[5 * H + 7] = 0.0f;
-          } else {
-            tp[6 * H + 8] = sm.hp0[6] + red[6];                    // b3c
-            tp[6 * H + 9] = 0.0f; tp[6 * H + 10] = 0.0f; tp[6 * H + 11] = 0.0f;
-          }
-        }
-      }
-    }
-    group_sync(gctr, epoch);
-    // ---- dZ2 and the tail column sums over the group's rows
-    float* tp = ptail + (int64_t)rb * L.tail;
-    auto tail = [&](auto actor) {
-      constexpr bool ACT = decltype(actor)::value;
-      constexpr int NC = ACT ? 3 : 1;
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int n = n0 + 16 * t + li;
-        float cb2 = 0.f, cw[NC];
-#pragma unroll
-        for (int q = 0; q < NC; ++q) cw[q] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * lg + j;
-          const float h = acc[0][t][j];
-          float dh;
-          if constexpr (ACT) dh = (sm.dz3s[g][r][0] * w3[t][0] + sm.dz3s[g][r][1] * w3[t][1]) +
-                                  sm.dz3s[g][r][2] * w3[t][2];
-          else dh = sm.dz3s[g][r][3] * w3[t][0];
-          const float d2 = dh * (1.0f - h * h);                    // tanh backward
-          sm.dzs[g][r][n] = d2;                                    // dZ2
-          d2v[0][t][j] = d2;
-          cb2 += d2;
-          if constexpr (ACT) {
-            cw[0] = fmaf(sm.dz3s[g][r][0], h, cw[0]); cw[1] = fmaf(sm.dz3s[g][r][1], h, cw[1]);
-            cw[2] = fmaf(sm.dz3s[g][r][2], h, cw[2]);
-          } else {
-            cw[0] = fmaf(sm.dz3s[g][r][3], h, cw[0]);
-          }
-        }
-        cb2 = xor32_sum(xor16_sum(cb2));
-#pragma unroll
-        for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
-        if (lg == 0) {
-          if (g == 0) {
-            sm.tp0[n] = cb2;
-#pragma unroll
-            for (int q = 0; q < NC; ++q) sm.tp0[(1 + q) * H + n] = cw[q];
-          } else {
-            tp[net * H + n] = sm.tp0[n] + cb2;                     // db2
-            if constexpr (ACT) {
-              tp[2 * H + n] = sm.tp0[H + n] + cw[0]; tp[3 * H + n] = sm.tp0[2 * H + n] + cw[1];
-              tp[4 * H + n] = sm.tp0[3 * H + n] + cw[2];           // dW3a
-            } else {
-              tp[5 * H + 8 + n] = sm.tp0[H + n] + cw[0];           // dW3c
-            }
-          }
-        }
-      }
-    };
-    if (net == 0) tail(std::true_type{});
-    else tail(std::false_type{});
-    store_rows<16, CT>(dZ2g + ((int64_t)net * mb + gr0) * H, H, n0, gvalid, d2v);
-    // the first W2T chunks of this group's D go out now, under the stage barrier
-    mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, pre);
-  };
-
-  auto phase_D = [&]() {
-#pragma unroll
-    for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-    mfma_rows<H, LDA, H, 1, CT, true, true>(&sm.dzs[g][0][0], W2T + (int64_t)net * H * H, n0, acc, &pre);
-  };
-
-  // phase E: dZ1 = dH1 (1 - H1^2); [dW1 | db1] over the group's rows, group 0's
-  // partial parked in LDS, group 1 adds its own and writes the block's slab
-  auto phase_E = [&]() {
-    float* pw = pw1 + (int64_t)rb * 2 * H * 20 + (int64_t)net * H * 20;
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float hh = sm.h1s[g][4 * lg + j][n0 + 16 * t + li];  // this lane's own tanh(fc1) values
-        acc[0][t][j] = acc[0][t][j] * (1.0f - hh * hh);
-      }
-#pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
-        f4 d = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[0][t][kk], sm.S[g][4 * lg + kk][16 * hb + li], d);
-        const int kp = 16 * hb + li;
-        if (kp < 20) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int n = n0 + 16 * t + 4 * lg + j;
-            if (g == 0) sm.pw0[n][kp] = d[j];
-            else pw[(int64_t)n * 20 + kp] = sm.pw0[n][kp] + d[j];
-          }
-        }
-      }
-    }
-  };
-
-  // ---- stages 2-6 ---------------------------------------------------------
-  if (g == 0) phase_B();                                           // 2
-  PHASE_PROBE(9);
-  lds_barrier();
-  PHASE_PROBE(2);
-  if (g == 0) phase_C(); else phase_B();                           // 3
-  PHASE_PROBE(10);
-  lds_barrier();
-  PHASE_PROBE(3);
-  if (g == 0) phase_D(); else phase_C();                           // 4
-  PHASE_PROBE(11);
-  lds_barrier();
-  PHASE_PROBE(4);
-  if (g == 0) phase_E(); else phase_D();                           // 5
-  PHASE_PROBE(12);
-  lds_barrier();
-  PHASE_PROBE(5);
-  if (g == 1) phase_E();                                           // 6
-  PHASE_PROBE(7);
-}
-
-// ---------------------------------------------------------------------------
 // policy: the rollout's forward passes on the rowpass's own MLP code
 // (mlp_forward), one workgroup per 32-row block and net.
 //   MODE 0  actor -> mean = max_action*tanh(.) -> Normal sample -> clamp ->
@@ -1626,16 +1229,6 @@ int n_adam_blocks(int H, int net) {
 
 bool valid_h(int H) { return H == 64 || H == 128 || H == 256; }
 
-// H = 256 rowpass: the software-pipelined kernel (default) or the one-stage
-// rowpass_kernel (dev A/B: SATRL_ROWPASS=classic)
-bool rowpass_pipe() {
-  static const bool on = [] {
-    const char* e = std::getenv("SATRL_ROWPASS");
-    return SATRL_ROWPASS_PIPE && kRows == 32 && kNW256 == 16 && !(e && std::string(e) == "classic");
-  }();
-  return on;
-}
-
 #define LAUNCH_CHECK()                                                      \
   do {                                                                      \
     hipError_t e_ = hipGetLastError();                                      \
@@ -1682,9 +1275,6 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
-  else if (rowpass_pipe())
-    hipLaunchKernelGGL(rowpass_pipe_kernel, g, dim3(1024), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef, max_action,
-                       H1, dZ2, ptail, pw1, net);
   else
     hipLaunchKernelGGL((rowpass_kernel<256, kNW256>), g, dim3(kNW256 * 64), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);

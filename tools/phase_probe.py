@@ -52,8 +52,7 @@ if probe:
     assert lib.satrl_probe_read(buf.ctypes.data) == 0
     b = buf.astype(np.int64)                     # [wg][stamp][wave][realtime, shader clock]
     order = [0, 8, 9, 10, 11, 1, 2, 3, 4, 5, 6, 7]
-    if os.environ.get("SATRL_ROWPASS", "") != "classic":   # the pipelined kernel's stamps
-        order = [0, 8, 1, 9, 2, 10, 3, 11, 4, 12, 5, 7]
+    b = b[:2 * (mb // 32)]                       # the launched workgroups only
     t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
     print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
           "(median over workgroups), waves 0..15; actor rows then critic rows")
