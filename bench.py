@@ -353,6 +353,7 @@ def main():
         return None
 
     rowpass_prof_us = prof_avg_us("rowpass_kernel<%d" % a.hidden)
+    head_us = rowpass_prof_us if rowpass_prof_us else rowpass_us
     traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
 
     # ---- env kernel: in the rollout (live: eager rollout steps -- policy kernel,
@@ -540,13 +541,21 @@ def main():
             "episodes_finished_total": float(stats[0]),
             "roofline": {"kernel": f"satrl_ppo_rowpass<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA 16x16x4)",
                          "bound": "mfma",
-                         "achieved": rowpass_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": rowpass_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
-                         "avg_launch_us": rowpass_us, "flop_per_launch": rowpass_flop, "rows_per_launch": mb_local,
-                         "timing": "live, HIP events on the launch stream: kernel_iters minibatch steps (rowpass -> "
-                                   "dW2 -> reduce -> Adam, each Adam rewriting the weights the next rowpass streams, "
-                                   "as in the update) minus the same steps without the rowpass, per launch; queued "
-                                   "behind a GPU spin so the kernels run back to back",
+                         "achieved": rowpass_flop / (head_us * 1e-6) / 1e12, "peak": FP32_MFMA_PEAK_TFS,
+                         "unit": "TFLOP/s",
+                         "frac": rowpass_flop / (head_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS, "traffic": traffic,
+                         "avg_launch_us": head_us, "flop_per_launch": rowpass_flop, "rows_per_launch": mb_local,
+                         "timing": ("in-update kernel duration: the rocprofv3 average of this command's rowpass "
+                                    "launches (profiles/, nearly all inside the update's graphs); the live HIP-event "
+                                    "figures beside it" if rowpass_prof_us else
+                                    "live marginal cost (no rocprof profile of this build present)"),
+                         "live_marginal_avg_launch_us": rowpass_us,
+                         "live_marginal_frac": rowpass_tfs / FP32_MFMA_PEAK_TFS,
+                         "live_marginal_timing": "HIP events on the launch stream: kernel_iters minibatch steps "
+                                                 "(rowpass -> dW2 -> reduce -> Adam, each Adam rewriting the weights "
+                                                 "the next rowpass streams, as in the update) minus the same steps "
+                                                 "without the rowpass, per launch, behind a GPU spin; it carries the "
+                                                 "launch boundary the rowpass adds to the chain",
                          "minibatch_step_us": t_chain,
                          "event_bracketed_avg_launch_us": rowpass_ev_us, "event_bracketed_median_us": rowpass_med,
                          "rocprof_avg_launch_us": rowpass_prof_us,
