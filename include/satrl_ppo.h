@@ -54,6 +54,17 @@ int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
 int satrl_ppo_dw2_splits(int H, int mb);
 int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream);
 
+/* The same slabs through hipBLASLt (the H = 256 path): one strided-batched
+ * f32 matmul over nets x S splits, mb % S == 0, the library heuristic's
+ * solution (a stream-K tile with a fixed fix-up order: bitwise repeatable).
+ * H1 / dZ2 / p2 point at the first selected net's block (net 1 alone: the
+ * critic's).  _workspace builds and caches the plan for
+ * (H, mb, S, nets) -- call it outside stream capture -- and reports the
+ * workspace bytes satrl_ppo_dw2_lib needs and the solution index chosen.  */
+int satrl_ppo_dw2_lib_workspace(int H, int mb, int net, int S, int64_t* ws_bytes, int* algo_index);
+int satrl_ppo_dw2_lib(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* workspace,
+                      int64_t ws_bytes, void* stream);
+
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
  * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and

@@ -1,0 +1,154 @@
+// dW2 on hipBLASLt for H = 256 (satrl_ppo_dw2_lib): the fc2 weight gradient
+// of ppo_continuous.py:226-238 (loss.backward() through fc2) as S-way split-K
+// slabs, the same product satrl_ppo_dw2 computes:
+//   p2[net][s] (H x H, row-major) = dZ2[net][rows of split s]^T H1[net][same rows]
+// In column-major terms each slab is D = A B^T with A = H1_s, B = dZ2_s (both
+// H x K, ld H): one strided-batched hipBLASLt matmul over nb*S batches.
+//
+// Algorithm: the library heuristic's first choice.  In-process the library
+// is torch's bundled hipBLASLt (libhipblaslt.so.1 resolves to the copy torch
+// already loaded), and tools/blaslt_search.py timed every solution of it that
+// supports these slabs on MI355X: at S = 4 the heuristic's stream-K
+// MT32x64x64 tile (11.7 us back to back) ties the fastest, and every
+// candidate reproduced its output bit for bit over repeated runs (the
+// stream-K fix-up has a fixed order).  SATRL_DW2_ALGO=<solution index> (dev
+// A/B) tries that solution first.
+//
+// Plans (descriptors, algorithm, workspace size) are cached per (H, mb, S,
+// nets): create the plan (satrl_ppo_dw2_lib_workspace) outside stream
+// capture; satrl_ppo_dw2_lib itself only enqueues the matmul, so it can be
+// captured into a hipGraph.
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
+
+#include <cstdint>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+void satrl_ppo_set_error(const char* msg);   // ppo_kernels.hip: satrl_ppo_last_error
+
+namespace {
+
+struct Plan {
+  hipblasLtMatmulDesc_t md = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  size_t ws = 0;
+  int index = -1;
+};
+
+std::mutex g_mu;
+hipblasLtHandle_t g_lt = nullptr;
+std::map<std::tuple<int, int, int, int>, Plan> g_plans;
+
+bool make_plan(int H, int mb, int S, int nb, Plan& p) {
+  if (!g_lt && hipblasLtCreate(&g_lt) != HIPBLAS_STATUS_SUCCESS) {
+    satrl_ppo_set_error("hipblasLtCreate");
+    return false;
+  }
+  const int K = mb / S, B = nb * S;
+  const int64_t sab = (int64_t)K * H, sc = (int64_t)H * H;
+  hipblasOperation_t opA = HIPBLAS_OP_N, opB = HIPBLAS_OP_T;
+  if (hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.la, HIP_R_32F, H, K, H) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_32F, H, K, H) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, H, H, H) != HIPBLAS_STATUS_SUCCESS) {
+    satrl_ppo_set_error("hipBLASLt descriptor");
+    return false;
+  }
+  for (auto l : {p.la, p.lb, p.lc}) {
+    const int64_t* stride = l == p.lc ? &sc : &sab;
+    if (hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &B, sizeof(B)) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, stride, sizeof(*stride)) !=
+            HIPBLAS_STATUS_SUCCESS) {
+      satrl_ppo_set_error("hipBLASLt layout");
+      return false;
+    }
+  }
+  const float alpha = 1.0f, beta = 0.0f;
+  std::vector<int> idx;
+  if (const char* e = std::getenv("SATRL_DW2_ALGO"))
+    if (std::atoi(e) >= 0) idx.push_back(std::atoi(e));
+  for (int i : idx) {
+    std::vector<int> one{i};
+    std::vector<hipblasLtMatmulHeuristicResult_t> r;
+    if (hipblaslt_ext::getAlgosFromIndex(g_lt, one, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) continue;
+    size_t w = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r[0].algo, w) !=
+        HIPBLAS_STATUS_SUCCESS)
+      continue;
+    p.algo = r[0].algo;
+    p.ws = w;
+    p.index = i;
+    return true;
+  }
+  hipblasLtMatmulPreference_t pref;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) {
+    satrl_ppo_set_error("hipBLASLt preference");
+    return false;
+  }
+  size_t cap = 64ull << 20;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &cap, sizeof(cap));
+  hipblasLtMatmulHeuristicResult_t h[1];
+  int nh = 0;
+  const hipblasStatus_t s = hipblasLtMatmulAlgoGetHeuristic(g_lt, p.md, p.la, p.lb, p.lc, p.lc, pref, 1, h, &nh);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (s != HIPBLAS_STATUS_SUCCESS || nh < 1) {
+    satrl_ppo_set_error("no hipBLASLt algorithm for the dW2 slabs");
+    return false;
+  }
+  p.algo = h[0].algo;
+  p.ws = h[0].workspaceSize;
+  p.index = hipblaslt_ext::getIndexFromAlgo(p.algo);
+  return true;
+}
+
+Plan* plan(int H, int mb, int S, int nb) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const auto key = std::make_tuple(H, mb, S, nb);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) return &it->second;
+  Plan p;
+  if (!make_plan(H, mb, S, nb, p)) return nullptr;
+  return &g_plans.emplace(key, p).first->second;
+}
+
+bool args_ok(int H, int mb, int net, int S) {
+  return H > 0 && H % 64 == 0 && mb > 0 && S >= 1 && mb % S == 0 && net >= -1 && net <= 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int satrl_ppo_dw2_lib_workspace(int H, int mb, int net, int S, int64_t* ws_bytes, int* algo_index) {
+  if (!args_ok(H, mb, net, S) || !ws_bytes) return -1;
+  Plan* p = plan(H, mb, S, net < 0 ? 2 : 1);
+  if (!p) return -2;
+  *ws_bytes = (int64_t)p->ws;
+  if (algo_index) *algo_index = p->index;
+  return 0;
+}
+
+int satrl_ppo_dw2_lib(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* ws,
+                      int64_t ws_bytes, void* stream) {
+  if (!args_ok(H, mb, net, S) || !H1 || !dZ2 || !p2) return -1;
+  Plan* p = plan(H, mb, S, net < 0 ? 2 : 1);
+  if (!p) return -2;
+  if ((int64_t)p->ws > ws_bytes || (p->ws > 0 && !ws)) return -1;   // workspace below the plan's
+  const float alpha = 1.0f, beta = 0.0f;
+  const hipblasStatus_t s = hipblasLtMatmul(g_lt, p->md, &alpha, H1, p->la, dZ2, p->lb, &beta, p2, p->lc, p2, p->lc,
+                                            &p->algo, ws, p->ws, (hipStream_t)stream);
+  if (s != HIPBLAS_STATUS_SUCCESS) { satrl_ppo_set_error("hipblasLtMatmul"); return -2; }
+  return 0;
+}
+
+}  // extern "C"

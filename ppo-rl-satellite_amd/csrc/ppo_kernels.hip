@@ -4,7 +4,8 @@
 //   rowpass  gather, fc1, fc2 (f32 MFMA), output layers, losses, backprop to
 //            dZ2 and through fc2 (f32 MFMA) and fc1's tanh; writes H1, dZ2
 //            and partial slabs of every small gradient
-//   [bmm]    dW2 = dZ2^T @ H1 split-K S ways (hipBLASLt, batch 2S)
+//   dW2      dZ2^T @ H1 split-K S ways: dw2_kernel (H <= 128) or hipBLASLt
+//            (H = 256, dw2_blas.cpp)
 //   reduce   partial slabs -> G (fixed order), per-block squared norms per net
 //   adam     clip coefficient per net + Adam (torch single-tensor formula),
 //            also refreshes fc2.weight^T used by the next rowpass
@@ -1408,6 +1409,9 @@ int satrl_ppo_tanh(int64_t n, const float* x, float* y, void* stream) {
 const char* satrl_ppo_last_error(void) { return g_err.c_str(); }
 
 }  // extern "C"
+
+// (dw2_blas.cpp reports through satrl_ppo_last_error too)
+void satrl_ppo_set_error(const char* msg) { g_err = msg; }
 
 #ifdef SATRL_PHASE_PROBE
 extern "C" int satrl_probe_read(unsigned long long* out) {

@@ -105,6 +105,8 @@ _SIGS = {
     "satrl_ppo_sizes": ([C.c_int, C.c_int, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
     "satrl_ppo_dw2_splits": ([C.c_int, C.c_int], C.c_int),
     "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_dw2_lib_workspace": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp], C.c_int),
+    "satrl_ppo_dw2_lib": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_int64, _vp], C.c_int),
     "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,

@@ -195,9 +195,10 @@ class FusedMinibatch:
         self.group = int(group)
         self.use_graph = use_graph
         # dW2: the hand-written split-K kernel for H <= 128 (hipBLASLt picks
-        # K-serial tiles there: 12.5 us vs 3 us at H = 64); at H = 256 the
-        # library GEMM (torch.bmm -> hipBLASLt, split-K 4) measured 13 us vs
-        # 15 us for satrl_ppo_dw2, so it stays a plain library GEMM
+        # K-serial tiles there: 12.5 us vs 3 us at H = 64); at H = 256 a
+        # plain library GEMM (satrl_ppo_dw2_lib: hipBLASLt from the C ABI,
+        # split-K 4, 11.7 us vs 15 us for satrl_ppo_dw2; its heuristic's
+        # stream-K tile ties the fastest of all 245 solutions that fit)
         self.lib_gemm = learner.H >= 256
         if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob
             self.lib_gemm = os.environ["SATRL_DW2_LIB"] == "1"
@@ -218,6 +219,11 @@ class FusedMinibatch:
         # (dw2_splits caps S at 256 / tiles), so a ragged tail minibatch whose
         # S exceeds the full minibatch's never writes past the slabs
         self.p2 = torch.empty(2 * self.max_splits(H) * H * H, **f32)
+        self.ws = None                     # hipBLASLt workspace of the dW2 plans
+        self._ws_retired = []
+        self._ws_for = {}                  # (mb, S, net) -> the workspace its plan was checked against
+        if self.lib_gemm and torch.cuda.is_available():
+            self._ws_for[(self.mb, self.S, -1)] = (self._dw2_plan(self.mb, self.S, -1),)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
@@ -281,11 +287,32 @@ class FusedMinibatch:
             check(_lib.lib().satrl_ppo_dw2(H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), stream_ptr()),
                   "satrl_ppo_dw2")
             return
-        lo, hi = (0, 2) if net < 0 else (net, net + 1)
-        nb = hi - lo
-        z = dZ2[lo * mb * H:hi * mb * H].view(nb * S, mb // S, H)
-        y = H1[lo * mb * H:hi * mb * H].view(nb * S, mb // S, H)
-        torch.bmm(z.transpose(1, 2), y, out=self.p2[lo * S * H * H:hi * S * H * H].view(nb * S, H, H))
+        lo = 0 if net < 0 else net
+        hit = self._ws_for.get((mb, S, net))
+        if hit is None:
+            hit = self._ws_for[(mb, S, net)] = (self._dw2_plan(mb, S, net),)
+        ws = hit[0]
+        o = 4 * lo * mb * H                # byte offset of the first selected net's block
+        check(_lib.lib().satrl_ppo_dw2_lib(H, mb, net, S, H1.data_ptr() + o, dZ2.data_ptr() + o,
+                                           self.p2.data_ptr() + 4 * lo * S * H * H,
+                                           None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
+                                           stream_ptr()), "satrl_ppo_dw2_lib")
+
+    def _dw2_plan(self, mb, S, net):
+        """Create (or look up) the hipBLASLt plan of a dW2 shape; grows the
+        shared workspace to its size.  Plans made here, before any capture,
+        keep graph capture free of library set-up."""
+        wsb, idx = C.c_int64(), C.c_int()
+        check(_lib.lib().satrl_ppo_dw2_lib_workspace(self.L.H, int(mb), int(net), int(S), C.byref(wsb),
+                                                     C.byref(idx)), "satrl_ppo_dw2_lib_workspace")
+        if wsb.value > 0 and (self.ws is None or self.ws.numel() < wsb.value):
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.NativeError("dW2 workspace must grow during graph capture; plan the shape first")
+            if self.ws is not None:
+                self._ws_retired.append(self.ws)     # captured graphs may still point at it
+            self.ws = torch.empty(wsb.value, dtype=torch.uint8, device=self.L.device)
+        self.dw2_algo = idx.value
+        return self.ws
 
     def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False):
         """One minibatch step of one chain.  Bench-only knobs: `events` (a pair

@@ -83,6 +83,10 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_rowpass(256, 64, -1, None, *args[1:]) == -1           # null rows
     assert lib.satrl_ppo_dw2(256, 4096, -1, 0, fake, fake, fake, None) == -1   # S < 1
     assert lib.satrl_ppo_dw2(256, 64, -1, 64, fake, fake, fake, None) == -1    # an empty split
+    assert lib.satrl_ppo_dw2_lib(256, 4096, -1, 3, fake, fake, fake, fake, 1 << 20, None) == -1   # mb % S
+    assert lib.satrl_ppo_dw2_lib(256, 4096, -1, 4, None, fake, fake, fake, 1 << 20, None) == -1   # null H1
+    assert lib.satrl_ppo_dw2_lib_workspace(256, 4096, 2, 4, fake, None) == -1                    # net
+    assert lib.satrl_ppo_dw2_lib_workspace(256, 4096, -1, 4, None, None) == -1                   # no output
     assert lib.satrl_ppo_reduce(256, 64, -1, 1, 4, fake, fake, fake, fake, fake, fake, None) == -1   # mode
     assert lib.satrl_ppo_reduce(256, 64, -1, 1, 2, fake, fake, fake, fake, None, None, None) == -1   # no nsq
     assert lib.satrl_gae(0, 4, fake, fake, fake, 0.99, 0.95, fake, fake, None) == -1

@@ -481,3 +481,41 @@ def test_dw2_kernel_vs_torch(H, mb):
     ref = torch.bmm(dZ2.view(2, mb, H).double().transpose(1, 2), H1.view(2, mb, H).double())
     err = (got - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item() + 1e-4, err
+
+
+@pytest.mark.parametrize("mb,S,net", [(4096, 4, -1), (4096, 4, 1), (4096, 1, -1), (776, 4, 0)])
+def test_dw2_lib_vs_fp64_and_deterministic(mb, S, net):
+    """satrl_ppo_dw2_lib (hipBLASLt, fixed stream-K solution) at H = 256:
+    each slab == its split's dZ2^T @ H1 in fp64 within f32 accumulation
+    error, only the selected net's slabs written, and a second call
+    reproduces every slab bit for bit (the stream-K fix-up has a fixed
+    order)."""
+    import ctypes as C
+    from satrl import _lib
+    H = 256
+    lib = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(mb + S)
+    H1 = torch.randn(2 * mb * H, device="cuda", generator=g)
+    dZ2 = torch.randn(2 * mb * H, device="cuda", generator=g)
+    wsb, idx = C.c_int64(), C.c_int()
+    _lib.check(lib.satrl_ppo_dw2_lib_workspace(H, mb, net, S, C.byref(wsb), C.byref(idx)), "workspace")
+    print(f"solution index {idx.value}, workspace {wsb.value} B")
+    ws = torch.empty(max(wsb.value, 1), dtype=torch.uint8, device="cuda")
+    lo = 0 if net < 0 else net
+    outs = []
+    for _ in range(2):
+        p2 = torch.full((2 * S * H * H,), float("nan"), device="cuda")
+        _lib.check(lib.satrl_ppo_dw2_lib(H, mb, net, S, _lib.ptr(H1[lo * mb * H:]), _lib.ptr(dZ2[lo * mb * H:]),
+                                         _lib.ptr(p2[lo * S * H * H:]), _lib.ptr(ws), wsb.value, _lib.stream_ptr()),
+                   "satrl_ppo_dw2_lib")
+        torch.cuda.synchronize()
+        outs.append(p2.view(2, S, H, H))
+    assert torch.equal(outs[0].view(-1).view(torch.int32), outs[1].view(-1).view(torch.int32))
+    K = mb // S
+    ref = torch.bmm(dZ2.view(2 * S, K, H).double().transpose(1, 2), H1.view(2 * S, K, H).double()).view(2, S, H, H)
+    for n in range(2):
+        if net >= 0 and n != net:
+            assert torch.isnan(outs[0][n]).all()                 # the other net untouched
+            continue
+        err = (outs[0][n].double() - ref[n]).abs().max().item()
+        assert err <= 1e-5 * ref[n].abs().max().item() + 1e-4, err

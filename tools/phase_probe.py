@@ -70,14 +70,14 @@ if probe:
                 print(f"   {k:2d}: " + "  ".join(f"{int(b[wg, k, w_, 0] - rt0):6d}/{int(b[wg, k, w_, 1] - ck0):7d}"
                                              for w_ in (0, 4, 8, 15)))
     nwg = 2 * (mb // 32)
-    st = b[:nwg, 0, :, 0].min(axis=1)
+    ws0 = b[:nwg, 0, :, 0].min(axis=1)
     en = b[:nwg, 7, :, 0].max(axis=1)
     cyc = (b[:nwg, 7, :, 1].max(axis=1) - b[:nwg, 0, :, 1].min(axis=1)).astype(np.float64)
-    wall = (en - st).astype(np.float64) / 100e6
+    wall = (en - ws0).astype(np.float64) / 100e6
     print("workgroup span: median %.2f us, max %.2f us; shader clock over it (median GHz) %.3f" %
           (np.median(wall) * 1e6, wall.max() * 1e6, float(np.median(cyc / wall)) / 1e9))
     print("start spread %.2f us, end spread %.2f us, kernel span %.2f us" %
-          ((st.max() - st.min()) / 100.0, (en.max() - en.min()) / 100.0, (en.max() - st.min()) / 100.0))
+          ((ws0.max() - ws0.min()) / 100.0, (en.max() - en.min()) / 100.0, (en.max() - ws0.min()) / 100.0))
 
 # event timings of each launch of one minibatch step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -99,6 +99,7 @@ def t(fn, n=200):
 
 
 nsq = st.nsq[0]
+print("dW2 solution index", st.dw2_algo if st.lib_gemm else "dw2_kernel")
 res = {
     "rowpass": t(lambda: st.rowpass(src, None)),
     "dw2": t(lambda: st._dw2(H1, dZ2, mb, S, -1)),
