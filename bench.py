@@ -50,10 +50,12 @@ def parse():
                     help="init the nccl process group even at world size 1 (rehearses the DP update path)")
     ap.add_argument("--surrogate", action="store_true",
                     help="config 5: ImprovedNN surrogate (bf16) evaluated on every env step of the rollout")
-    ap.add_argument("--dp-minibatch", choices=("global", "per_gpu"), default="global",
+    ap.add_argument("--dp-minibatch", choices=("auto", "global", "per_gpu"), default="auto",
                     help="data parallelism: 'global' = --minibatch is the global minibatch, each of N ranks steps "
                          "minibatch/N of its rows per Adam step (the reference's semantics, SURVEY 8e); 'per_gpu' = "
-                         "every rank steps --minibatch rows (global minibatch N x --minibatch)")
+                         "every rank steps --minibatch rows (global minibatch N x --minibatch); 'auto' (default) = "
+                         "global for BASELINE configs[3] (65536 envs over 8 GPUs) and at N = 1, per_gpu for the "
+                         "weak-scaling series of configs[2] (16384 envs per GPU at N = 2/4/8)")
     ap.add_argument("--profile-tag", default="r2", help="profiles/<tag>_* files the rocprof cross-check fields read")
     return ap.parse_args()
 
@@ -202,7 +204,21 @@ def workload_name(a, world):
             return "BASELINE.json configs[1]: " + desc
         if world == 8 and a.num_envs == 8192 and a.hidden == 256:
             return "BASELINE.json configs[3]: " + desc
+    if (world > 1 and a.dp_minibatch == "per_gpu" and a.num_envs == 16384 and a.hidden == 256
+            and a.horizon == 2048 and a.minibatch == 4096 and a.epochs == 10 and not a.surrogate):
+        return ("weak-scaling series of BASELINE.json configs[2] (each GPU runs configs[2] on its env shard, "
+                "gradients averaged per minibatch): " + desc)
     return desc
+
+
+def dp_mode(a, world):
+    """--dp-minibatch auto: the reference's global minibatch wherever the total
+    env count is a configuration's own (N = 1, configs[3]); per_gpu for the
+    weak-scaling series, where the global minibatch would multiply the number
+    of sequential Adam steps by N and the per-GPU work would not stay fixed."""
+    if a.dp_minibatch != "auto":
+        return a.dp_minibatch
+    return "global" if world == 1 or (world == 8 and a.num_envs == 8192) else "per_gpu"
 
 
 def main():
@@ -211,6 +227,7 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    a.dp_minibatch = dp_mode(a, world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
