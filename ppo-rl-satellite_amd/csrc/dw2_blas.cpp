@@ -117,7 +117,12 @@ Plan* plan(int H, int mb, int S, int nb) {
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return &it->second;
   Plan p;
-  if (!make_plan(H, mb, S, nb, p)) return nullptr;
+  if (!make_plan(H, mb, S, nb, p)) {                 // release what a failed plan created
+    for (auto l : {p.la, p.lb, p.lc})
+      if (l) hipblasLtMatrixLayoutDestroy(l);
+    if (p.md) hipblasLtMatmulDescDestroy(p.md);
+    return nullptr;
+  }
   return &g_plans.emplace(key, p).first->second;
 }
 
