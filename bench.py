@@ -377,6 +377,16 @@ def main():
     rowpass_prof_us = prof_avg_us("rowpass_kernel<%d" % a.hidden)
     head_us = rowpass_prof_us if rowpass_prof_us else rowpass_us
     traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
+    mfma_util = None                   # SQ_VALU_MFMA_BUSY_CYCLES pass (tools/profile_round.sh)
+    mfma_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_rowpass_mfma_pmc.json")
+    if os.path.exists(mfma_file):
+        with open(mfma_file) as f:
+            d = json.load(f)
+        if d.get("hidden") == a.hidden and d.get("minibatch") == mb_local:
+            mfma_util = {"mfma_busy_cycles_per_launch": d["SQ_VALU_MFMA_BUSY_CYCLES_median"],
+                         "mfma_busy_frac_dispatch_window": d["mfma_busy_frac"],
+                         "source": f"profiles/{a.profile_tag}_rowpass_mfma_pmc.json (lower bound: the --pmc "
+                                   "dispatch window includes the profiler's set-up)"}
 
     # ---- env kernel: in the rollout (live: eager rollout steps -- policy kernel,
     # then the env step between HIP events -- after the timed region, the
@@ -587,6 +597,7 @@ def main():
                          "back_to_back_frac": rowpass_flop / (b2b_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS,
                          "traffic_source": f"profiles/{a.profile_tag}_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
                                            "bytes/launch)",
+                         "mfma_utilisation": mfma_util,
                          "note": "f32 MFMA; one net per workgroup of 32 rows, each streams that net's fc2 weights "
                                  "from L2 per phase (DESIGN.md 3.4)"},
             "roofline_env": {"kernel": "satenv step_kernel_wide<autoreset, 64> (hand-written HIP, FP64)", "bound": "hbm",

@@ -55,6 +55,35 @@ def main():
         with open(os.path.join(prof, f"{tag}_rowpass_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res))
+    mfma = os.path.join(d, "pmc_mfma", "run_counter_collection.csv")
+    if os.path.exists(mfma):
+        # MFMA utilisation of the rowpass: SQ_VALU_MFMA_BUSY_CYCLES sums each MFMA's
+        # busy cycles on its SIMD over the chip; GRBM_GUI_ACTIVE sums the busy
+        # cycles of the 8 XCDs (MI355X_MICROARCH.md), so one XCD's span is /8
+        busy, nb = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
+        grbm, ng = pmc_per_dispatch(mfma, "rowpass_kernel", "GRBM_GUI_ACTIVE")
+        sqb, ns = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_BUSY_CYCLES")
+        n_simd = 256 * 4
+        # v_mfma_f32_16x16x4f32 per launch: per row and net fc2 fwd + dH1 (2 x 2 H^2 FLOP) and
+        # fc1 fwd + [dW1|db1] (2 x 2 H 32 FLOP, K padded to 32): 288 per wave, 1 179 648 per launch
+        n_mfma = 2 * 4096 * (2 * 2 * 256 * 256 + 2 * 2 * 256 * 32) / (16 * 16 * 4 * 2)
+        res = {"kernel": "rowpass_kernel<256, 16>", "hidden": 256, "minibatch": 4096, "dispatches": [nb, ng, ns],
+               "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
+               "SQ_BUSY_CYCLES_median": sqb,
+               "xcd_cycles": grbm / 8.0 if grbm else None,
+               "mfma_busy_frac": busy / (grbm / 8.0 * n_simd) if busy and grbm else None,
+               "mfma_instructions_per_launch": n_mfma,
+               "busy_cycles_per_mfma": busy / n_mfma if busy else None,
+               "definition": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the "
+                             "fraction of SIMD-cycles of the dispatch window in which the matrix core was busy, at "
+                             "the clock the chip ran (roofline.frac prices against the 2.4 GHz peak instead). The "
+                             "window of a ~30 us dispatch under --pmc includes the profiler's per-dispatch set-up "
+                             "(MI355X_MICROARCH.md: GRBM quotients read high below ~0.3 ms), so this is a lower "
+                             "bound; busy_cycles_per_mfma = 32 shows the counter equals 32 x the kernel's MFMA count",
+               "workload": "tools/rowpass_workload.py"}
+        with open(os.path.join(prof, f"{tag}_rowpass_mfma_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
     fetch = os.path.join(d, "pmc_env_fetch", "run_counter_collection.csv")
     write = os.path.join(d, "pmc_env_write", "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
