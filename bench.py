@@ -377,6 +377,28 @@ def main():
     rowpass_prof_us = prof_avg_us("rowpass_kernel<%d" % a.hidden)
     head_us = rowpass_prof_us if rowpass_prof_us else rowpass_us
     traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
+    # the rollout's policy kernel (both agents' forward, the (num_envs x hidden)
+    # GEMMs): per row and agent fc1 2*18*H + H, fc2 2*H*H + H, mean layer 2*3*H + 3
+    policy_roof = None
+    pol_us = prof_avg_us("policy_kernel<%d;16;0>" % a.hidden)
+    if pol_us:
+        pol_flop = 2 * a.num_envs * (2 * 18 * a.hidden + a.hidden + 2 * a.hidden * a.hidden + a.hidden
+                                     + 2 * 3 * a.hidden + 3)
+        pol_tfs = pol_flop / (pol_us * 1e-6) / 1e12
+        policy_roof = {"kernel": f"policy_kernel<{a.hidden},16,0> (both agents' choose_action, f32 MFMA)",
+                       "bound": "mfma", "achieved": pol_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                       "frac": pol_tfs / FP32_MFMA_PEAK_TFS, "avg_launch_us": pol_us, "flop_per_launch": pol_flop,
+                       "timing": f"rocprofv3 average over the rollout's launches "
+                                 f"(profiles/{a.profile_tag}_bench_kernel_stats.csv)"}
+        pol_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_policy_mfma_pmc.json")
+        if os.path.exists(pol_file):
+            with open(pol_file) as f:
+                d = json.load(f)
+            policy_roof["mfma_utilisation"] = {
+                "mfma_busy_cycles_per_launch": d["SQ_VALU_MFMA_BUSY_CYCLES_median"],
+                "mfma_busy_frac_dispatch_window": d["mfma_busy_frac"],
+                "source": f"profiles/{a.profile_tag}_policy_mfma_pmc.json (lower bound: the --pmc dispatch "
+                          "window includes the profiler's set-up)"}
     mfma_util = None                   # SQ_VALU_MFMA_BUSY_CYCLES pass (tools/profile_round.sh)
     mfma_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_rowpass_mfma_pmc.json")
     if os.path.exists(mfma_file):
@@ -619,6 +641,7 @@ def main():
             "roofline_update": {"bound": "mfma", "achieved": upd_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                                 "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
                                 "flop_per_transition_epoch": flop_per_transition_epoch},
+            "roofline_policy": policy_roof,
             "propagators": {"rk4_j2_state_steps_per_s": a.num_envs * rk_steps / (rk4_ms * 1e-3),
                             "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
                             "env_rk4_cw_avg_launch_us": env_rk_us,

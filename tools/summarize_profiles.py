@@ -84,6 +84,25 @@ def main():
         with open(os.path.join(prof, f"{tag}_rowpass_mfma_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res))
+    pol = os.path.join(d, "pmc_policy_mfma", "run_counter_collection.csv")
+    if os.path.exists(pol):
+        # the rollout's policy kernel (both agents' forward, 16384 rows each): per row and
+        # agent fc1 (K padded to 32) + fc2 = 72 v_mfma_f32_16x16x4f32
+        busy, nb = pmc_per_dispatch(pol, "policy_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
+        grbm, ng = pmc_per_dispatch(pol, "policy_kernel", "GRBM_GUI_ACTIVE")
+        n_mfma = 2 * 16384 * (2 * 256 * 32 + 2 * 256 * 256) / (16 * 16 * 4 * 2)
+        res = {"kernel": "policy_kernel<256, 16, 0>", "hidden": 256, "num_envs": 16384, "agents": 2,
+               "dispatches": [nb, ng], "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
+               "xcd_cycles": grbm / 8.0 if grbm else None,
+               "mfma_busy_frac": busy / (grbm / 8.0 * 1024) if busy and grbm else None,
+               "mfma_instructions_per_launch": n_mfma,
+               "busy_cycles_per_mfma": busy / n_mfma if busy else None,
+               "definition": "as in the rowpass summary: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 "
+                             "SIMDs) over the --pmc dispatch window",
+               "workload": "tools/policy_workload.py"}
+        with open(os.path.join(prof, f"{tag}_policy_mfma_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
     fetch = os.path.join(d, "pmc_env_fetch", "run_counter_collection.csv")
     write = os.path.join(d, "pmc_env_write", "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
