@@ -5,14 +5,17 @@
 // In column-major terms each slab is D = A B^T with A = H1_s, B = dZ2_s (both
 // H x K, ld H): one strided-batched hipBLASLt matmul over nb*S batches.
 //
-// Algorithm: the library heuristic's first choice.  In-process the library
-// is torch's bundled hipBLASLt (libhipblaslt.so.1 resolves to the copy torch
-// already loaded), and tools/blaslt_search.py timed every solution of it that
-// supports these slabs on MI355X: at S = 4 the heuristic's stream-K
-// MT32x64x64 tile (11.7 us back to back) ties the fastest, and every
-// candidate reproduced its output bit for bit over repeated runs (the
-// stream-K fix-up has a fixed order).  SATRL_DW2_ALGO=<solution index> (dev
-// A/B) tries that solution first.
+// Algorithm.  Under torch the library is torch's bundled hipBLASLt
+// (libhipblaslt.so.1 resolves to the copy torch already loaded), and
+// tools/blaslt_search.py timed every solution of it that supports these slabs
+// on MI355X: at S = 4 the heuristic's stream-K MT32x64x64 tile (11.7 us back
+// to back) ties the fastest, so its first choice is taken.  A C host without
+// torch loads ROCm 7.2's hipBLASLt, whose heuristic picks a 12.6 us tile
+// while its stream-K MT32x64x64 solution takes 11.0 us: that one is
+// preferred when present (kPreferred256, checked by name).  Every candidate
+// reproduced its output bit for bit over repeated runs (the stream-K fix-up
+// has a fixed order).  SATRL_DW2_ALGO=<solution index> (dev A/B) tries that
+// solution first; SATRL_DW2_ALGO=-1 takes the heuristic's choice.
 //
 // Plans (descriptors, algorithm, workspace size) are cached per (H, mb, S,
 // nets): create the plan (satrl_ppo_dw2_lib_workspace) outside stream
@@ -33,6 +36,11 @@
 void satrl_ppo_set_error(const char* msg);   // ppo_kernels.hip: satrl_ppo_last_error
 
 namespace {
+
+// ROCm 7.2's hipBLASLt (what a C host without torch loads): its fastest
+// solution for the H = 256, S = 4 slabs, 11.0 us against 12.6 us for its
+// heuristic's first choice (tools/blaslt_search.cpp built against /opt/rocm)
+const int kPreferred256[] = {483347};
 
 struct Plan {
   hipblasLtMatmulDesc_t md = nullptr;
@@ -75,12 +83,21 @@ bool make_plan(int H, int mb, int S, int nb, Plan& p) {
   }
   const float alpha = 1.0f, beta = 0.0f;
   std::vector<int> idx;
-  if (const char* e = std::getenv("SATRL_DW2_ALGO"))
-    if (std::atoi(e) >= 0) idx.push_back(std::atoi(e));
+  const char* e = std::getenv("SATRL_DW2_ALGO");
+  if (e && std::atoi(e) >= 0) idx.push_back(std::atoi(e));
+  if (!e && H == 256 && S == 4)
+    for (int i : kPreferred256) idx.push_back(i);
   for (int i : idx) {
     std::vector<int> one{i};
     std::vector<hipblasLtMatmulHeuristicResult_t> r;
     if (hipblaslt_ext::getAlgosFromIndex(g_lt, one, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) continue;
+    // an index names a solution only within one library build: take it only
+    // if it is the stream-K MT32x64x64 tile it was measured as (ROCm 7.2's
+    // hipBLASLt; torch's bundled copy has other indices and keeps its heuristic)
+    if (!e) {
+      const std::string name = hipblaslt_ext::getSolutionNameFromAlgo(g_lt, r[0].algo);
+      if (name.find("_MT32x64x64_") == std::string::npos || name.find("_SK3_") == std::string::npos) continue;
+    }
     size_t w = 0;
     if (hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r[0].algo, w) !=
         HIPBLAS_STATUS_SUCCESS)
