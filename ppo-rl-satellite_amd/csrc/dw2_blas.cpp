@@ -5,28 +5,32 @@
 // In column-major terms each slab is D = A B^T with A = H1_s, B = dZ2_s (both
 // H x K, ld H): one strided-batched hipBLASLt matmul over nb*S batches.
 //
-// Algorithm.  Under torch the library is torch's bundled hipBLASLt
-// (libhipblaslt.so.1 resolves to the copy torch already loaded), and
-// tools/blaslt_search.py timed every solution of it that supports these slabs
-// on MI355X: at S = 4 the heuristic's stream-K MT32x64x64 tile (11.7 us back
-// to back) ties the fastest, so its first choice is taken.  A C host without
-// torch loads ROCm 7.2's hipBLASLt, whose heuristic picks a 12.6 us tile
-// while its stream-K MT32x64x64 solution takes 11.0 us: that one is
-// preferred when present (kPreferred256, checked by name).  Every candidate
-// reproduced its output bit for bit over repeated runs (the stream-K fix-up
-// has a fixed order).  SATRL_DW2_ALGO=<solution index> (dev A/B) tries that
-// solution first; SATRL_DW2_ALGO=-1 takes the heuristic's choice.
+// Algorithm: tuned once per shape when the plan is made.  The library
+// heuristic's first choice is good for the bench shape (mb 4096, S 4: its
+// stream-K MT32x64x64 tile, 11.7 us, ties the fastest of torch's bundled
+// hipBLASLt) but not for short splits: at mb 512 / 1024 it picks tiles of
+// 35 / 63 us where stream-K tiles take 8.7 / 8.3 us (tools/blaslt_search.py).
+// So every supported solution (workspace <= 32 MB) is timed on scratch slabs
+// of the shape; the fastest that reproduces its output bit for bit over
+// repeated runs is kept, the heuristic's choice whenever it is within 3 % of
+// that.  Under torch the library is torch's copy (libhipblaslt.so.1 resolves
+// to the one torch loaded); a C host without torch gets ROCm 7.2's, whose
+// solutions differ -- the tuner covers both.  SATRL_DW2_TUNE=0 keeps the
+// heuristic's choice; SATRL_DW2_ALGO=<solution index> (dev A/B) forces one.
 //
 // Plans (descriptors, algorithm, workspace size) are cached per (H, mb, S,
 // nets): create the plan (satrl_ppo_dw2_lib_workspace) outside stream
-// capture; satrl_ppo_dw2_lib itself only enqueues the matmul, so it can be
-// captured into a hipGraph.
+// capture -- tuning allocates scratch and synchronises its own stream;
+// satrl_ppo_dw2_lib itself only enqueues the matmul, so it can be captured
+// into a hipGraph.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
@@ -37,10 +41,7 @@ void satrl_ppo_set_error(const char* msg);   // ppo_kernels.hip: satrl_ppo_last_
 
 namespace {
 
-// ROCm 7.2's hipBLASLt (what a C host without torch loads): its fastest
-// solution for the H = 256, S = 4 slabs, 11.0 us against 12.6 us for its
-// heuristic's first choice (tools/blaslt_search.cpp built against /opt/rocm)
-const int kPreferred256[] = {483347};
+constexpr size_t kWsCap = 32ull << 20;        // workspace a tuned solution may ask for
 
 struct Plan {
   hipblasLtMatmulDesc_t md = nullptr;
@@ -48,11 +49,138 @@ struct Plan {
   hipblasLtMatmulAlgo_t algo{};
   size_t ws = 0;
   int index = -1;
+  float us = -1.0f;                           // tuned time (back to back), -1 untuned
 };
 
 std::mutex g_mu;
 hipblasLtHandle_t g_lt = nullptr;
 std::map<std::tuple<int, int, int, int>, Plan> g_plans;
+std::vector<hipblasLtMatmulHeuristicResult_t> g_all;   // every N x T f32 solution of the library
+
+// scratch operands for the tuner: a hash of the index in [-0.5, 0.5)
+__global__ void fill_kernel(float* p, int64_t n, uint32_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+  h ^= h >> 15; h *= 2246822519u; h ^= h >> 13;
+  p[i] = (float)(h & 0xffffff) / 16777216.0f - 0.5f;
+}
+
+struct Scratch {
+  float *a = nullptr, *b = nullptr, *d = nullptr;
+  void* ws = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  ~Scratch() {
+    if (st) (void)hipStreamSynchronize(st);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    if (d) (void)hipFree(d);
+    if (ws) (void)hipFree(ws);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+// time solution r on the scratch slabs (us per launch, back to back), and
+// whether three runs agree bit for bit; < 0 when it fails to run
+float time_algo(const Plan& p, hipblasLtMatmulAlgo_t& algo, size_t w, Scratch& s, size_t dn, bool* det) {
+  const float alpha = 1.0f, beta = 0.0f;
+  auto run = [&]() {
+    return hipblasLtMatmul(g_lt, p.md, &alpha, s.a, p.la, s.b, p.lb, &beta, s.d, p.lc, s.d, p.lc, &algo, s.ws, w,
+                           s.st) == HIPBLAS_STATUS_SUCCESS;
+  };
+  if (!run()) return -1.0f;                   // (first call: loads the kernel's code object)
+  if (hipStreamSynchronize(s.st) != hipSuccess) return -1.0f;
+  if (det) {
+    std::vector<uint32_t> o0(dn), o1(dn);
+    if (hipMemcpy(o0.data(), s.d, dn * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1.0f;
+    *det = true;
+    for (int k = 0; k < 2 && *det; ++k) {
+      if (hipMemsetAsync(s.d, 0xff, dn * 4, s.st) != hipSuccess || !run() ||
+          hipMemcpyAsync(o1.data(), s.d, dn * 4, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
+          hipStreamSynchronize(s.st) != hipSuccess)
+        return -1.0f;
+      *det = std::memcmp(o0.data(), o1.data(), dn * 4) == 0;
+    }
+  }
+  constexpr int kReps = 5;
+  if (hipEventRecord(s.e0, s.st) != hipSuccess) return -1.0f;
+  for (int k = 0; k < kReps; ++k)
+    if (!run()) return -1.0f;
+  if (hipEventRecord(s.e1, s.st) != hipSuccess || hipEventSynchronize(s.e1) != hipSuccess) return -1.0f;
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, s.e0, s.e1) != hipSuccess) return -1.0f;
+  return ms * 1e3f / kReps;
+}
+
+// fastest deterministic solution (the heuristic's first choice when within 3 %);
+// false leaves p.algo as the heuristic set it
+bool tune(int H, int mb, int S, int nb, Plan& p) {
+  if (g_all.empty() &&
+      hipblaslt_ext::getAllAlgos(g_lt, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_N, HIPBLAS_OP_T, HIP_R_32F,
+                                 HIP_R_32F, HIP_R_32F, HIP_R_32F, HIPBLAS_COMPUTE_32F, g_all) != HIPBLAS_STATUS_SUCCESS)
+    return false;
+  Scratch s;
+  const size_t an = (size_t)nb * mb * H, dn = (size_t)nb * S * H * H;
+  if (hipMalloc(&s.a, an * 4) != hipSuccess || hipMalloc(&s.b, an * 4) != hipSuccess ||
+      hipMalloc(&s.d, dn * 4) != hipSuccess || hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&s.e0) != hipSuccess || hipEventCreate(&s.e1) != hipSuccess)
+    return false;
+  const unsigned gb = (unsigned)((an + 255) / 256);
+  hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(256), 0, s.st, s.a, (int64_t)an, 0x1234u);
+  hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(256), 0, s.st, s.b, (int64_t)an, 0x9e37u);
+  if (hipGetLastError() != hipSuccess) return false;
+  const float alpha = 1.0f, beta = 0.0f;
+  struct Cand { float us; int index; size_t w; hipblasLtMatmulAlgo_t algo; };
+  std::vector<Cand> cands;
+  size_t ws_have = 0;
+  for (auto& r : g_all) {
+    size_t w = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r.algo, w) !=
+            HIPBLAS_STATUS_SUCCESS || w > kWsCap)
+      continue;
+    if (w > ws_have) {                        // grow the tuner's workspace as candidates need it
+      if (s.ws) (void)hipFree(s.ws);
+      s.ws = nullptr;
+      if (hipMalloc(&s.ws, w) != hipSuccess) return false;
+      ws_have = w;
+    }
+    const float us = time_algo(p, r.algo, w, s, dn, nullptr);
+    if (us > 0.0f) cands.push_back({us, hipblaslt_ext::getIndexFromAlgo(r.algo), w, r.algo});
+  }
+  if (cands.empty()) return false;
+  std::sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) {
+    return x.us < y.us || (x.us == y.us && x.index < y.index);
+  });
+  // the heuristic's choice, re-timed beside the field
+  size_t hw = p.ws;
+  bool hdet = false;
+  if (hw > ws_have) {
+    if (s.ws) (void)hipFree(s.ws);
+    s.ws = nullptr;
+    if (hipMalloc(&s.ws, hw) != hipSuccess) return false;
+    ws_have = hw;
+  }
+  const float hus = time_algo(p, p.algo, hw, s, dn, &hdet);
+  for (auto& c : cands) {
+    if (hus > 0.0f && hdet && hus <= 1.03f * c.us) {
+      p.us = hus;                             // heuristic within 3 % of the fastest left: keep it
+      return true;
+    }
+    bool det = false;
+    const float us = time_algo(p, c.algo, c.w, s, dn, &det);
+    if (us > 0.0f && det) {
+      p.algo = c.algo;
+      p.ws = c.w;
+      p.index = c.index;
+      p.us = us;
+      return true;
+    }
+  }
+  return false;
+}
 
 bool make_plan(int H, int mb, int S, int nb, Plan& p) {
   if (!g_lt && hipblasLtCreate(&g_lt) != HIPBLAS_STATUS_SUCCESS) {
@@ -82,37 +210,25 @@ bool make_plan(int H, int mb, int S, int nb, Plan& p) {
     }
   }
   const float alpha = 1.0f, beta = 0.0f;
-  std::vector<int> idx;
-  const char* e = std::getenv("SATRL_DW2_ALGO");
-  if (e && std::atoi(e) >= 0) idx.push_back(std::atoi(e));
-  if (!e && H == 256 && S == 4)
-    for (int i : kPreferred256) idx.push_back(i);
-  for (int i : idx) {
-    std::vector<int> one{i};
+  if (const char* e = std::getenv("SATRL_DW2_ALGO")) {   // dev A/B: one forced solution
+    std::vector<int> one{std::atoi(e)};
     std::vector<hipblasLtMatmulHeuristicResult_t> r;
-    if (hipblaslt_ext::getAlgosFromIndex(g_lt, one, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) continue;
-    // an index names a solution only within one library build: take it only
-    // if it is the stream-K MT32x64x64 tile it was measured as (ROCm 7.2's
-    // hipBLASLt; torch's bundled copy has other indices and keeps its heuristic)
-    if (!e) {
-      const std::string name = hipblaslt_ext::getSolutionNameFromAlgo(g_lt, r[0].algo);
-      if (name.find("_MT32x64x64_") == std::string::npos || name.find("_SK3_") == std::string::npos) continue;
-    }
     size_t w = 0;
-    if (hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r[0].algo, w) !=
-        HIPBLAS_STATUS_SUCCESS)
-      continue;
-    p.algo = r[0].algo;
-    p.ws = w;
-    p.index = i;
-    return true;
+    if (one[0] >= 0 && hipblaslt_ext::getAlgosFromIndex(g_lt, one, r) == HIPBLAS_STATUS_SUCCESS && !r.empty() &&
+        hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r[0].algo, w) ==
+            HIPBLAS_STATUS_SUCCESS) {
+      p.algo = r[0].algo;
+      p.ws = w;
+      p.index = one[0];
+      return true;
+    }
   }
   hipblasLtMatmulPreference_t pref;
   if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) {
     satrl_ppo_set_error("hipBLASLt preference");
     return false;
   }
-  size_t cap = 64ull << 20;
+  size_t cap = kWsCap;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &cap, sizeof(cap));
   hipblasLtMatmulHeuristicResult_t h[1];
   int nh = 0;
@@ -125,6 +241,8 @@ bool make_plan(int H, int mb, int S, int nb, Plan& p) {
   p.algo = h[0].algo;
   p.ws = h[0].workspaceSize;
   p.index = hipblaslt_ext::getIndexFromAlgo(p.algo);
+  const char* t = std::getenv("SATRL_DW2_TUNE");
+  if (!(t && std::strcmp(t, "0") == 0)) tune(H, mb, S, nb, p);   // (untuned: the heuristic's choice stands)
   return true;
 }
 
@@ -169,7 +287,10 @@ int satrl_ppo_dw2_lib(int H, int mb, int net, int S, const float* H1, const floa
   const float alpha = 1.0f, beta = 0.0f;
   const hipblasStatus_t s = hipblasLtMatmul(g_lt, p->md, &alpha, H1, p->la, dZ2, p->lb, &beta, p2, p->lc, p2, p->lc,
                                             &p->algo, ws, p->ws, (hipStream_t)stream);
-  if (s != HIPBLAS_STATUS_SUCCESS) { satrl_ppo_set_error("hipblasLtMatmul"); return -2; }
+  if (s != HIPBLAS_STATUS_SUCCESS) {
+    satrl_ppo_set_error("hipblasLtMatmul");
+    return -2;
+  }
   return 0;
 }
 

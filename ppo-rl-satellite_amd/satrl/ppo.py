@@ -197,8 +197,8 @@ class FusedMinibatch:
         # dW2: the hand-written split-K kernel for H <= 128 (hipBLASLt picks
         # K-serial tiles there: 12.5 us vs 3 us at H = 64); at H = 256 a
         # plain library GEMM (satrl_ppo_dw2_lib: hipBLASLt from the C ABI,
-        # split-K 4, 11.7 us vs 15 us for satrl_ppo_dw2; its heuristic's
-        # stream-K tile ties the fastest of all 245 solutions that fit)
+        # split-K 4, 11.7 us vs 15 us for satrl_ppo_dw2; the plan times the
+        # library's solutions per shape, which matters for short splits)
         self.lib_gemm = learner.H >= 256
         if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob
             self.lib_gemm = os.environ["SATRL_DW2_LIB"] == "1"
