@@ -39,7 +39,8 @@ enum { SATRL_PPO_OFF_W2 = 0, SATRL_PPO_OFF_W1, SATRL_PPO_OFF_B2, SATRL_PPO_OFF_W
 
 /* host helper: element offsets of the flat layout for hidden width H (64, 128 or 256) */
 int satrl_ppo_layout(int H, int64_t* offsets /* [SATRL_PPO_NOFF] */);
-/* number of partial slabs (32-row blocks) and of norm blocks for a minibatch of mb rows */
+/* number of partial slabs (row blocks: 32 rows, or 16 at H = 256 for mb <= 1024) the rowpass of a
+ * minibatch of mb rows -- or of any shorter one -- writes, and of norm blocks */
 int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
 
 /* `net` (rowpass, reduce, adam): -1 = actor and critic in one launch, 0 =
@@ -98,7 +99,7 @@ int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* step
  * src[idx[r]] (idx nullable: rows 0..mb-1 of src, contiguous).  Writes H1
  * and dZ2 [2][mb][H] (inputs of the dW2 GEMM), the tail partial slabs
  * [n_head_wg][6H+12] and the [dW1 | db1] partial slabs [n_head_wg][2][H][20]
- * (n_head_wg = ceil(mb/32), satrl_ppo_sizes).                             */
+ * (n_head_wg from satrl_ppo_sizes).                                      */
 int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const float* W2T,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream);

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <type_traits>
 
@@ -46,8 +47,15 @@ __device__ unsigned long long g_probe[512][16][16][2];
 #endif
 constexpr int kRows = SATRL_RP_ROWS;   // minibatch rows per rowpass workgroup (and per partial slab)
 constexpr int kNW256 = SATRL_RP_NW256; // waves per rowpass workgroup at H = 256
-// rowpass workgroups resident per CU the register allocation must allow
-constexpr int kRpWgPerCU = kRows == 16 ? 2 : 1;
+// rowpass workgroups resident per CU the register allocation must allow (the
+// 8-wave 16-row dev variant runs two per CU)
+template <int R, int NW>
+constexpr int rp_wg_per_cu() { return R == 16 && NW == 8 ? 2 : 1; }
+// short minibatches at H = 256 (configs[3]: 512 rows per rank; ragged tails)
+// run 16-row workgroups of the same 16 waves, one 16-row tile each: twice the
+// workgroups on the chip, and every row's arithmetic -- the forward's MFMA
+// order and output-layer sums included -- is the 32-row kernel's
+constexpr int kRowsShort = 16;
 
 constexpr float kLogSqrt2Pi = 0.9189385332046727f;   // math.log(math.sqrt(2*math.pi))
 
@@ -502,16 +510,16 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
   return od;
 }
 
-template <int H, int NW>
-__global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
+template <int H, int NW, int R = kRows>
+__global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 256)) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const float* __restrict__ W2T, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1, int net_sel) {
-  constexpr int R = kRows, RT = R / 16, LDA = H + 4, CT = H / 16 / NW;
+  constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW;
   const Layout L = layout(H);
-  __shared__ MlpSmem<H, NW> sm;
+  __shared__ MlpSmem<H, NW, R> sm;
   __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
   __shared__ float ax[R][8];
   __shared__ float dz3s[R][4];
@@ -557,7 +565,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
       hcs[2][t0] = 1.0f / var;
     }
   };
-  mlp_forward<H, NW, kRows, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
   if constexpr (SATRL_RP_EARLYD) mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
@@ -572,7 +580,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanh_f32(out_sum<NW, kRows>(sm.osum, r, d) + hb3[d]);
+          th[d] = tanh_f32(out_sum<NW, R>(sm.osum, r, d) + hb3[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           var[d] = hcs[0][d];
           dv[d] = ax[r][d] - mu[d];
@@ -600,7 +608,7 @@ __global__ void __launch_bounds__(NW * 64, kRpWgPerCU * NW * 64 / 256) rowpass_k
           dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        const float vc = out_sum<NW, kRows>(sm.osum, r, 0) + hb3c;
+        const float vc = out_sum<NW, R>(sm.osum, r, 0) + hb3c;
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
@@ -1207,8 +1215,28 @@ __global__ void __launch_bounds__(256) tanh_kernel(int64_t n, const float* __res
   if (i < n) y[i] = tanh_f32(x[i]);
 }
 
-int n_head_wg(int mb) { return (mb + kRows - 1) / kRows; }
-int n_w1_wg(int mb) { return n_head_wg(mb); }
+// rows per rowpass workgroup for a minibatch of mb rows: kRowsShort at
+// H = 256 up to kShortMb rows (SATRL_RP_SHORT_MB, dev A/B; 0 turns it off)
+int short_mb() {
+  static const int v = [] {
+    const char* e = std::getenv("SATRL_RP_SHORT_MB");
+    return e ? std::atoi(e) : 1024;
+  }();
+  return v;
+}
+int rows_per_wg(int H, int mb) { return (H == 256 && kRows == 32 && mb <= short_mb()) ? kRowsShort : kRows; }
+int n_head_wg(int H, int mb) {
+  const int R = rows_per_wg(H, mb);
+  return (mb + R - 1) / R;
+}
+int n_w1_wg(int H, int mb) { return n_head_wg(H, mb); }
+// slab capacity a minibatch of mb rows needs, and any shorter one (a ragged
+// tail of a minibatch above the short threshold can have more row blocks)
+int n_head_wg_cap(int H, int mb) {
+  const int m = mb < short_mb() ? mb : short_mb();
+  const int a = n_head_wg(H, mb), b = m > 0 ? n_head_wg(H, m) : 0;
+  return a > b ? a : b;
+}
 RedGeom geom(int H, int mb, int S, int net = -1) {
   const Layout L = layout(H);
   const int nn = net < 0 ? 2 : 1;                                  // nets covered
@@ -1217,8 +1245,8 @@ RedGeom geom(int H, int mb, int S, int net = -1) {
   g.nb1 = (int)((nn * (int64_t)H * 20 / 4 + (256 / kRedCH1) - 1) / (256 / kRedCH1));
   g.nbt = (int)((L.tail / 4 + (256 / kRedCHt) - 1) / (256 / kRedCHt));
   g.S = S;
-  g.nw1 = n_w1_wg(mb);
-  g.nwg = n_head_wg(mb);
+  g.nw1 = n_w1_wg(H, mb);
+  g.nwg = n_head_wg(H, mb);
   g.net = net;
   return g;
 }
@@ -1257,7 +1285,7 @@ int satrl_ppo_layout(int H, int64_t* off) {
 
 int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
   if (!valid_h(H) || mb <= 0) return -1;
-  if (nwg) *nwg = n_head_wg(mb);
+  if (nwg) *nwg = n_head_wg_cap(H, mb);                         // >= every minibatch of <= mb rows
   if (nblk) *nblk = n_blocks(geom(H, mb, 1, -1));                 // >= the per-net counts
   return 0;
 }
@@ -1267,7 +1295,8 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
                       float* pw1, void* stream) {
   if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1)
     return -1;
-  dim3 g((net < 0 ? 2 : 1) * n_head_wg(mb));      // (row block, net) pairs, or row blocks of one net
+  const int R = rows_per_wg(H, mb);
+  dim3 g((net < 0 ? 2 : 1) * n_head_wg(H, mb));   // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
   if (H == 64)
@@ -1276,6 +1305,9 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
+  else if (R == kRowsShort && kRows != kRowsShort)
+    hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, mb, src, idx, P, W2T, epsilon,
+                       ent_coef, max_action, H1, dZ2, ptail, pw1, net);
   else
     hipLaunchKernelGGL((rowpass_kernel<256, kNW256>), g, dim3(kNW256 * 64), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
