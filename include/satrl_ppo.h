@@ -58,7 +58,7 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
 /* The same slabs through hipBLASLt (the H = 256 path): one strided-batched
  * f32 matmul over nets x S splits, mb % S == 0.  The solution is tuned when
  * the plan is made (the fastest that repeats its output bit for bit; the
- * library heuristic's choice when within 3 % of it).
+ * library heuristic's choice when within 15 % of it).
  * H1 / dZ2 / p2 point at the first selected net's block (net 1 alone: the
  * critic's).  _workspace builds and caches the plan for
  * (H, mb, S, nets) -- call it outside stream capture -- and reports the

@@ -12,8 +12,8 @@
 // 35 / 63 us where stream-K tiles take 8.7 / 8.3 us (tools/blaslt_search.py).
 // So every supported solution (workspace <= 32 MB) is timed on scratch slabs
 // of the shape; the fastest that reproduces its output bit for bit over
-// repeated runs is kept, the heuristic's choice whenever it is within 3 % of
-// that.  Under torch the library is torch's copy (libhipblaslt.so.1 resolves
+// repeated runs is kept, the heuristic's choice whenever it is within 15 % of
+// that (kKeepHeuristic).  Under torch the library is torch's copy (libhipblaslt.so.1 resolves
 // to the one torch loaded); a C host without torch gets ROCm 7.2's, whose
 // solutions differ -- the tuner covers both.  SATRL_DW2_TUNE=0 keeps the
 // heuristic's choice; SATRL_DW2_ALGO=<solution index> (dev A/B) forces one.
@@ -42,6 +42,12 @@ void satrl_ppo_set_error(const char* msg);   // ppo_kernels.hip: satrl_ppo_last_
 namespace {
 
 constexpr size_t kWsCap = 32ull << 20;        // workspace a tuned solution may ask for
+// the heuristic's choice stands unless a solution beats it by more than 15 %
+// on the tuner's clock: back-to-back launches on warm scratch slabs rank
+// tiles differently from the update's graphs, where the operands arrive cold
+// from the rowpass (at mb 4096 a tile 4 % faster there ran 13.9 us in the
+// update against the heuristic's 12.2)
+constexpr float kKeepHeuristic = 1.15f;
 
 struct Plan {
   hipblasLtMatmulDesc_t md = nullptr;
@@ -115,7 +121,7 @@ float time_algo(const Plan& p, hipblasLtMatmulAlgo_t& algo, size_t w, Scratch& s
   return ms * 1e3f / kReps;
 }
 
-// fastest deterministic solution (the heuristic's first choice when within 3 %);
+// fastest deterministic solution (the heuristic's first choice when within 15 %);
 // false leaves p.algo as the heuristic set it
 bool tune(int H, int mb, int S, int nb, Plan& p) {
   if (g_all.empty() &&
@@ -165,8 +171,8 @@ bool tune(int H, int mb, int S, int nb, Plan& p) {
   }
   const float hus = time_algo(p, p.algo, hw, s, dn, &hdet);
   for (auto& c : cands) {
-    if (hus > 0.0f && hdet && hus <= 1.03f * c.us) {
-      p.us = hus;                             // heuristic within 3 % of the fastest left: keep it
+    if (hus > 0.0f && hdet && hus <= kKeepHeuristic * c.us) {
+      p.us = hus;                             // heuristic close to the fastest left: keep it
       return true;
     }
     bool det = false;
