@@ -370,6 +370,30 @@ def test_rowpass_contiguous_rows_match_gather():
         assert torch.equal(a, b)
 
 
+def test_short_rowpass_rows_match_long():
+    """At H = 256 a minibatch of <= 1024 rows runs 16-row workgroups
+    (rowpass_kernel<256, 16, 16>), a longer one 32-row workgroups; every
+    row's arithmetic is the same, so tanh(fc1) (H1) of a 1024-row minibatch
+    equals the first 1024 rows of a 1056-row one bit for bit, for both nets
+    (the forward's later phases share this code; the fused-step tests at
+    mb 512 / 777 / 100 check the short kernel's gradients against torch)."""
+    from satrl.ppo import PPOLearner
+    torch.manual_seed(8)
+    args = _args(hidden_width=256, mini_batch_size=1024, batch_size=8192)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    src = torch.randn((1056, 32), device="cuda", generator=g)
+    src[:, 21:24] = -1.0 - torch.rand((1056, 3), device="cuda", generator=g)
+    H = 256
+    h1 = {}
+    for mb in (1024, 1056):
+        H1, _ = L.stepper(mb).rowpass(src, None, mb)
+        torch.cuda.synchronize()
+        h1[mb] = H1.view(2, mb, H).clone()
+    assert torch.equal(h1[1024], h1[1056][:, :1024])
+
+
 def test_update_graph_groups_equal_eager():
     """FusedMinibatch.run: graph replays that walk the permutation through the
     device group counter (satrl_ppo_stage / satrl_ppo_group_advance), then
