@@ -144,10 +144,11 @@ def cpu_baseline(seconds, n, T, H, mb, epochs):
     r = g.standard_normal(T).astype(np.float32)
     vs = g.standard_normal(T).astype(np.float32)
     dn = (g.random(T) < 0.01).astype(np.float32)
-    t0 = time.perf_counter()
-    for _ in range(2):
+    t_gae_env = float("inf")
+    for _ in range(2):                         # the faster of two samples (shared host)
+        t0 = time.perf_counter()
         O.gae_flat(r, vs, vs, dn, dn)
-    t_gae_env = (time.perf_counter() - t0) / 2
+        t_gae_env = min(t_gae_env, time.perf_counter() - t0)
     t_iter = (T * (t_env_step + t_pol) + (T + 1) * t_val + n * t_gae_env / threads
               + epochs * (n * T // mb) * t_mb)
     total = os.cpu_count() or threads
@@ -157,8 +158,9 @@ def cpu_baseline(seconds, n, T, H, mb, epochs):
                       f"threads of '{cpu_model()}' ({how}; the host has {total} hardware threads), scaled from "
                       f"samples: env step = the product's host build satenv_cpu_step_autoreset, {n} envs x {steps} "
                       f"steps from reset (Flag 0, U(-1.6,1.6) actions, d_capture 15000, max_episode_steps 1000); "
-                      f"policy/values/update = oracle/ppo_cpu.py torch-CPU f32 (8 policy steps, 2 value passes, "
-                      f"24 minibatches); GAE = the reference's python loop on 2 envs x {T}",
+                      f"policy/values/update = oracle/ppo_cpu.py torch-CPU f32 (fastest of 3 samples of 2 policy "
+                      f"steps, of 2 value passes, of 3 samples of 8 minibatches); GAE = the reference's python "
+                      f"loop on 1 env x {T}, faster of 2",
             "iteration_s": t_iter,
             "env_step_only_env_steps_per_s": n / t_env_step,
             "env_only_4096x100": {"threads_1": env_only_1, f"threads_{threads}": env_only_all,
