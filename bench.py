@@ -56,7 +56,16 @@ def parse():
                          "every rank steps --minibatch rows (global minibatch N x --minibatch); 'auto' (default) = "
                          "global for BASELINE configs[3] (65536 envs over 8 GPUs) and at N = 1, per_gpu for the "
                          "weak-scaling series of configs[2] (16384 envs per GPU at N = 2/4/8)")
-    ap.add_argument("--profile-tag", default="r2", help="profiles/<tag>_* files the rocprof cross-check fields read")
+    ap.add_argument("--profile-tag", default="r3", help="profiles/<tag>_* files the rocprof cross-check fields read")
+    ap.add_argument("--global-slice", type=int, default=256,
+                    help="N > 1: minibatches of the configs[3]-semantics slice timed after the run (global "
+                         "minibatch --minibatch, i.e. --minibatch/N rows per rank per Adam step); 0 = off")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: rehearse the launch, barrier, max-over-ranks timing and the rank-0 JSON line "
+                         "with gloo all-reduces of the gradient bucket's size (CPU test of the N-rank path)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on cuda:0 over gloo (RCCL refuses two ranks on "
+                         "one GPU); use a small --num-envs/--horizon, the update is eager there")
     return ap.parse_args()
 
 
@@ -196,7 +205,7 @@ def workload_name(a, world):
             f"global minibatch={gmb} ({gmb // world if world > 1 else gmb} rows per GPU per Adam step), "
             f"{a.epochs} PPO epochs")
     if a.surrogate:
-        desc += ", ImprovedNN surrogate bf16 per env-step"
+        desc += ", ImprovedNN surrogate bf16 per env-step (trained on the reference's golden pairs)"
     if a.horizon == 2048 and gmb == 4096 and a.epochs == 10:
         if world == 1 and a.num_envs == 16384 and a.hidden == 256 and a.surrogate:
             return "BASELINE.json configs[4]: " + desc
@@ -223,15 +232,124 @@ def dp_mode(a, world):
     return "global" if world == 1 or (world == 8 and a.num_envs == 8192) else "per_gpu"
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N fresh copies of this
+    command, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous
+    on 127.0.0.1), and wait for them.  The parent never imports torch or
+    touches a GPU (a process that has initialised the GPU must not exec).
+    Rank 0 prints the JSON line.  If a rank fails, the others are stopped and
+    the parent exits with the failing rank's code."""
+    import signal
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    signal.signal(signal.SIGTERM, lambda *_: (stop(), sys.exit(143)))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                sys.stderr.write(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others\n")
+                stop()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     a = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    world = int(world_env or "1")
+    if world != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU, the two must agree")
+    if a.dry_run:
+        sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
+        from satrl import dist as _dist
+        return _dist.run_or_exit(dry_run, a, world, world=world)
+    sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
+    from satrl import dist as _dist
+    return _dist.run_or_exit(run, a, world, world=world)
+
+
+def dry_run(a, world):
+    """The N-rank launch / barrier / max-over-ranks timing / rank-0 report
+    path without a GPU: gloo process group, each "step" one all-reduce of the
+    per-minibatch gradient bucket (142 860 f32 at H 256)."""
+    import datetime
     import torch
     import torch.distributed as dist
+    from satrl import dist as _dist
+    rank = int(os.environ.get("RANK", "0"))
+    pg = None
+    if world > 1:
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=_dist.dp_timeout_s()))
+        pg = dist.group.WORLD
+        assert dist.get_world_size() == a.gpus, (dist.get_world_size(), a.gpus)
+    g = torch.ones(142860, dtype=torch.float32)
+    cnt = torch.ones(1, dtype=torch.float32)
+    _dist.sum_inplace_(cnt, pg)
+    for _ in range(a.warmup):
+        _dist.sum_inplace_(g, pg)
+    if pg is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        _dist.sum_inplace_(g, pg)
+    if os.environ.get("SATRL_DRY_RUN_FAIL_RANK") == str(rank):     # failure-path test hook
+        os._exit(7)
+    if pg is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if pg is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n_gpus = dist.get_world_size() if pg is not None else 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "env-steps/s", "n_gpus": n_gpus,
+                          "steps": a.steps, "warmup": a.warmup, "ms_per_step": float(t.item()) / a.steps * 1e3,
+                          "dry_run": True, "ranks_seen": int(cnt.item()),
+                          "config": {"workload": workload_name(a, n_gpus), "parallelism": f"dp{n_gpus}"}}),
+              flush=True)
+    if pg is not None:
+        dist.destroy_process_group()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def run(a, world):
+    import datetime
+    import torch
+    import torch.distributed as dist
+    from satrl import dist as _dist
+
     a.dp_minibatch = dp_mode(a, world)
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if a.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     pg = None
     if world > 1 or a.force_dist:
@@ -239,8 +357,15 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        timeout = datetime.timedelta(seconds=_dist.dp_timeout_s())
+        if a.one_device:
+            dist.init_process_group("gloo", timeout=timeout)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         pg = dist.group.WORLD
+        if dist.get_world_size() != a.gpus:
+            raise RuntimeError(f"process group has {dist.get_world_size()} ranks, --gpus {a.gpus}")
+    n_gpus = dist.get_world_size() if pg is not None else 1
 
     from satrl.trainer import VecTrainer, args_param
     args = args_param(batch_size=a.num_envs * a.horizon, mini_batch_size=a.minibatch, hidden_width=a.hidden,
@@ -271,7 +396,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    n_total = a.num_envs * world
+    n_total = a.num_envs * n_gpus
     env_steps = n_total * a.horizon * a.steps
     value = env_steps / elapsed
 
@@ -439,129 +564,189 @@ def main():
     rew = torch.empty(a.num_envs, dtype=torch.float32, device="cuda")
     dn = torch.empty(a.num_envs, dtype=torch.uint8, device="cuda")
 
-    # ---- north-star sweep: the env kernel alone at num_envs 4k / 16k / 64k on this GPU
-    # (autoreset, U(-1.6,1.6) f32 actions cycled from 64 pre-drawn sets, 256 untimed
-    # steps first so episodes are mid-flight and the danger-zone solves are in their
-    # steady mix, then kernel_iters timed launches)
-    from satrl.env import VecSatellites
-    env_sweep = {}
-    gs = torch.Generator(device="cuda").manual_seed(7)
-    for n_sw in (4096, 16384, 65536):
-        e_sw = VecSatellites(n_sw, d_capture=a.d_capture, max_episode_steps=1000)
-        e_sw.reset(0)
-        acts = (torch.rand((64, 2, n_sw, 3), device="cuda", generator=gs) * 3.2 - 1.6).contiguous()
-        o_sw = torch.empty((n_sw, 18), dtype=torch.float32, device="cuda")
-        r_sw = torch.empty(n_sw, dtype=torch.float32, device="cuda")
-        d_sw = torch.empty(n_sw, dtype=torch.uint8, device="cuda")
-        for k in range(256):
-            e_sw.step_autoreset(acts[k % 64, 0], acts[k % 64, 1], o_sw, r_sw, d_sw)
+    # ---- single-GPU figures (sweeps, propagators, RD grid, surrogate): measured at N = 1;
+    # at N > 1 every rank would repeat them on its own GPU, so the N-rank run skips them
+    env_sweep, rollout_sweep = None, None
+    if world == 1:
+        # ---- north-star sweep: the env kernel alone at num_envs 4k / 16k / 64k on this GPU
+        # (autoreset, U(-1.6,1.6) f32 actions cycled from 64 pre-drawn sets, 256 untimed
+        # steps first so episodes are mid-flight and the danger-zone solves are in their
+        # steady mix, then kernel_iters timed launches)
+        from satrl.env import VecSatellites
+        env_sweep = {}
+        gs = torch.Generator(device="cuda").manual_seed(7)
+        for n_sw in (4096, 16384, 65536):
+            e_sw = VecSatellites(n_sw, d_capture=a.d_capture, max_episode_steps=1000)
+            e_sw.reset(0)
+            acts = (torch.rand((64, 2, n_sw, 3), device="cuda", generator=gs) * 3.2 - 1.6).contiguous()
+            o_sw = torch.empty((n_sw, 18), dtype=torch.float32, device="cuda")
+            r_sw = torch.empty(n_sw, dtype=torch.float32, device="cuda")
+            d_sw = torch.empty(n_sw, dtype=torch.uint8, device="cuda")
+            for k in range(256):
+                e_sw.step_autoreset(acts[k % 64, 0], acts[k % 64, 1], o_sw, r_sw, d_sw)
+            e0.record()
+            for k in range(a.kernel_iters):
+                e_sw.step_autoreset(acts[k % 64, 0], acts[k % 64, 1], o_sw, r_sw, d_sw)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+            gbs = n_sw * ENV_BYTES_PER_STEP / (us * 1e-6) / 1e9
+            env_sweep[str(n_sw)] = {"avg_launch_us": us, "env_steps_per_s": n_sw / (us * 1e-6), "achieved_GBs": gbs,
+                                    "hbm_frac": gbs / HBM_PEAK_GBS}
+            del e_sw, acts
+
+        # ---- north-star sweep, end to end: the rollout (both agents' policy kernel ->
+        # Philox sampling -> env step, hipGraph chunks) at num_envs 4k / 16k / 64k, a
+        # 256-step horizon after one untimed collect (graphs captured, episodes mid-flight)
+        rollout_sweep = {}
+        for n_sw in (4096, 16384, 65536):
+            a_sw = args_param(batch_size=n_sw * 256, mini_batch_size=a.minibatch, hidden_width=a.hidden, K_epochs=1,
+                              max_episode_steps=1000, num_envs=n_sw, horizon=256, seed=0, max_train_steps=int(3e6),
+                              chkpt_dir="/tmp")
+            tr_sw = VecTrainer(a_sw, flag=0, d_capture=a.d_capture)
+            tr_sw.collect()
+            torch.cuda.synchronize()
+            e0.record()
+            tr_sw.collect()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1)
+            rollout_sweep[str(n_sw)] = {"ms_per_256_steps": ms, "env_steps_per_s": n_sw * 256 / (ms * 1e-3)}
+            del tr_sw
+
+        # ---- §8f propagators: RK4 two-body + J2 batch kernel, and the env step in RK4-CW mode
+        from satrl.env import rk4_j2
+        g = torch.Generator(device="cuda").manual_seed(3)
+        rv = torch.empty((a.num_envs, 6), dtype=torch.float64, device="cuda")
+        rv[:, :3] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 7000.0
+        rv[:, 3:] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 5.0
+        rk_steps = 100
+        rk4_j2(rv, 1.0, 2)
         e0.record()
-        for k in range(a.kernel_iters):
-            e_sw.step_autoreset(acts[k % 64, 0], acts[k % 64, 1], o_sw, r_sw, d_sw)
+        rk4_j2(rv, 1.0, rk_steps)
         e1.record()
         torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
-        gbs = n_sw * ENV_BYTES_PER_STEP / (us * 1e-6) / 1e9
-        env_sweep[str(n_sw)] = {"avg_launch_us": us, "env_steps_per_s": n_sw / (us * 1e-6), "achieved_GBs": gbs,
-                                "hbm_frac": gbs / HBM_PEAK_GBS}
-        del e_sw, acts
-
-    # ---- north-star sweep, end to end: the rollout (both agents' policy kernel ->
-    # Philox sampling -> env step, hipGraph chunks) at num_envs 4k / 16k / 64k, a
-    # 256-step horizon after one untimed collect (graphs captured, episodes mid-flight)
-    rollout_sweep = {}
-    for n_sw in (4096, 16384, 65536):
-        a_sw = args_param(batch_size=n_sw * 256, mini_batch_size=a.minibatch, hidden_width=a.hidden, K_epochs=1,
-                          max_episode_steps=1000, num_envs=n_sw, horizon=256, seed=0, max_train_steps=int(3e6),
-                          chkpt_dir="/tmp")
-        tr_sw = VecTrainer(a_sw, flag=0, d_capture=a.d_capture)
-        tr_sw.collect()
-        torch.cuda.synchronize()
+        rk4_ms = e0.elapsed_time(e1)
+        env_rk = VecSatellites(a.num_envs, d_capture=a.d_capture, max_episode_steps=1000, propagator=1, rk4_substeps=10)
+        env_rk.reset(0)
+        for _ in range(10):
+            env_rk.step_autoreset(pa, ea, obs, rew, dn)
         e0.record()
-        tr_sw.collect()
+        for _ in range(a.kernel_iters):
+            env_rk.step_autoreset(pa, ea, obs, rew, dn)
         e1.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1)
-        rollout_sweep[str(n_sw)] = {"ms_per_256_steps": ms, "env_steps_per_s": n_sw * 256 / (ms * 1e-3)}
-        del tr_sw
+        env_rk_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+        # propagator 2: solve_ivp RK45 on the CW orbit_ode (satellite_function.py:783-839)
+        env_rk.set_params(propagator=2)
+        env_rk.reset(0)
+        for _ in range(10):
+            env_rk.step_autoreset(pa, ea, obs, rew, dn)
+        e0.record()
+        for _ in range(a.kernel_iters):
+            env_rk.step_autoreset(pa, ea, obs, rew, dn)
+        e1.record()
+        torch.cuda.synchronize()
+        env_rk45_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+        del env_rk
 
-    # ---- §8f propagators: RK4 two-body + J2 batch kernel, and the env step in RK4-CW mode
-    from satrl.env import rk4_j2
-    g = torch.Generator(device="cuda").manual_seed(3)
-    rv = torch.empty((a.num_envs, 6), dtype=torch.float64, device="cuda")
-    rv[:, :3] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 7000.0
-    rv[:, 3:] = torch.randn((a.num_envs, 3), dtype=torch.float64, device="cuda", generator=g) * 5.0
-    rk_steps = 100
-    rk4_j2(rv, 1.0, 2)
-    e0.record()
-    rk4_j2(rv, 1.0, rk_steps)
-    e1.record()
-    torch.cuda.synchronize()
-    rk4_ms = e0.elapsed_time(e1)
-    env_rk = VecSatellites(a.num_envs, d_capture=a.d_capture, max_episode_steps=1000, propagator=1, rk4_substeps=10)
-    env_rk.reset(0)
-    for _ in range(10):
-        env_rk.step_autoreset(pa, ea, obs, rew, dn)
-    e0.record()
-    for _ in range(a.kernel_iters):
-        env_rk.step_autoreset(pa, ea, obs, rew, dn)
-    e1.record()
-    torch.cuda.synchronize()
-    env_rk_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
-    # propagator 2: solve_ivp RK45 on the CW orbit_ode (satellite_function.py:783-839)
-    env_rk.set_params(propagator=2)
-    env_rk.reset(0)
-    for _ in range(10):
-        env_rk.step_autoreset(pa, ea, obs, rew, dn)
-    e0.record()
-    for _ in range(a.kernel_iters):
-        env_rk.step_autoreset(pa, ea, obs, rew, dn)
-    e1.record()
-    torch.cuda.synchronize()
-    env_rk45_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
-    del env_rk
+        # ---- §8f rank 4: reachable-domain grid (RD_single_pulse.py:40-148), the reference's
+        # default 1 x 201 x 201 direction grid for a batch of orbits in one launch
+        from satrl import reachable as RD
+        rd_sets = 256
+        gr = np.random.default_rng(5)
+        rd_orb = RD.orbits_tensor(gr.uniform(7e6, 5e7, rd_sets), gr.uniform(0.0, 0.8, rd_sets),
+                                  gr.uniform(0.05, 2 * np.pi - 0.05, rd_sets), gr.uniform(50.0, 1000.0, rd_sets),
+                                  device="cuda")
+        rd_out = RD.reachable_domain_grid(rd_orb, 1, 200, 200)
+        rd_reach = int((rd_out[2] == 1).sum())
+        rd_iters = 5
+        e0.record()
+        for _ in range(rd_iters):
+            RD.reachable_domain_grid(rd_orb, 1, 200, 200)
+        e1.record()
+        torch.cuda.synchronize()
+        rd_ms = e0.elapsed_time(e1) / rd_iters
+        ell, ell_info = RD.ellipse_fit(*rd_out)
+        e0.record()
+        for _ in range(rd_iters):
+            RD.ellipse_fit(*rd_out)
+        e1.record()
+        torch.cuda.synchronize()
+        ell_ms = e0.elapsed_time(e1) / rd_iters
+        ell_ok = int((ell_info > 0).sum())
+        del rd_out, ell, ell_info
 
-    # ---- §8f rank 4: reachable-domain grid (RD_single_pulse.py:40-148), the reference's
-    # default 1 x 201 x 201 direction grid for a batch of orbits in one launch
-    from satrl import reachable as RD
-    rd_sets = 256
-    gr = np.random.default_rng(5)
-    rd_orb = RD.orbits_tensor(gr.uniform(7e6, 5e7, rd_sets), gr.uniform(0.0, 0.8, rd_sets),
-                              gr.uniform(0.05, 2 * np.pi - 0.05, rd_sets), gr.uniform(50.0, 1000.0, rd_sets),
-                              device="cuda")
-    rd_out = RD.reachable_domain_grid(rd_orb, 1, 200, 200)
-    rd_reach = int((rd_out[2] == 1).sum())
-    rd_iters = 5
-    e0.record()
-    for _ in range(rd_iters):
-        RD.reachable_domain_grid(rd_orb, 1, 200, 200)
-    e1.record()
-    torch.cuda.synchronize()
-    rd_ms = e0.elapsed_time(e1) / rd_iters
-    ell, ell_info = RD.ellipse_fit(*rd_out)
-    e0.record()
-    for _ in range(rd_iters):
-        RD.ellipse_fit(*rd_out)
-    e1.record()
-    torch.cuda.synchronize()
-    ell_ms = e0.elapsed_time(e1) / rd_iters
-    ell_ok = int((ell_info > 0).sum())
-    del rd_out, ell, ell_info
+        # ---- config 5 kernel: ImprovedNN surrogate (bf16 MFMA) on every env's current orbit
+        from satrl.surrogate import Surrogate
+        sur = tr.surrogate if tr.surrogate is not None else Surrogate(device="cuda", seed=0)
+        sur_out = torch.empty((a.num_envs, 10), dtype=torch.float32, device="cuda")
+        for _ in range(10):
+            sur.env_forward(env, out=sur_out)
+        e0.record()
+        for _ in range(a.kernel_iters):
+            sur.env_forward(env, out=sur_out)
+        e1.record()
+        torch.cuda.synchronize()
+        sur_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
+        sur_flop = a.num_envs * SURROGATE_FLOP_PER_ENV
+        sur_tfs = sur_flop / (sur_us * 1e-6) / 1e12
 
-    # ---- config 5 kernel: ImprovedNN surrogate (bf16 MFMA) on every env's current orbit
-    from satrl.surrogate import Surrogate
-    sur = tr.surrogate if tr.surrogate is not None else Surrogate(device="cuda", seed=0)
-    sur_out = torch.empty((a.num_envs, 10), dtype=torch.float32, device="cuda")
-    for _ in range(10):
-        sur.env_forward(env, out=sur_out)
-    e0.record()
-    for _ in range(a.kernel_iters):
-        sur.env_forward(env, out=sur_out)
-    e1.record()
-    torch.cuda.synchronize()
-    sur_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
-    sur_flop = a.num_envs * SURROGATE_FLOP_PER_ENV
-    sur_tfs = sur_flop / (sur_us * 1e-6) / 1e12
+    # ---- data parallelism (N > 1): the per-minibatch gradient all-reduce alone, and a
+    # bounded slice of the configs[3] semantics (global minibatch --minibatch over the N
+    # ranks: minibatch/N rows per rank per Adam step, the all-reduce on the chain)
+    dp_out = {}
+    if pg is not None:
+        dp = {"world": n_gpus, "backend": dist.get_backend(pg), "dp_minibatch": tr.dp_minibatch,
+              "gradient_bucket_bytes": L.G.numel() * 4, "minibatch_step_us": t_chain,
+              "dw2_plan": {"solution": st.dw2_algo if st.lib_gemm else None,
+                           "source": getattr(st, "dw2_source", None) if st.lib_gemm else None}}
+        if L.comm is not None:
+            scratch = torch.zeros_like(L.G)
+            L.comm.warm(scratch)
+            barrier()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.kernel_iters):
+                L.comm.all_reduce_sum_(scratch)
+            e1.record()
+            torch.cuda.synchronize()
+            ar = torch.tensor([e0.elapsed_time(e1) * 1e3 / a.kernel_iters], dtype=torch.float64, device="cuda")
+            dist.all_reduce(ar, op=dist.ReduceOp.MAX)
+            dp["allreduce_us"] = float(ar.item())
+            dp["allreduce_timing"] = ("HIP events on the compute stream around kernel_iters back-to-back "
+                                      "ncclAllReduce calls (satrl.rccl, the call the update's graphs capture), "
+                                      "max over ranks")
+        if a.global_slice > 0 and tr.dp_minibatch == "per_gpu" and a.minibatch % n_gpus == 0:
+            mbg = a.minibatch // n_gpus
+            stg = L.stepper(mbg)
+            gperm = torch.randperm(src.shape[0], device="cuda", generator=g)[:a.global_slice * mbg].contiguous()
+            stg.run(src, gperm)                      # plans, captures the graphs, warms
+            torch.cuda.synchronize()
+            barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            stg.run(src, gperm)
+            torch.cuda.synchronize()
+            barrier()
+            torch.cuda.synchronize()
+            tg = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+            us_g = float(tg.item()) / a.global_slice * 1e6
+            steps_c3 = a.epochs * (65536 * a.horizon) // a.minibatch
+            dp["configs3_semantics_slice"] = {
+                "global_minibatch": a.minibatch, "rows_per_rank": mbg, "minibatches": a.global_slice,
+                "us_per_global_minibatch_step": us_g,
+                "dw2_plan": {"solution": stg.dw2_algo if stg.lib_gemm else None,
+                             "source": getattr(stg, "dw2_source", None) if stg.lib_gemm else None},
+                "note": ("global-minibatch mode (the reference's BatchSampler(..., 4096) semantics, "
+                         "ppo_continuous.py:215) timed on a bounded slice after the run: wall time of "
+                         f"{a.global_slice} minibatch steps between barriers, max over ranks; the "
+                         "all-reduce is on every step's critical path"),
+                "configs3_update_s_projected": steps_c3 * us_g * 1e-6,
+                "configs3_projection": f"BASELINE configs[3] (65536 envs, T {a.horizon}, {a.epochs} epochs, global "
+                                       f"minibatch {a.minibatch}) has {steps_c3} global minibatch steps per update"}
+        dp_out = {"data_parallel": dp}
 
     rollout_ms = sum(timers["rollout_ms"]) / len(timers["rollout_ms"])
     update_ms = sum(timers["update_ms"]) / len(timers["update_ms"])
@@ -578,16 +763,16 @@ def main():
                            a.epochs) if host_baseline else None
         rd_cpu_ms = rd_cpu_baseline() if host_baseline else None
         out = {
-            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": n_gpus, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64+f32",
             "data": "synthetic: reference reset state, random-init (orthogonal, seed 0) policies",
-            "config": {"workload": workload_name(a, world),
+            "config": {"workload": workload_name(a, n_gpus),
                        "num_envs_per_gpu": a.num_envs, "num_envs_total": n_total, "horizon": a.horizon,
                        "hidden": a.hidden, "minibatch_global": tr.global_minibatch,
                        "minibatch_rows_per_gpu": tr.mb_local, "dp_minibatch": tr.dp_minibatch,
                        "minibatch_sampler": tr.sampler, "epochs": a.epochs,
-                       "d_capture": a.d_capture, "parallelism": f"dp{world}"},
+                       "d_capture": a.d_capture, "parallelism": f"dp{n_gpus}"},
             "ppo_updates_per_s": a.steps / elapsed,
             "rollout_env_steps_per_s": n_total * a.horizon / (rollout_ms * 1e-3),
             "rollout_sweep_num_envs": rollout_sweep,
@@ -644,32 +829,35 @@ def main():
                                 "frac": upd_tfs / FP32_MFMA_PEAK_TFS,
                                 "flop_per_transition_epoch": flop_per_transition_epoch},
             "roofline_policy": policy_roof,
-            "propagators": {"rk4_j2_state_steps_per_s": a.num_envs * rk_steps / (rk4_ms * 1e-3),
-                            "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
-                            "env_rk4_cw_avg_launch_us": env_rk_us,
-                            "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6),
-                            "env_rk45_cw_avg_launch_us": env_rk45_us,
-                            "env_rk45_cw_env_steps_per_s": a.num_envs / (env_rk45_us * 1e-6),
-                            "note": "rk4_cw: propagator 1 (RK4, 10 substeps); rk45_cw: propagator 2, the "
-                                    "reference's solve_ivp RK45 on orbit_ode (satellite_function.py:783-839)"},
-            "surrogate": {"kernel": "satenv_surrogate (ImprovedNN 5-256-128-64-10, bf16 MFMA 16x16x32, f32 acc)",
-                          "in_rollout": bool(a.surrogate), "avg_launch_us": sur_us,
-                          "env_steps_per_s": a.num_envs / (sur_us * 1e-6), "bound": "mfma",
-                          "achieved": sur_tfs, "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                          "frac": sur_tfs / BF16_MFMA_PEAK_TFS, "flop_per_env": SURROGATE_FLOP_PER_ENV,
-                          "note": "latency bound: 91 KB of packed weights staged into LDS per workgroup; "
-                                  "FP64 orbital elements per env"},
-            "reachable_domain": {"grids_per_s": rd_sets / (rd_ms * 1e-3), "ms_per_launch": rd_ms,
-                                 "sample": f"{rd_sets} random orbits x 201 x 201 directions (RD_single_pulse "
-                                           "defaults N1=1, N2=N3=200), one launch incl. output zero-fill",
-                                 "reachable_directions": rd_reach,
-                                 "cpu_oracle_ms_per_grid": rd_cpu_ms[0] if rd_cpu_ms else None,
-                                 "ellipse_fit_ms_per_launch": ell_ms,
-                                 "ellipse_fits_per_s": 2 * rd_sets / (ell_ms * 1e-3), "ellipse_fits_ok": ell_ok,
-                                 "grid_plus_fit_orbits_per_s": rd_sets / ((rd_ms + ell_ms) * 1e-3),
-                                 "cpu_oracle_ms_per_curve_fitting": rd_cpu_ms[1] if rd_cpu_ms else None},
             "cpu_baseline": cpu,
         }
+        if world == 1:
+            out.update({
+                "propagators": {"rk4_j2_state_steps_per_s": a.num_envs * rk_steps / (rk4_ms * 1e-3),
+                                "rk4_j2_sample": f"{a.num_envs} states x {rk_steps} RK4 steps (h=1 s), one launch",
+                                "env_rk4_cw_avg_launch_us": env_rk_us,
+                                "env_rk4_cw_env_steps_per_s": a.num_envs / (env_rk_us * 1e-6),
+                                "env_rk45_cw_avg_launch_us": env_rk45_us,
+                                "env_rk45_cw_env_steps_per_s": a.num_envs / (env_rk45_us * 1e-6),
+                                "note": "rk4_cw: propagator 1 (RK4, 10 substeps); rk45_cw: propagator 2, the "
+                                        "reference's solve_ivp RK45 on orbit_ode (satellite_function.py:783-839)"},
+                "surrogate": {"kernel": "satenv_surrogate (ImprovedNN 5-256-128-64-10, bf16 MFMA 16x16x32, f32 acc)",
+                              "in_rollout": bool(a.surrogate), "avg_launch_us": sur_us,
+                              "env_steps_per_s": a.num_envs / (sur_us * 1e-6), "bound": "mfma",
+                              "achieved": sur_tfs, "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                              "frac": sur_tfs / BF16_MFMA_PEAK_TFS, "flop_per_env": SURROGATE_FLOP_PER_ENV,
+                              "note": "latency bound: 91 KB of packed weights staged into LDS per workgroup; "
+                                      "FP64 orbital elements per env"},
+                "reachable_domain": {"grids_per_s": rd_sets / (rd_ms * 1e-3), "ms_per_launch": rd_ms,
+                                     "sample": f"{rd_sets} random orbits x 201 x 201 directions (RD_single_pulse "
+                                               "defaults N1=1, N2=N3=200), one launch incl. output zero-fill",
+                                     "reachable_directions": rd_reach,
+                                     "cpu_oracle_ms_per_grid": rd_cpu_ms[0] if rd_cpu_ms else None,
+                                     "ellipse_fit_ms_per_launch": ell_ms,
+                                     "ellipse_fits_per_s": 2 * rd_sets / (ell_ms * 1e-3), "ellipse_fits_ok": ell_ok,
+                                     "grid_plus_fit_orbits_per_s": rd_sets / ((rd_ms + ell_ms) * 1e-3),
+                                     "cpu_oracle_ms_per_curve_fitting": rd_cpu_ms[1] if rd_cpu_ms else None}})
+        out.update(dp_out)
         print(json.dumps(out), flush=True)
     if pg is not None:
         dist.destroy_process_group()

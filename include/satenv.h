@@ -219,6 +219,16 @@ int satenv_surrogate_pack(const float* w1, const float* b1, const float* w2, con
                           const float* b3, const float* w4, const float* b4, void* blob, void* stream);
 int satenv_surrogate(satenv_env* h, const void* blob, float* out, void* stream);
 int satenv_surrogate_mlp(int64_t n, const float* x, const void* blob, float* out, void* stream);
+/* The offline trainer's StandardScalers (single_pulse_fully_connected_model.py:
+ * 273-278: input_scaler / output_scaler, fitted on all_input.csv /
+ * output_data.csv) into the blob: the kernels standardise the features in f64
+ * before the bf16 input layer, (x - in_mean) / in_scale, and map fc4's output
+ * back, y * out_scale + out_mean (sklearn's transform / inverse_transform), so
+ * a net trained on standardised data emits real ellipse parameters.  Host
+ * arrays of 5, 5, 10, 10 doubles (sklearn's mean_ / scale_).  _pack resets
+ * them to the identity (the reference's untrained-scaler MLPNet2 path).      */
+int satenv_surrogate_set_scalers(void* blob, const double* in_mean, const double* in_scale, const double* out_mean,
+                                 const double* out_scale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -66,6 +66,16 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
 int satrl_ppo_dw2_lib_workspace(int H, int mb, int net, int S, int64_t* ws_bytes, int* algo_index);
 int satrl_ppo_dw2_lib(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* workspace,
                       int64_t ws_bytes, void* stream);
+/* Reproducible plans: _pin makes (or remakes, outside capture) the plan of
+ * (H, mb, S, nets) with solution `algo_index`; `kernel` (nullable) must be
+ * that solution's kernel name in the loaded hipBLASLt (an index names another
+ * solution in another library build): -3 when it is unsupported or differs.
+ * _plan_info reports a made plan's solution index and kernel name.  The
+ * Python host pins every shape from a committed table (satrl/dw2_plans.json)
+ * and, under data parallelism, to rank 0's choice, so every rank and every
+ * run sums dW2 with the same tiles.                                        */
+int satrl_ppo_dw2_lib_pin(int H, int mb, int net, int S, int algo_index, const char* kernel);
+int satrl_ppo_dw2_lib_plan_info(int H, int mb, int net, int S, int* algo_index, char* kernel, int kernel_len);
 
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -48,6 +49,7 @@ constexpr size_t kWsCap = 32ull << 20;        // workspace a tuned solution may 
 // from the rowpass (at mb 4096 a tile 4 % faster there ran 13.9 us in the
 // update against the heuristic's 12.2)
 constexpr float kKeepHeuristic = 1.15f;
+constexpr float kTie = 1.05f;                 // candidates within 5 % of the fastest tie
 
 struct Plan {
   hipblasLtMatmulDesc_t md = nullptr;
@@ -170,6 +172,16 @@ bool tune(int H, int mb, int S, int nb, Plan& p) {
     ws_have = hw;
   }
   const float hus = time_algo(p, p.algo, hw, s, dn, &hdet);
+  // near-ties (stream-K tiles at short splits time within noise of each
+  // other) go to the lowest solution index, so that independent processes
+  // mostly agree; the pinned table (satrl/dw2_plans.json) and the rank-0
+  // broadcast under data parallelism make the choice exact
+  const float best = cands.front().us;
+  std::stable_sort(cands.begin(), cands.end(), [best](const Cand& x, const Cand& y) {
+    const bool tx = x.us <= kTie * best, ty = y.us <= kTie * best;
+    if (tx != ty) return tx;
+    return tx ? x.index < y.index : x.us < y.us;
+  });
   for (auto& c : cands) {
     if (hus > 0.0f && hdet && hus <= kKeepHeuristic * c.us) {
       p.us = hus;                             // heuristic close to the fastest left: keep it
@@ -188,7 +200,7 @@ bool tune(int H, int mb, int S, int nb, Plan& p) {
   return false;
 }
 
-bool make_plan(int H, int mb, int S, int nb, Plan& p) {
+bool make_descriptors(int H, int mb, int S, int nb, Plan& p) {
   if (!g_lt && hipblasLtCreate(&g_lt) != HIPBLAS_STATUS_SUCCESS) {
     satrl_ppo_set_error("hipblasLtCreate");
     return false;
@@ -215,6 +227,38 @@ bool make_plan(int H, int mb, int S, int nb, Plan& p) {
       return false;
     }
   }
+  return true;
+}
+
+std::string kernel_name(hipblasLtMatmulAlgo_t& algo) {
+  return hipblaslt_ext::getKernelNameFromAlgo(g_lt, algo);
+}
+
+// the plan with solution `index` (its kernel name checked when kname is given)
+bool make_pinned(int H, int mb, int S, int nb, int index, const char* kname, Plan& p) {
+  if (!make_descriptors(H, mb, S, nb, p)) return false;
+  const float alpha = 1.0f, beta = 0.0f;
+  std::vector<int> one{index};
+  std::vector<hipblasLtMatmulHeuristicResult_t> r;
+  size_t w = 0;
+  if (index < 0 || hipblaslt_ext::getAlgosFromIndex(g_lt, one, r) != HIPBLAS_STATUS_SUCCESS || r.empty() ||
+      hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r[0].algo, w) !=
+          HIPBLAS_STATUS_SUCCESS || w > kWsCap) {
+    satrl_ppo_set_error("pinned dW2 solution not supported by this hipBLASLt for the shape");
+    return false;
+  }
+  if (kname && *kname && kernel_name(r[0].algo) != kname) {
+    satrl_ppo_set_error("pinned dW2 solution index names another kernel in this hipBLASLt");
+    return false;
+  }
+  p.algo = r[0].algo;
+  p.ws = w;
+  p.index = index;
+  return true;
+}
+
+bool make_plan(int H, int mb, int S, int nb, Plan& p) {
+  if (!make_descriptors(H, mb, S, nb, p)) return false;
   const float alpha = 1.0f, beta = 0.0f;
   if (const char* e = std::getenv("SATRL_DW2_ALGO")) {   // dev A/B: one forced solution
     std::vector<int> one{std::atoi(e)};
@@ -252,19 +296,37 @@ bool make_plan(int H, int mb, int S, int nb, Plan& p) {
   return true;
 }
 
-Plan* plan(int H, int mb, int S, int nb) {
-  std::lock_guard<std::mutex> lk(g_mu);
+void release(Plan& p) {
+  for (auto l : {p.la, p.lb, p.lc})
+    if (l) hipblasLtMatrixLayoutDestroy(l);
+  if (p.md) hipblasLtMatmulDescDestroy(p.md);
+  p = Plan{};
+}
+
+// pinned: -1 = make the plan by the heuristic + tuner; >= 0 = this solution
+// index only (the kernel name, when given, must match: an index names
+// another solution in another library build)
+Plan* plan_locked(int H, int mb, int S, int nb, int pinned = -1, const char* kname = nullptr) {
   const auto key = std::make_tuple(H, mb, S, nb);
   auto it = g_plans.find(key);
-  if (it != g_plans.end()) return &it->second;
+  if (it != g_plans.end() && (pinned < 0 || it->second.index == pinned)) return &it->second;
   Plan p;
-  if (!make_plan(H, mb, S, nb, p)) {                 // release what a failed plan created
-    for (auto l : {p.la, p.lb, p.lc})
-      if (l) hipblasLtMatrixLayoutDestroy(l);
-    if (p.md) hipblasLtMatmulDescDestroy(p.md);
+  const bool ok = pinned < 0 ? make_plan(H, mb, S, nb, p) : make_pinned(H, mb, S, nb, pinned, kname, p);
+  if (!ok) {                                         // release what a failed plan created
+    release(p);
     return nullptr;
   }
+  if (it != g_plans.end()) {                         // re-pin: the old descriptors go
+    release(it->second);
+    it->second = p;
+    return &it->second;
+  }
   return &g_plans.emplace(key, p).first->second;
+}
+
+Plan* plan(int H, int mb, int S, int nb) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return plan_locked(H, mb, S, nb);
 }
 
 bool args_ok(int H, int mb, int net, int S) {
@@ -281,6 +343,28 @@ int satrl_ppo_dw2_lib_workspace(int H, int mb, int net, int S, int64_t* ws_bytes
   if (!p) return -2;
   *ws_bytes = (int64_t)p->ws;
   if (algo_index) *algo_index = p->index;
+  return 0;
+}
+
+int satrl_ppo_dw2_lib_pin(int H, int mb, int net, int S, int algo_index, const char* kernel) {
+  if (!args_ok(H, mb, net, S) || algo_index < 0) return -1;
+  std::lock_guard<std::mutex> lk(g_mu);
+  return plan_locked(H, mb, S, net < 0 ? 2 : 1, algo_index, kernel) ? 0 : -3;
+}
+
+int satrl_ppo_dw2_lib_plan_info(int H, int mb, int net, int S, int* algo_index, char* kernel, int kernel_len) {
+  if (!args_ok(H, mb, net, S) || !algo_index || (kernel && kernel_len < 1)) return -1;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_plans.find(std::make_tuple(H, mb, S, net < 0 ? 2 : 1));
+  if (it == g_plans.end()) {
+    satrl_ppo_set_error("no dW2 plan for the shape: make it first (satrl_ppo_dw2_lib_workspace)");
+    return -2;
+  }
+  *algo_index = it->second.index;
+  if (kernel) {
+    const std::string k = kernel_name(it->second.algo);
+    std::snprintf(kernel, (size_t)kernel_len, "%s", k.c_str());
+  }
   return 0;
 }
 

@@ -596,6 +596,7 @@ __global__ void __launch_bounds__(surrogate::kThreads) surrogate_kernel(const Pa
   __syncthreads();
   const unsigned short* W = reinterpret_cast<const unsigned short*>(lds);
   const float* Bs = reinterpret_cast<const float*>(lds + kBiasOffBytes);
+  const Scalers& SC = *reinterpret_cast<const Scalers*>(lds + kScaleOffBytes);
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile * 16 < n; tile += (int64_t)gridDim.x * 4) {
     const int64_t env = tile * 16 + c;
@@ -605,7 +606,7 @@ __global__ void __launch_bounds__(surrogate::kThreads) surrogate_kernel(const Pa
     for (int k = 0; k < 8; ++k) in1[0][k] = 0;
     int ok = 0;
     if (g == 0 && valid) {
-      float fv[kIn];
+      double fv[kIn];
       if (x) {
 #pragma unroll
         for (int k = 0; k < kIn; ++k) fv[k] = x[env * kIn + k];
@@ -616,11 +617,12 @@ __global__ void __launch_bounds__(surrogate::kThreads) surrogate_kernel(const Pa
                                         prm.R_cw[2] + f64[2 * n + env], prm.V_cw[0] + f64[3 * n + env],
                                         prm.V_cw[1] + f64[4 * n + env], prm.V_cw[2] + f64[5 * n + env], E);
         ok = rc == 0;
+        // the reference's float32 feature tensor (real_time_data_process.py:117)
         fv[0] = (float)E.a; fv[1] = (float)E.e; fv[2] = (float)E.i; fv[3] = (float)E.f;
         fv[4] = (float)f64[12 * n + env];
       }
 #pragma unroll
-      for (int k = 0; k < kIn; ++k) in1[0][k] = (short)f2bf(fv[k]);
+      for (int k = 0; k < kIn; ++k) in1[0][k] = (short)f2bf((float)((fv[k] - SC.in_mean[k]) / SC.in_scale[k]));
     }
     ok = __shfl(ok, c, 64);
     frag_ab h1[8], h2[4], h3[2];
@@ -637,7 +639,9 @@ __global__ void __launch_bounds__(surrogate::kThreads) surrogate_kernel(const Pa
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int o = 4 * g + i;
-        if (o < kOut) out[env * kOut + o] = ok ? acc[i] + b4[o] : __uint_as_float(0x7fc00000u);
+        if (o < kOut)
+          out[env * kOut + o] = ok ? (float)((double)(acc[i] + b4[o]) * SC.out_scale[o] + SC.out_mean[o])
+                                   : __uint_as_float(0x7fc00000u);
       }
     }
   }
@@ -943,6 +947,25 @@ int satenv_surrogate_pack(const float* w1, const float* b1, const float* w2, con
                      b4, (uint8_t*)blob);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
+}
+
+int satenv_surrogate_set_scalers(void* blob, const double* in_mean, const double* in_scale, const double* out_mean,
+                                 const double* out_scale, void* stream) {
+  if (!blob || !in_mean || !in_scale || !out_mean || !out_scale)
+    return fail(SATENV_ERR_ARG, "satenv_surrogate_set_scalers: null pointer");
+  surrogate::Scalers sc{};
+  for (int k = 0; k < 8; ++k) {
+    sc.in_mean[k] = k < surrogate::kIn ? in_mean[k] : 0.0;
+    sc.in_scale[k] = k < surrogate::kIn ? in_scale[k] : 1.0;
+  }
+  for (int k = 0; k < surrogate::kOutPad; ++k) {
+    sc.out_scale[k] = k < surrogate::kOut ? out_scale[k] : 1.0;
+    sc.out_mean[k] = k < surrogate::kOut ? out_mean[k] : 0.0;
+  }
+  for (int k = 0; k < surrogate::kIn; ++k)
+    if (!(sc.in_scale[k] != 0.0)) return fail(SATENV_ERR_ARG, "satenv_surrogate_set_scalers: zero input scale");
+  hipLaunchKernelGGL(surrogate::set_scalers_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sc, (uint8_t*)blob);
+  return hipGetLastError() == hipSuccess ? 0 : fail(SATENV_ERR_HIP, "satenv_surrogate_set_scalers: launch");
 }
 
 int satenv_surrogate(satenv_env* h, const void* blob, float* out, void* stream) {

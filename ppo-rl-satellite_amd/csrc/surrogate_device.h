@@ -33,7 +33,16 @@ constexpr int kW4Off = kW3Off + kH3 * kW3Row;
 constexpr int kWElems = kW4Off + kOutPad * kW4Row;
 constexpr int kBiasOffBytes = kWElems * 2;                       // f32 b1 | b2 | b3 | b4(16)
 constexpr int kBiasElems = kH1 + kH2 + kH3 + kOutPad;
-constexpr int kBlobBytes = kBiasOffBytes + kBiasElems * 4;       // 93 248 B
+// the trainer's StandardScalers (single_pulse_fully_connected_model.py:273-278),
+// f64: x_std = (x - in_mean) / in_scale before the bf16 input, y = y_std *
+// out_scale + out_mean after fc4 (sklearn's transform / inverse_transform);
+// identity (0 / 1) unless set (satenv_surrogate_set_scalers)
+struct Scalers {
+  double in_mean[8], in_scale[8], out_scale[kOutPad], out_mean[kOutPad];
+};
+constexpr int kScaleOffBytes = kBiasOffBytes + kBiasElems * 4;
+constexpr int kBlobBytes = kScaleOffBytes + (int)sizeof(Scalers);   // 93 632 B
+static_assert(kScaleOffBytes % 16 == 0 && kBlobBytes % 16 == 0, "blob staged as 16-B words");
 
 __device__ __forceinline__ unsigned short f2bf(float f) {        // round to nearest even (torch .to(bfloat16))
   unsigned u = __float_as_uint(f);
@@ -88,6 +97,15 @@ __global__ void pack_kernel(const float* __restrict__ w1, const float* __restric
     }
     W[t] = f2bf(v);
   }
+  if (blockIdx.x == 0 && threadIdx.x < sizeof(Scalers) / 8) {      // identity scalers
+    double* S = reinterpret_cast<double*>(blob + kScaleOffBytes);
+    const int k = threadIdx.x;                                     // in_mean 0..7, in_scale 8..15, out_scale 16..31
+    S[k] = (k >= 8 && k < 32) ? 1.0 : 0.0;
+  }
+}
+
+__global__ void set_scalers_kernel(const Scalers sc, uint8_t* __restrict__ blob) {
+  *reinterpret_cast<Scalers*>(blob + kScaleOffBytes) = sc;
 }
 
 // bias + ReLU of one accumulator tile into half `h` (elements 4h..4h+3) of a bf16 fragment

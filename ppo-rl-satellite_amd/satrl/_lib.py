@@ -81,6 +81,7 @@ _SIGS = {
     "satenv_surrogate_pack": ([_vp] * 10, C.c_int),
     "satenv_surrogate": ([_vp, _vp, _vp, _vp], C.c_int),
     "satenv_surrogate_mlp": ([_i64, _vp, _vp, _vp, _vp], C.c_int),
+    "satenv_surrogate_set_scalers": ([_vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_ellipse_fit": ([_i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_rd_orbits": ([_vp, _vp, _vp, _vp], C.c_int),
     "satenv_cpu_last_error": ([], C.c_char_p),
@@ -107,6 +108,8 @@ _SIGS = {
     "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_dw2_lib_workspace": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "satrl_ppo_dw2_lib": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_int64, _vp], C.c_int),
+    "satrl_ppo_dw2_lib_pin": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p], C.c_int),
+    "satrl_ppo_dw2_lib_plan_info": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.c_char_p, C.c_int], C.c_int),
     "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,

@@ -177,6 +177,64 @@ def ppo_layout(H):
     return dict(zip(OFF_NAMES, [int(v) for v in off]))
 
 
+DW2_PLANS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dw2_plans.json")
+_dw2_table = None
+
+
+def dw2_plan_table():
+    """{(H, mb, S, nets): (solution index, kernel name)} of the committed
+    table (SATRL_DW2_PLANS overrides the path; "none" disables it)."""
+    global _dw2_table
+    if _dw2_table is None:
+        import json
+        path = os.environ.get("SATRL_DW2_PLANS", DW2_PLANS)
+        _dw2_table = {}
+        if path != "none" and os.path.exists(path):
+            with open(path) as f:
+                for e in json.load(f)["plans"]:
+                    _dw2_table[(e["H"], e["mb"], e["S"], e["nets"])] = (int(e["index"]), e["kernel"])
+    return _dw2_table
+
+
+def dw2_plan_info(H, mb, net, S):
+    """(solution index, kernel name) of a made dW2 plan."""
+    idx, name = C.c_int(), C.create_string_buffer(512)
+    check(_lib.lib().satrl_ppo_dw2_lib_plan_info(H, mb, net, S, C.byref(idx), name, 512), "satrl_ppo_dw2_lib_plan_info")
+    return idx.value, name.value.decode()
+
+
+def dw2_pin_plan(H, mb, net, S, pg=None):
+    """Make the hipBLASLt dW2 plan of (H, mb, S, nets) reproducibly and
+    return (solution index, kernel name, source).  Single process: the
+    committed table's solution when it names one for the shape and the
+    loaded library has that kernel ("table"), else the tuner's
+    ("tuned").  Under data parallelism rank 0 decides that way and every
+    rank pins rank 0's solution ("rank0"), so all ranks sum their dW2
+    partials with the same tiles (a collective call: every rank plans the
+    same shapes in the same order)."""
+    lib = _lib.lib()
+    nets = 2 if net < 0 else 1
+    source = None
+    if _dist.world_size(pg) == 1 or _dist.rank(pg) == 0:
+        hit = dw2_plan_table().get((H, mb, S, nets))
+        if hit is not None and lib.satrl_ppo_dw2_lib_pin(H, mb, net, S, hit[0], hit[1].encode()) == 0:
+            source = "table"
+        else:
+            wsb, idx = C.c_int64(), C.c_int()
+            check(lib.satrl_ppo_dw2_lib_workspace(H, mb, net, S, C.byref(wsb), C.byref(idx)),
+                  "satrl_ppo_dw2_lib_workspace")
+            source = "tuned"
+        idx, name = dw2_plan_info(H, mb, net, S)
+    else:
+        idx, name = -1, ""
+    if _dist.world_size(pg) > 1:
+        idx, name = _dist.broadcast_object((idx, name), pg)
+        if _dist.rank(pg) != 0:
+            check(lib.satrl_ppo_dw2_lib_pin(H, mb, net, S, idx, name.encode()), "satrl_ppo_dw2_lib_pin")
+            source = "rank0"
+    return idx, name, source
+
+
 class FusedMinibatch:
     """One PPO minibatch step for actor + critic on shared rows:
     satrl_ppo_rowpass (gather, MLP forward/backward on f32 MFMA, losses),
@@ -219,11 +277,15 @@ class FusedMinibatch:
         # (dw2_splits caps S at 256 / tiles), so a ragged tail minibatch whose
         # S exceeds the full minibatch's never writes past the slabs
         self.p2 = torch.empty(2 * self.max_splits(H) * H * H, **f32)
-        self.ws = None                     # hipBLASLt workspace of the dW2 plans
+        # hipBLASLt workspaces of the dW2 plans, one per concurrent chain: the
+        # stream-K solutions keep partial tiles in the workspace, so the
+        # actor and critic chains of split mode must never share one
+        self.ws = {}
         self._ws_retired = []
         self._ws_for = {}                  # (mb, S, net) -> the workspace its plan was checked against
         if self.lib_gemm and torch.cuda.is_available():
-            self._ws_for[(self.mb, self.S, -1)] = (self._dw2_plan(self.mb, self.S, -1),)
+            for net in ((0, 1) if self.split else (-1,)):
+                self._ws_for[(self.mb, self.S, net)] = (self._dw2_plan(self.mb, self.S, net),)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
@@ -290,6 +352,9 @@ class FusedMinibatch:
         lo = 0 if net < 0 else net
         hit = self._ws_for.get((mb, S, net))
         if hit is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.NativeError(f"dW2 shape (mb {mb}, S {S}) reached graph capture unplanned: "
+                                       "plan it first (FusedMinibatch.plan_shape)")
             hit = self._ws_for[(mb, S, net)] = (self._dw2_plan(mb, S, net),)
         ws = hit[0]
         o = 4 * lo * mb * H                # byte offset of the first selected net's block
@@ -298,21 +363,38 @@ class FusedMinibatch:
                                            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
                                            stream_ptr()), "satrl_ppo_dw2_lib")
 
+    def plan_shape(self, mb):
+        """Make the dW2 plan of a minibatch of mb rows (e.g. the epoch's
+        ragged tail) before the update loop, so no plan is tuned between
+        minibatch steps and none inside a capture."""
+        mb = int(mb)
+        if not self.lib_gemm or not torch.cuda.is_available():
+            return
+        S = self.S if mb == self.mb else self.splits(self.L.H, mb)
+        for net in ((0, 1) if self.split else (-1,)):
+            if (mb, S, net) not in self._ws_for:
+                self._ws_for[(mb, S, net)] = (self._dw2_plan(mb, S, net),)
+
     def _dw2_plan(self, mb, S, net):
-        """Create (or look up) the hipBLASLt plan of a dW2 shape; grows the
-        shared workspace to its size.  Plans made here, before any capture,
-        keep graph capture free of library set-up."""
+        """Create (or look up) the hipBLASLt plan of a dW2 shape and grow the
+        chain's workspace to its size.  Plans made here, before any capture,
+        keep graph capture free of library set-up.  The solution is
+        reproducible (dw2_pin_plan): the committed table's, else the tuner's,
+        and under data parallelism rank 0's on every rank."""
+        H = self.L.H
+        self.dw2_algo, self.dw2_kernel, self.dw2_source = dw2_pin_plan(H, int(mb), int(net), int(S), self.L.pg)
         wsb, idx = C.c_int64(), C.c_int()
-        check(_lib.lib().satrl_ppo_dw2_lib_workspace(self.L.H, int(mb), int(net), int(S), C.byref(wsb),
-                                                     C.byref(idx)), "satrl_ppo_dw2_lib_workspace")
-        if wsb.value > 0 and (self.ws is None or self.ws.numel() < wsb.value):
+        check(_lib.lib().satrl_ppo_dw2_lib_workspace(H, int(mb), int(net), int(S), C.byref(wsb), C.byref(idx)),
+              "satrl_ppo_dw2_lib_workspace")
+        chain = 1 if (self.split and net == 1) else 0
+        ws = self.ws.get(chain)
+        if wsb.value > 0 and (ws is None or ws.numel() < wsb.value):
             if torch.cuda.is_current_stream_capturing():
                 raise _lib.NativeError("dW2 workspace must grow during graph capture; plan the shape first")
-            if self.ws is not None:
-                self._ws_retired.append(self.ws)     # captured graphs may still point at it
-            self.ws = torch.empty(wsb.value, dtype=torch.uint8, device=self.L.device)
-        self.dw2_algo = idx.value
-        return self.ws
+            if ws is not None:
+                self._ws_retired.append(ws)          # captured graphs may still point at it
+            ws = self.ws[chain] = torch.empty(wsb.value, dtype=torch.uint8, device=self.L.device)
+        return ws
 
     def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False):
         """One minibatch step of one chain.  Bench-only knobs: `events` (a pair
@@ -420,6 +502,8 @@ class FusedMinibatch:
         B = perm.numel()
         mb, G = self.mb, self.group
         nfull = B // mb
+        if B % mb:
+            self.plan_shape(B % mb)          # the ragged tail's dW2 plan, before any step of the epoch
         graphable = self.use_graph and torch.cuda.is_available() and (self.L.pg is None or self.L.comm is not None)
         k = 0
         if graphable and nfull >= G:

@@ -18,12 +18,19 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 
 import torch
 
 NCCL_UNIQUE_ID_BYTES = 128            # rccl.h:40
 _NCCL_FLOAT32, _NCCL_FLOAT64 = 7, 8   # rccl.h:466-467 ncclDataType_t
 _NCCL_SUM = 0                         # rccl.h:448 ncclRedOp_t
+_NCCL_IN_PROGRESS = 7                 # ncclResult_t ncclInProgress
+
+
+class CommError(RuntimeError):
+    """A collective failed or stalled: the communicator has been aborted
+    (ncclCommAbort), so the caller must not issue further collectives on it."""
 
 
 class _UniqueId(C.Structure):
@@ -45,6 +52,8 @@ def _lib():
         lib.ncclCommInitRank.argtypes = [C.POINTER(C.c_void_p), C.c_int, _UniqueId, C.c_int]
         lib.ncclAllReduce.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         lib.ncclCommDestroy.argtypes = [C.c_void_p]
+        lib.ncclCommAbort.argtypes = [C.c_void_p]
+        lib.ncclCommGetAsyncError.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         _LIB = lib
     return _LIB
 
@@ -104,10 +113,52 @@ class Comm:
         torch.cuda.synchronize(self.device)
         self._warm.add(key)
 
+    def async_error(self) -> int:
+        """ncclCommGetAsyncError: 0 (ok), 7 (in progress) or an error code."""
+        if not self._comm:
+            return 0
+        err = C.c_int(0)
+        rc = _lib().ncclCommGetAsyncError(self._comm, C.byref(err))
+        return rc if rc not in (0, _NCCL_IN_PROGRESS) else err.value
+
+    def wait(self, deadline_s: float, stream=None, poll_s: float = 0.005):
+        """Host watchdog between graph replays: block until the work queued so
+        far on `stream` (default: the current one) has finished, polling
+        ncclCommGetAsyncError meanwhile.  An RCCL error, or no completion
+        within deadline_s (a dead or stalled peer leaves this rank's
+        all-reduce kernels waiting forever), aborts the communicator
+        (ncclCommAbort ends its kernels) and raises CommError."""
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        t0 = time.monotonic()
+        while not ev.query():
+            err = self.async_error()
+            if err not in (0, _NCCL_IN_PROGRESS):
+                self.abort()
+                raise CommError(f"RCCL asynchronous error {err}: {_lib().ncclGetErrorString(err).decode()}")
+            if time.monotonic() - t0 > deadline_s:
+                self.abort()
+                raise CommError(f"collective stalled: no completion within {deadline_s:.0f} s (peer lost?)")
+            time.sleep(poll_s)
+
+    def abort(self):
+        if self._comm:
+            _lib().ncclCommAbort(self._comm)
+            self._comm = C.c_void_p()
+
     def destroy(self):
         if self._comm:
             _lib().ncclCommDestroy(self._comm)
             self._comm = C.c_void_p()
+
+
+def abort_all():
+    """ncclCommAbort every communicator of this process (the failure path)."""
+    for c in list(_COMMS.values()):
+        try:
+            c.abort()
+        except Exception:                          # noqa: BLE001 -- best effort on the way out
+            pass
 
 
 _COMMS = {}

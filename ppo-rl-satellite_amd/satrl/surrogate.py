@@ -12,11 +12,19 @@ accumulation whose activations never leave registers (surrogate_device.h).
 Inference semantics: no dropout (the reference constructs the net fresh in
 training mode, so its dropout would make the output random).
 """
+import ctypes as C
+import os
+
 import numpy as np
 import torch
 
 from . import _lib
 from ._lib import check, ptr, stream_ptr
+
+# ImprovedNN trained on the reference's 841 golden pairs by the reference's
+# own recipe (tools/train_improvednn.py, single_pulse_fully_connected_model.py:
+# 263-350): weights + StandardScalers + the held-out split
+TRAINED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "improvednn_trained.npz")
 
 
 class ImprovedNN(torch.nn.Module):
@@ -37,8 +45,20 @@ class ImprovedNN(torch.nn.Module):
         return self.fc4(x)
 
 
+def load_trained(path=TRAINED):
+    """(state_dict, scalers) of a tools/train_improvednn.py bundle; scalers =
+    (in_mean, in_scale, out_mean, out_scale) f64, sklearn's mean_ / scale_."""
+    with np.load(path, allow_pickle=False) as z:
+        sd = {f"fc{k}.{w}": torch.from_numpy(z[f"fc{k}_{w}"]) for k in range(1, 5) for w in ("weight", "bias")}
+        sc = tuple(np.asarray(z[n], dtype=np.float64) for n in ("in_mean", "in_scale", "out_mean", "out_scale"))
+    return sd, sc
+
+
 class Surrogate:
-    """Packed bf16 copy of an ImprovedNN on the device + the env-path kernel."""
+    """Packed bf16 copy of an ImprovedNN on the device + the env-path kernel.
+    state_dict: None (random init from `seed`), a state_dict or .pth path, or
+    "trained" (the committed net trained on the reference's golden pairs,
+    with its StandardScalers in the blob: outputs are ellipse parameters)."""
 
     def __init__(self, device="cuda", seed=0, state_dict=None):
         self.device = torch.device(device)
@@ -46,6 +66,9 @@ class Surrogate:
         with g:
             torch.manual_seed(seed)
             self.net = ImprovedNN()
+        self.scalers = None
+        if isinstance(state_dict, str) and state_dict == "trained":
+            state_dict, self.scalers = load_trained()
         if state_dict is not None:
             self.load_state_dict(state_dict)
         self.net.to(self.device)
@@ -67,6 +90,31 @@ class Surrogate:
         self._packed_from = ps          # keep alive until the pack kernel ran
         check(_lib.lib().satenv_surrogate_pack(*[ptr(t) for t in ps], ptr(self.blob), stream_ptr()),
               "satenv_surrogate_pack")
+        if self.scalers is not None:
+            self.set_scalers(*self.scalers)
+
+    def set_scalers(self, in_mean, in_scale, out_mean, out_scale):
+        """The trainer's StandardScalers (sklearn mean_ / scale_) into the blob:
+        features are standardised before the bf16 input layer and fc4's
+        output is mapped back (satenv_surrogate_set_scalers)."""
+        arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (in_mean, in_scale, out_mean, out_scale)]
+        if [a.size for a in arrs] != [5, 5, 10, 10]:
+            raise ValueError("scalers: in_mean/in_scale of 5, out_mean/out_scale of 10")
+        self.scalers = tuple(arrs)
+        check(_lib.lib().satenv_surrogate_set_scalers(ptr(self.blob), *[a.ctypes.data_as(C.c_void_p) for a in arrs],
+                                                      stream_ptr()), "satenv_surrogate_set_scalers")
+
+    def reference_forward(self, x):
+        """fp32 torch forward of the same network incl. the scalers (f64
+        standardisation as sklearn), the numerics reference of the kernel."""
+        xs = x.double()
+        if self.scalers is not None:
+            im, isc, om, osc = (torch.as_tensor(v, device=x.device) for v in self.scalers)
+            xs = (xs - im) / isc
+        y = self.net(xs.float()).double()
+        if self.scalers is not None:
+            y = y * osc + om
+        return y.float()
 
     def env_forward(self, env, out=None):
         """ellipse_params [N][10] f32 from the env's current pursuer state."""

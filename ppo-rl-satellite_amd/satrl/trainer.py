@@ -71,7 +71,9 @@ class args_param:  # noqa: N801
         self.update_graph_group = update_graph_group
         self.device = device
         # config 5: evaluate the ImprovedNN surrogate (bf16) on every env step into
-        # VecTrainer.ellipse_params (environment.py:158); a path or state_dict loads weights
+        # VecTrainer.ellipse_params (environment.py:158); True = the net trained on the
+        # reference's golden pairs (satrl/data/improvednn_trained.npz, with its scalers);
+        # a path or state_dict loads other weights
         self.surrogate = surrogate
         # data parallelism: "global" -- mini_batch_size is the
         # GLOBAL minibatch, each of W ranks steps mini_batch_size / W of its
@@ -290,7 +292,7 @@ class VecTrainer:
         self.ellipse_params = None
         if getattr(args, "surrogate", False):
             from .surrogate import Surrogate
-            sd = args.surrogate if isinstance(args.surrogate, (str, dict)) else None
+            sd = args.surrogate if isinstance(args.surrogate, (str, dict)) else "trained"
             self.surrogate = Surrogate(device=self.device, seed=self.seed, state_dict=sd)
             self.ellipse_params = torch.zeros((self.N, 10), dtype=torch.float32, device=self.device)
         self.env.reset(self.flag, obs_out=self.buf.obs[0])
@@ -475,6 +477,10 @@ class VecTrainer:
         ev[2].record()
         self.update()
         ev[3].record()
+        if self.learner.comm is not None:
+            # RCCL watchdog over the update's graph replays: a dead or stalled
+            # peer aborts the communicator and raises instead of hanging here
+            self.learner.comm.wait(_dist.dp_timeout_s())
         stats = self.finish_iteration()
         if timers is not None:
             torch.cuda.synchronize()

@@ -67,3 +67,82 @@ def test_workload_labels(bench):
     a = _args(bench, "--surrogate")
     a.dp_minibatch = bench.dp_mode(a, 1)
     assert bench.workload_name(a, 1).startswith("BASELINE.json configs[4]:")
+
+
+def _run_bench(*argv, env=None, timeout=180):
+    import subprocess
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.pop("RANK", None)
+    e.pop("LOCAL_RANK", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=e, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_gpus_n_launches_n_ranks_and_rank0_reports_once():
+    """`bench.py --gpus 2` (no launcher) starts 2 ranks itself; the process
+    group has 2 ranks, the max-over-ranks timing and the report run, and
+    exactly one JSON line comes out (rank 0's), with n_gpus from the group."""
+    import json
+    r = _run_bench("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2 and out["steps"] == 3 and out["dry_run"]
+    assert out["config"]["parallelism"] == "dp2"
+
+
+def test_gpus_1_stays_one_process():
+    import json
+    r = _run_bench("--dry-run", "--steps", "2", "--warmup", "0")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 1 and out["ranks_seen"] == 1
+
+
+def test_world_size_must_match_gpus():
+    r = _run_bench("--gpus", "2", "--dry-run", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+def test_lost_rank_ends_the_run_nonzero():
+    """A rank that dies mid-run (exit 7 before the closing barrier): the other
+    rank's collective fails, satrl.dist.run_or_exit aborts and exits non-zero
+    (3), the launcher stops and reports a failure -- within the deadline, no
+    hang."""
+    import time
+    t0 = time.time()
+    r = _run_bench("--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1",
+                   env={"SATRL_DRY_RUN_FAIL_RANK": "1", "SATRL_DP_TIMEOUT_S": "30"}, timeout=120)
+    assert r.returncode != 0
+    assert time.time() - t0 < 90
+    assert not [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+
+
+def test_surviving_rank_exits_nonzero_on_its_own():
+    """Under an external launcher (torchrun-style env, no bench.py parent to
+    stop it), the surviving rank itself detects the lost peer at its next
+    collective and exits with satrl.dist.EXIT_PEER_FAILURE within the
+    deadline."""
+    import socket
+    import subprocess
+    import time
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = str(s.getsockname()[1])
+    procs = []
+    for r in range(2):
+        e = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                 MASTER_PORT=port, SATRL_DRY_RUN_FAIL_RANK="1", SATRL_DP_TIMEOUT_S="30")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                                       "--steps", "2", "--warmup", "1"], env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    t0 = time.time()
+    out0, err0 = procs[0].communicate(timeout=120)
+    procs[1].communicate(timeout=60)
+    assert procs[1].returncode == 7
+    assert procs[0].returncode == 3, err0[-2000:]
+    assert "data-parallel failure, aborting" in err0
+    assert time.time() - t0 < 90
