@@ -554,8 +554,28 @@ def run(a, world):
     env_us = (timed_run(a.kernel_iters, lambda k: roll_step(k, None), 40.0)
               - timed_run(a.kernel_iters, roll_policy_only, 30.0))
     env_ev_us, env_med = timed_pairs(a.kernel_iters, roll_step, 40.0)
-    env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
-    env_prof_us = prof_avg_us("step_kernel_wide<true;64>")
+    env_live_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_us * 1e-6) / 1e9
+    # rocprof figures from the env-only profile passes (tools/profile_round.sh): the
+    # in-rollout average (a process running nothing but the training rollout) and the
+    # mid-episode averages per env count (kernel trace split by grid size)
+    env_roll_prof, env_sweep_prof = None, None
+    if profiled_shape:
+        f_roll = os.path.join(ROOT, "profiles", f"{a.profile_tag}_env_rollout.json")
+        f_sweep = os.path.join(ROOT, "profiles", f"{a.profile_tag}_env_sweep.json")
+        if os.path.exists(f_roll):
+            env_roll_prof = json.load(open(f_roll))
+        if os.path.exists(f_sweep):
+            env_sweep_prof = json.load(open(f_sweep))["sizes"]
+    env_prof_us = env_roll_prof["avg_launch_us"] if env_roll_prof else None
+    env_fp64 = None
+    f_fp64 = os.path.join(ROOT, "profiles", f"{a.profile_tag}_env_fp64_pmc.json")
+    if os.path.exists(f_fp64):
+        d = json.load(open(f_fp64))
+        env_fp64 = {"fp64_flops_per_launch": d["fp64_flops_per_launch"], "fp64_frac": d["fp64_frac"],
+                    "peak_tflops": d["fp64_vector_peak_tflops"],
+                    "source": f"profiles/{a.profile_tag}_env_fp64_pmc.json (16384 envs mid-episode)"}
+    env_head_us = env_prof_us if env_prof_us else env_us
+    env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_head_us * 1e-6) / 1e9
     env_traffic = pmc("env", num_envs=a.num_envs)
     env = tr.env
     pa = tr.buf.act[0].clone()
@@ -811,15 +831,21 @@ def run(a, world):
                                  "from L2 per phase (DESIGN.md 3.4)"},
             "roofline_env": {"kernel": "satenv step_kernel_wide<autoreset, 64> (hand-written HIP, FP64)", "bound": "hbm",
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
-                             "avg_launch_us": env_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
+                             "avg_launch_us": env_head_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
                              "num_envs": a.num_envs,
-                             "timing": "in_rollout: live, HIP events: kernel_iters eager rollout steps (policy kernel "
-                                       "-> env step) on the trainer's envs and policy after the timed region, minus "
-                                       "the same steps without the env step, per launch",
+                             "timing": ("in-rollout kernel duration: the rocprofv3 average over every env-step launch "
+                                        "of a process running only the training rollout (16384 envs, H 256, hipGraph "
+                                        "chunks; profiles/%s_env_rollout.json)" % a.profile_tag
+                                        if env_prof_us else "live marginal cost (no env-rollout profile)"),
+                             "live_marginal_avg_launch_us": env_us, "live_marginal_GBs": env_live_gbs,
+                             "live_marginal_timing": "HIP events: kernel_iters eager rollout steps (policy kernel -> "
+                                                     "env step) on the trainer's envs after the timed region, minus "
+                                                     "the same steps without the env step, per launch",
                              "event_bracketed_avg_launch_us": env_ev_us, "event_bracketed_median_us": env_med,
                              "rocprof_avg_launch_us": env_prof_us,
-                             "rocprof_source": f"profiles/{a.profile_tag}_bench_kernel_stats.csv (all launches of "
-                                               "this command: rollout + sweep)",
+                             "rocprof_source": f"profiles/{a.profile_tag}_env_rollout.json / _env_rollout_kernel_stats.csv",
+                             "rocprof_mid_episode_by_num_envs": env_sweep_prof,
+                             "fp64_utilisation": env_fp64,
                              "traffic": env_traffic,
                              "traffic_source": f"profiles/{a.profile_tag}_env_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
                                                "bytes/launch, 16384 envs mid-episode, uniform actions)",

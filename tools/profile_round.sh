@@ -1,35 +1,48 @@
 #!/bin/bash
-# Run on the GPU box (gpurun): the FETCH_SIZE and WRITE_SIZE passes (separate
-# runs, no tracing domains beside --pmc) on the rowpass workload, then
-# bench.py under rocprofv3 kernel stats (it reads the traffic figure the PMC
-# passes just wrote into profiles/).  Scratch goes to gpurun_out/prof_<tag>;
-# the summaries land in gpurun_out/prof_<tag>/profiles (copied into the
-# committed profiles/ afterwards).
+# Run on the GPU box (gpurun): every counter pass in a run of its own (no
+# tracing domains beside --pmc), the env kernel's in-rollout and per-size
+# kernel traces, then bench.py under rocprofv3 kernel stats (it reads the
+# PMC summaries just written into profiles/).  Scratch goes to
+# gpurun_out/prof_<tag>; the summaries land in gpurun_out/prof_<tag>/profiles
+# (copied into the committed profiles/ afterwards).
 set -euo pipefail
-TAG=${1:-r1}
+TAG=${1:-r3}
 ROOT=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 "$ROOT/tools/rowpass_workload.py" 40 > /dev/null 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 "$ROOT/tools/rowpass_workload.py" 40 > /dev/null 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_env_fetch" -o run -- \
-    python3 "$ROOT/tools/env_workload.py" 40 > /dev/null 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_env_write" -o run -- \
-    python3 "$ROOT/tools/env_workload.py" 40 > /dev/null 2>&1
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
-    -d "$OUT/pmc_mfma" -o run -- python3 "$ROOT/tools/rowpass_workload.py" 40 > /dev/null 2>&1
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
-    -d "$OUT/pmc_policy_mfma" -o run -- python3 "$ROOT/tools/policy_workload.py" 40 > /dev/null 2>&1
-python3 "$ROOT/tools/summarize_profiles.py" "$OUT" "$TAG" "$ROOT/profiles"
+W="$ROOT/tools"
+timeout -s KILL 60 rocprofv3 -L > "$OUT/avail.txt" 2>&1 || true
+pmc() {   # pmc <dir> <counters...> -- <workload args>
+  local d=$1; shift
+  local ctr=()
+  while [ "$1" != "--" ]; do ctr+=("$1"); shift; done
+  shift
+  timeout -s KILL 180 rocprofv3 --pmc "${ctr[@]}" --output-format csv -d "$OUT/$d" -o run -- python3 "$@" > /dev/null 2>&1
+}
+pmc pmc_fetch FETCH_SIZE -- "$W/rowpass_workload.py" 40
+pmc pmc_write WRITE_SIZE -- "$W/rowpass_workload.py" 40
+pmc pmc_env_fetch FETCH_SIZE -- "$W/env_workload.py" 40
+pmc pmc_env_write WRITE_SIZE -- "$W/env_workload.py" 40
+pmc pmc_mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/rowpass_workload.py" 40
+pmc pmc_policy_mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/policy_workload.py" 40
+# FP64 VALU work of the env step: the F64 instruction counters this rocprofv3 lists (<= 7 SQ + GRBM)
+F64=$(grep -o 'SQ_INSTS_VALU_[A-Z0-9_]*F64' "$OUT/avail.txt" | sort -u | head -7 | tr '\n' ' ')
+if [ -n "$F64" ]; then
+  # shellcheck disable=SC2086
+  pmc pmc_env_fp64 $F64 GRBM_GUI_ACTIVE -- "$W/env_workload.py" 40
+fi
+# env kernel durations: the training rollout alone, and mid-episode per env count
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/env_rollout" -o run -- \
+    python3 "$W/env_workload.py" rollout 1 > /dev/null 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/env_sweep" -o run -- \
+    python3 "$W/env_workload.py" sweep 200 > /dev/null 2>&1
+python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$ROOT/profiles"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o run -- \
-    python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
-rm -f "$OUT/bench/run_kernel_trace.csv"
-python3 "$ROOT/tools/summarize_profiles.py" "$OUT" "$TAG" "$OUT/profiles"
-cp "$ROOT/profiles/${TAG}_rowpass_pmc.json" "$ROOT/profiles/${TAG}_env_pmc.json" "$ROOT/profiles/${TAG}_rowpass_mfma_pmc.json" \
-    "$ROOT/profiles/${TAG}_policy_mfma_pmc.json" \
-    "$OUT/profiles/" 2>/dev/null || true
+    python3 "$ROOT/bench.py" --profile-tag "$TAG" > "$OUT/bench.json" 2> "$OUT/bench.err"
+rm -f "$OUT/bench/run_kernel_trace.csv" "$OUT/env_rollout/run_kernel_trace.csv"
+python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$OUT/profiles"
+cp "$ROOT"/profiles/"${TAG}"_*.json "$OUT/profiles/" 2>/dev/null || true
+cp "$ROOT"/profiles/"${TAG}"_*.csv "$OUT/profiles/" 2>/dev/null || true
 cp "$OUT/profiles/${TAG}_bench_kernel_stats.csv" "$ROOT/profiles/"
 tail -1 "$OUT/bench.json"

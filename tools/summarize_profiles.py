@@ -121,6 +121,84 @@ def main():
         with open(os.path.join(prof, f"{tag}_env_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res))
+    env_extra(d, tag, prof)
+
+
+def env_extra(d, tag, prof):
+    """The env kernel's in-rollout kernel stats, its mid-episode durations per
+    env count (kernel trace split by grid size), and its FP64 VALU work."""
+    hbm_peak, bytes_per_env = 8000.0, 381
+    ks = os.path.join(d, "env_rollout", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        rows = kernel_stats(ks, os.path.join(prof, f"{tag}_env_rollout_kernel_stats.csv"))
+        env = [r for r in rows if "step_kernel_wide" in r["Name"]]
+        pol = [r for r in rows if "policy_kernel" in r["Name"]]
+        if env:
+            us = float(env[0]["AverageNs"]) / 1e3
+            res = {"kernel": env[0]["Name"], "calls": int(env[0]["Calls"]), "avg_launch_us": us, "num_envs": 16384,
+                   "achieved_GBs": 16384 * bytes_per_env / (us * 1e-6) / 1e9,
+                   "hbm_frac": 16384 * bytes_per_env / (us * 1e-6) / 1e9 / hbm_peak,
+                   "env_steps_per_s": 16384 / (us * 1e-6),
+                   "policy_kernel_avg_us": float(pol[0]["AverageNs"]) / 1e3 if pol else None,
+                   "workload": "tools/env_workload.py rollout 1: VecTrainer.collect() x 2 (16384 envs, H 256, "
+                               "2048 steps, hipGraph chunks); every env-step dispatch is an in-rollout launch",
+                   "bytes_per_env_step": bytes_per_env}
+            with open(os.path.join(prof, f"{tag}_env_rollout.json"), "w") as f:
+                json.dump(res, f, indent=1)
+            print(json.dumps(res))
+    tr = os.path.join(d, "env_sweep", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        by = {}
+        for r in csv.DictReader(open(tr)):
+            if "step_kernel_wide" not in r["Kernel_Name"]:
+                continue
+            gk = [k for k in r if k.startswith("Grid_Size")]
+            grid = 1
+            for k in gk:
+                grid *= max(1, int(float(r[k])))
+            by.setdefault(grid, []).append((int(r["Dispatch_Id"]),
+                                            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+        res = {"workload": "tools/env_workload.py sweep 200: per env count 256 warm-up steps (U(-1.6,1.6) actions), "
+                           "then 200 mid-episode launches; kernel trace, the last 200 dispatches per grid size",
+               "bytes_per_env_step": bytes_per_env, "sizes": {}}
+        # grid = threads = 4 waves x 64 lanes per 64 envs -> envs = grid / 4
+        for grid, v in sorted(by.items()):
+            v.sort()
+            us = sorted(t for _, t in v[-200:])
+            n = grid // 4
+            avg = sum(us) / len(us)
+            res["sizes"][str(n)] = {"dispatches": len(us), "avg_launch_us": avg, "median_launch_us": us[len(us) // 2],
+                                    "env_steps_per_s": n / (avg * 1e-6),
+                                    "hbm_frac": n * bytes_per_env / (avg * 1e-6) / 1e9 / hbm_peak}
+        with open(os.path.join(prof, f"{tag}_env_sweep.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
+    fp = os.path.join(d, "pmc_env_fp64", "run_counter_collection.csv")
+    if os.path.exists(fp):
+        names = sorted({r["Counter_Name"] for r in csv.DictReader(open(fp))})
+        vals = {c: pmc_per_dispatch(fp, "step_kernel", c, last=40)[0] for c in names}
+        flops = 0.0
+        for c, v in vals.items():
+            if v is None or not c.endswith("F64"):
+                continue
+            w = 2 if "FMA" in c else (0 if "MFMA" in c else 1)
+            flops += 64.0 * w * v
+        sweep = os.path.join(prof, f"{tag}_env_sweep.json")
+        us = None
+        if os.path.exists(sweep):
+            us = json.load(open(sweep))["sizes"].get("16384", {}).get("avg_launch_us")
+        res = {"kernel": "satenv step_kernel_wide<true, 64>, 16384 envs mid-episode", "counters_per_launch": vals,
+               "fp64_flops_per_launch": flops,
+               "avg_launch_us": us, "fp64_tflops_achieved": flops / (us * 1e-6) / 1e12 if us else None,
+               "fp64_vector_peak_tflops": 78.6,
+               "fp64_frac": flops / (us * 1e-6) / 1e12 / 78.6 if us else None,
+               "definition": "FLOPs = 64 lanes x (ADD + MUL + TRANS + 2 x FMA) F64 wave instructions, the last 40 "
+                             "dispatches (median); duration = the sweep trace's 16384-env average (the same "
+                             "workload, unprofiled); peak = AMD's FP64 vector figure (not in the local guide)",
+               "workload": "tools/env_workload.py 40"}
+        with open(os.path.join(prof, f"{tag}_env_fp64_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
 
 
 if __name__ == "__main__":
