@@ -729,6 +729,320 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
 }
 
 // ---------------------------------------------------------------------------
+// rowpass_dual: the same row-parallel step with ONE workgroup per 16-row block
+// and BOTH nets (H = 256): waves 0-7 the actor, 8-15 the critic, each wave
+// one 16-row tile x two 16-column tiles of its net.  The two nets share only
+// the gathered rows, so after one workgroup barrier each net runs its phases
+// on its own 8-wave barrier (an LDS counter), and the matrix pipe of every
+// SIMD (two actor + two critic waves) is shared by whichever net is in an
+// MFMA phase: the non-MFMA phases of one net (fc1 tanh, the output layer, the
+// loss head, the tail partials, dZ1/[dW1|db1]) run beside the other net's
+// fc2 / dH1 MFMA streams instead of leaving the pipe idle, as they do when a
+// workgroup owns one net.  Every row's arithmetic is that of rowpass_kernel
+// <256, 16, 16> (the forward's MFMA order, the output-layer sums as sixteen
+// 16-column partials in column order, the head, the tail and [dW1|db1] sums
+// over the block's rows): the outputs are bitwise those of the 16-row
+// kernel, so logp still equals the rollout's bit for bit.
+// ---------------------------------------------------------------------------
+#ifndef SATRL_RP_DUAL_PRIO
+#define SATRL_RP_DUAL_PRIO 0   // s_setprio for waves in their MFMA phases (dev A/B)
+#endif
+#ifndef SATRL_RP_DUAL_TOKEN
+#define SATRL_RP_DUAL_TOKEN 0  // MFMA phases strictly alternate B_a, B_c, D_a, D_c (dev A/B)
+#endif
+
+// wait (bounded) until the counter reaches target, without arriving
+__device__ __forceinline__ void net_wait(const unsigned* cnt, unsigned target) {
+  for (int it = 0; it < (1 << 22); ++it) {
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// one net's 8 waves meet: each wave's lane 0 adds 1 to the net's LDS counter
+// after its LDS writes, then the wave waits for `target` arrivals (a bounded
+// spin: a lost arrival ends the wait instead of hanging the workgroup)
+__device__ __forceinline__ void net_sync(unsigned* cnt, unsigned target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int it = 0; it < (1 << 22); ++it) {
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int H>
+__global__ void __launch_bounds__(1024, 1) rowpass_dual_kernel(int mb, const float* __restrict__ src,
+                                                               const int64_t* __restrict__ idx,
+                                                               const float* __restrict__ P,
+                                                               const float* __restrict__ W2T, float epsilon,
+                                                               float ent_coef, float max_action,
+                                                               float* __restrict__ H1g, float* __restrict__ dZ2g,
+                                                               float* __restrict__ ptail, float* __restrict__ pw1) {
+  constexpr int R = 16, NWN = 8, CT = H / 16 / NWN, LDA = H + 4, LDS_S = 36, NT = 1024;
+  static_assert(CT == 2, "two 16-column tiles per wave");
+  const Layout L = layout(H);
+  __shared__ __attribute__((aligned(16))) float S[R][LDS_S];     // [s(18) | 1 | 0...] per row
+  __shared__ float ax[R][8];                                     // a, logp_old, adv, v_target
+  __shared__ __attribute__((aligned(16))) float hs[2][R][LDA];   // per net: tanh(fc1), then dZ2
+  __shared__ float osum[2][2 * NWN][R][3];                       // per net: 16-column output-layer partials
+  __shared__ float dz3s[2][R][4];
+  __shared__ float hcs[3][3];
+  __shared__ unsigned nbar[2];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
+  const int net = w >> 3, wn = w & 7, n0 = wn * (H / NWN);
+  const int rb = blockIdx.x, r0 = rb * R, nvalid = mb - r0;
+  unsigned* bar = &nbar[net];
+  unsigned gen = 0;
+
+  // ---- gather (shared by both nets), this wave's W1aug rows ---------------------
+  float4 bw1[CT][2];
+  {
+    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
+      bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lg < 2) {
+        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
+        bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
+      } else if (lg == 2) {
+        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
+      }
+    }
+  }
+  float hb3[3], hls[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) { hb3[d] = P[L.b3a + d]; hls[d] = P[L.ls + d]; }
+  const float hb3c = P[L.b3c];
+  for (int q = tid; q < R * 26; q += NT) {
+    const int r = q / 26, c = q % 26, row = r0 + r;
+    const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
+    if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;
+  }
+  for (int q = tid; q < R * (LDS_S - 18); q += NT) {
+    const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
+    S[r][c] = (c == 18 && r < nvalid) ? 1.0f : 0.0f;
+  }
+  if (tid < 3) {
+    const float ls = tid == 0 ? hls[0] : (tid == 1 ? hls[1] : hls[2]);
+    const float sd = expf(ls), var = sd * sd;
+    hcs[0][tid] = var;
+    hcs[1][tid] = logf(sd);
+    hcs[2][tid] = 1.0f / var;
+  }
+  if (tid < 2) nbar[tid] = 0u;
+  float b2v[CT], w3[CT][3];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int n = n0 + 16 * t + li;
+    b2v[t] = P[L.b2 + net * H + n];
+    if (net == 0) {
+      w3[t][0] = P[L.W3a + n]; w3[t][1] = P[L.W3a + H + n]; w3[t][2] = P[L.W3a + 2 * H + n];
+    } else {
+      w3[t][0] = P[L.W3c + n]; w3[t][1] = 0.0f; w3[t][2] = 0.0f;
+    }
+  }
+  __syncthreads();                                               // the only workgroup-wide barrier
+
+  // ---- A: fc1 on MFMA, tanh -> registers, LDS, H1 (HBM) --------------------------
+  f4 acc[1][CT];
+  float h1[1][CT][4];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
+  mfma_chunk<LDS_S, 1, CT>(&S[li][8 * lg], bw1, acc);
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int n = n0 + 16 * t + li;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float h = tanh_f32(acc[0][t][j]);
+      h1[0][t][j] = h;
+      hs[net][4 * lg + j][n] = h;
+    }
+    acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, nvalid, h1);
+  net_sync(bar, gen += NWN);
+
+  // ---- B: Z2 = H1 W2^T ------------------------------------------------------------
+  if (SATRL_RP_DUAL_TOKEN && net == 1) net_wait(&nbar[0], 2 * NWN);   // after the actor's B
+  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(1);
+  mfma_rows<H, LDA, H, 1, CT, true>(&hs[net][0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(0);
+
+  // ---- C (forward): tanh(fc2), output-layer partials per 16-column tile ------------
+  {
+    float ps[3 * CT * 4];
+#pragma unroll
+    for (int k = 0; k < 3 * CT * 4; ++k) ps[k] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float h = tanh_f32(acc[0][t][j] + b2v[t]);
+        acc[0][t][j] = h;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ps[(q * CT + t) * 4 + j] = fmaf(h, w3[t][q], 0.0f);
+      }
+    if (net == 0) {
+      row16_sum_n<3 * CT * 4>(ps);
+    } else {
+      float p0[CT * 4];
+#pragma unroll
+      for (int k = 0; k < CT * 4; ++k) p0[k] = ps[k];
+      row16_sum_n<CT * 4>(p0);
+#pragma unroll
+      for (int k = 0; k < CT * 4; ++k) ps[k] = p0[k];
+    }
+    if (li == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (q >= (net == 0 ? 3 : 1)) break;
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) osum[net][CT * wn + t][4 * lg + j][q] = ps[(q * CT + t) * 4 + j];
+      }
+    }
+  }
+  net_sync(bar, gen += NWN);
+
+  // ---- C: the net's loss head (16 lanes of the net's first wave) -----------------
+  if (wn == 0 && l < R) {
+    const int r = l, row = r0 + r;
+    float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
+    if (row < mb) {
+      const float inv = 1.0f / (float)mb;
+      if (net == 0) {
+        float th[3], mu[3], dv[3], var[3], logp[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          th[d] = tanh_f32(out_sum<2 * NWN, R>(osum[0], r, d) + hb3[d]);
+          mu[d] = max_action * th[d];
+          var[d] = hcs[0][d];
+          dv[d] = ax[r][d] - mu[d];
+          logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - hcs[1][d]) - kLogSqrt2Pi;
+        }
+        const float lsum = (logp[0] + logp[1]) + logp[2];
+        const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
+        const float ratio = expf(lsum - lold);
+        const float adv = ax[r][6];
+        const float s1 = ratio * adv;
+        const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
+        const float s2 = cr * adv;
+        const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+        const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+        const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
+        const float dmin = -inv;
+        const float dratio = dmin * g1 * adv + dmin * g2 * adv * inside;
+        const float dlsum = dratio * ratio;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const float dvv = dv[d] * hcs[2][d];
+          const float dmu = dlsum * dvv;
+          dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
+          dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
+        }
+      } else {
+        const float vc = out_sum<2 * NWN, R>(osum[1], r, 0) + hb3c;
+        dz[3] = 2.0f * inv * (vc - ax[r][7]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dz3s[net][r][q] = dz[q];
+    float* tp = ptail + (int64_t)rb * L.tail;
+    float red[7] = {dz[0], dz[1], dz[2], dls[0], dls[1], dls[2], dz[3]};
+    row16_sum_n<7>(red);
+    if (r == 0) {
+      if (net == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          tp[5 * H + q] = red[q];
+          tp[5 * H + 4 + q] = red[3 + q];
+        }
+        tp[5 * H + 3] = 0.0f;
+        tp[5 * H + 7] = 0.0f;
+      } else {
+        tp[6 * H + 8] = red[6];
+        tp[6 * H + 9] = 0.0f; tp[6 * H + 10] = 0.0f; tp[6 * H + 11] = 0.0f;
+      }
+    }
+  }
+  net_sync(bar, gen += NWN);
+
+  // ---- C: dZ2 (LDS over this net's tanh(fc1) image, HBM), db2 / dW3 partials --------
+  {
+    float* tp = ptail + (int64_t)rb * L.tail;
+    float d2v[1][CT][4];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int n = n0 + 16 * t + li;
+      float cb2 = 0.f, cw[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * lg + j;
+        const float h = acc[0][t][j];
+        float dh;
+        if (net == 0) dh = (dz3s[0][r][0] * w3[t][0] + dz3s[0][r][1] * w3[t][1]) + dz3s[0][r][2] * w3[t][2];
+        else dh = dz3s[1][r][3] * w3[t][0];
+        const float d2 = dh * (1.0f - h * h);
+        hs[net][r][n] = d2;
+        d2v[0][t][j] = d2;
+        cb2 += d2;
+        if (net == 0) {
+          cw[0] = fmaf(dz3s[0][r][0], h, cw[0]); cw[1] = fmaf(dz3s[0][r][1], h, cw[1]);
+          cw[2] = fmaf(dz3s[0][r][2], h, cw[2]);
+        } else {
+          cw[0] = fmaf(dz3s[1][r][3], h, cw[0]);
+        }
+      }
+      cb2 = xor32_sum(xor16_sum(cb2));
+      cw[0] = xor32_sum(xor16_sum(cw[0]));
+      if (net == 0) { cw[1] = xor32_sum(xor16_sum(cw[1])); cw[2] = xor32_sum(xor16_sum(cw[2])); }
+      if (lg == 0) {
+        tp[net * H + n] = cb2;
+        if (net == 0) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }
+        else tp[5 * H + 8 + n] = cw[0];
+      }
+    }
+    store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, nvalid, d2v);
+  }
+  net_sync(bar, gen += NWN);
+
+  // ---- D: dH1 = dZ2 W2 ---------------------------------------------------------------
+#pragma unroll
+  for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
+  if (SATRL_RP_DUAL_TOKEN) net_wait(&nbar[1 - net], net == 0 ? 2 * NWN : 5 * NWN);   // after the other's B / D
+  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(1);
+  mfma_rows<H, LDA, H, 1, CT, true>(&hs[net][0][0], W2T + (int64_t)net * H * H, n0, acc);
+  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(0);
+  if (SATRL_RP_DUAL_TOKEN && net == 0 && (threadIdx.x & 63) == 0)                   // the actor's D is done
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+  // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1] = dZ1^T [S | 1] ----------------------------
+  float* pw = pw1 + (int64_t)rb * 2 * H * 20 + (int64_t)net * H * 20;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[0][t][j] = acc[0][t][j] * (1.0f - h1[0][t][j] * h1[0][t][j]);
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      f4 d = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[0][t][kk], S[4 * lg + kk][16 * hb + li], d);
+      const int kp = 16 * hb + li;
+      if (kp < 20) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pw[(int64_t)(n0 + 16 * t + 4 * lg + j) * 20 + kp] = d[j];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // policy: the rollout's forward passes on the rowpass's own MLP code
 // (mlp_forward), one workgroup per 32-row block and net.
 //   MODE 0  actor -> mean = max_action*tanh(.) -> Normal sample -> clamp ->
@@ -1224,7 +1538,18 @@ int short_mb() {
   }();
   return v;
 }
-int rows_per_wg(int H, int mb) { return (H == 256 && kRows == 32 && mb <= short_mb()) ? kRowsShort : kRows; }
+// the dual-net rowpass at H = 256 (SATRL_RP_DUAL=1): 16-row blocks at every mb
+bool dual_rowpass() {
+  static const bool v = [] {
+    const char* e = std::getenv("SATRL_RP_DUAL");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+int rows_per_wg(int H, int mb) {
+  if (H == 256 && dual_rowpass()) return kRowsShort;
+  return (H == 256 && kRows == 32 && mb <= short_mb()) ? kRowsShort : kRows;
+}
 int n_head_wg(int H, int mb) {
   const int R = rows_per_wg(H, mb);
   return (mb + R - 1) / R;
@@ -1233,6 +1558,7 @@ int n_w1_wg(int H, int mb) { return n_head_wg(H, mb); }
 // slab capacity a minibatch of mb rows needs, and any shorter one (a ragged
 // tail of a minibatch above the short threshold can have more row blocks)
 int n_head_wg_cap(int H, int mb) {
+  if (H == 256 && dual_rowpass()) return n_head_wg(H, mb);
   const int m = mb < short_mb() ? mb : short_mb();
   const int a = n_head_wg(H, mb), b = m > 0 ? n_head_wg(H, m) : 0;
   return a > b ? a : b;
@@ -1305,6 +1631,9 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
+  else if (net < 0 && dual_rowpass())
+    hipLaunchKernelGGL((rowpass_dual_kernel<256>), dim3(n_head_wg(H, mb)), dim3(1024), 0, s, mb, src, idx, P, W2T,
+                       epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1);
   else if (R == kRowsShort && kRows != kRowsShort)
     hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, mb, src, idx, P, W2T, epsilon,
                        ent_coef, max_action, H1, dZ2, ptail, pw1, net);
