@@ -282,22 +282,34 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   const float* ap = A + i * LDA + 8 * g;
   const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
   if constexpr (APRE) {
+#ifdef SATRL_RP_FAKE_LDS_B
+    // timing probe only (numerically wrong): the B operand read from LDS (the A
+    // image), i.e. the MFMA phases with a perfect on-chip weight feed
+    bp = A + i * LDA + 8 * g;
+    constexpr int LDB_ = LDA;
+#else
+    constexpr int LDB_ = LDB;
+#endif
     // fully unrolled so every buffer index is static
     constexpr int NB = kBPD + 1;
     float4 bb[NB][CT][2], aa[2][RT][2];
+#ifdef SATRL_RP_FAKE_LDS_B
+    if constexpr (false) {
+#else
     if constexpr (PRE) {
+#endif
 #pragma unroll
       for (int c = 0; c < kBPD; ++c)
 #pragma unroll
         for (int t = 0; t < CT; ++t) { bb[c][t][0] = pre->bb[c][t][0]; bb[c][t][1] = pre->bb[c][t][1]; }
     } else {
 #pragma unroll
-      for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
+      for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB_, bb[c]);
     }
     a_chunk<LDA, RT>(ap, aa[0]);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (c + kBPD < NC) b_chunk<CT>(bp + 32 * (c + kBPD), LDB, bb[(c + kBPD) % NB]);
+      if (c + kBPD < NC) b_chunk<CT>(bp + 32 * (c + kBPD), LDB_, bb[(c + kBPD) % NB]);
       if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
       mfma_regs<RT, CT>(aa[c % 2], bb[c % NB], acc);
     }
