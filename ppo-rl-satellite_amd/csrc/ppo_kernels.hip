@@ -311,6 +311,12 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
     for (int c = 0; c < NC; ++c) {
       if (c + kBPD < NC) b_chunk<CT>(bp + 32 * (c + kBPD), LDB_, bb[(c + kBPD) % NB]);
       if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
+#ifdef SATRL_RP_CHUNK_SYNC
+      // timing variant: the workgroup's waves meet every SATRL_RP_CHUNK_SYNC
+      // chunks, so the waves of a SIMD interleave their MFMA streams instead of
+      // running them oldest first (each wave's prefetch then covers 4x longer)
+      if (c > 0 && c % SATRL_RP_CHUNK_SYNC == 0) __builtin_amdgcn_s_barrier();
+#endif
       mfma_regs<RT, CT>(aa[c % 2], bb[c % NB], acc);
     }
   } else {
@@ -399,12 +405,17 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
       const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
       bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
       bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+#ifdef SATRL_RP_FAKE_GATHER
+      (void)bp;                                  // timing probe only: no W1 loads
+      bw1[t][0] = make_float4(0.01f, 0.02f, 0.f, 0.f);
+#else
       if (lg < 2) {
         bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
         bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
       } else if (lg == 2) {
         bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
       }
+#endif
     }
   }
   gather(tid, NT);
@@ -566,7 +577,11 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   auto gather = [&](int t0, int nt) {
     for (int q = t0; q < R * 26; q += nt) {
       const int r = q / 26, c = q % 26, row = r0 + r;
+#ifdef SATRL_RP_FAKE_GATHER
+      const float v = row < mb ? 0.001f * (float)(c + r) : 0.0f;   // timing probe only: no row loads
+#else
       const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
+#endif
       if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
     }
     if (t0 < 3) {
