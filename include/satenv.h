@@ -137,6 +137,11 @@ int satenv_solve_alpha(int64_t n, const double* in, double* alpha_out, void* str
  * (tests/test_env_gpu.py), so the hybrd restatement's arithmetic is the
  * library's.                                                              */
 int satenv_sincos(int64_t n, const double* x, double* s_out, double* c_out, int32_t use_library, void* stream);
+/* Self-test of the env step's f64 acos (no reference counterpart): the
+ * straight-line transcription of OCML's acos the orbital elements and the
+ * rf theta use (use_library = 0), or the library acos() (1): out f64 [n].
+ * The two must agree bitwise (tests/test_env_gpu.py).                     */
+int satenv_acos(int64_t n, const double* x, double* out, int32_t use_library, void* stream);
 
 /* synchronises the handle's device; *status = first sticky device error (0 = none) */
 int satenv_check(satenv_env* h, int32_t* status);

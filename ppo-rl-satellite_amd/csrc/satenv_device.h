@@ -86,6 +86,60 @@ SATENV_HD double norm3(double a0, double a1, double a2) {
   return sqrt(dot3(a0, a1, a2, a0, a1, a2));
 }
 
+// OCML's __ocml_acos_f64 (ROCm 7.2 ocml.bc) as straight-line code: the
+// library branches to its |x| >= 1/2 arm (a sqrt of (1 - |x|)/2 refined in
+// double-double and a reciprocal), which keeps a wave's four element acos()
+// calls apart; here both arms are computed and selected, operation for
+// operation as the bitcode has them, so results are bit-identical to acos()
+// (tests/test_env_gpu.py through satenv_acos) while the compiler may
+// interleave independent calls.  Device only: the host build is glibc's acos.
+SATENV_HD double acos_sl(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(SATENV_ACOS_LIBRARY)   // (dev A/B: the library call)
+  const double ax = fabs(x);
+  const bool big = ax >= 0.5;
+  const double y = fma(ax, -0.5, 0.5);
+  const double u = big ? y : x * x;
+  double p = fma(u, 0x1.059859fea6a70p-5, -0x1.0a5a378a05eafp-6);
+  p = fma(u, p, 0x1.4052137024d6ap-6);
+  p = fma(u, p, 0x1.ab3a098a70509p-8);
+  p = fma(u, p, 0x1.8ed60a300c8d2p-7);
+  p = fma(u, p, 0x1.c6fa84b77012bp-7);
+  p = fma(u, p, 0x1.1c6c111dccb70p-6);
+  p = fma(u, p, 0x1.6e89f0a0adacfp-6);
+  p = fma(u, p, 0x1.f1c72c668963fp-6);
+  p = fma(u, p, 0x1.6db6db41ce4bdp-5);
+  p = fma(u, p, 0x1.333333336fd5bp-4);
+  p = fma(u, p, 0x1.5555555555380p-3);
+  const double r = u * p;
+  const double small = fma(0x1.dd9ad336a0500p-1, 0x1.af154eeb562d6p+0, -fma(x, r, x));
+  // |x| >= 1/2: s = sqrt(y) by rsq + two refinements, then the double-double remainder
+  const double rs = __builtin_amdgcn_rsq(y);
+  const double s0 = y * rs, h0 = rs * 0.5;
+  const double e0 = fma(-h0, s0, 0.5);
+  const double h1 = fma(h0, e0, h0), s1 = fma(s0, e0, s0);
+  const double d1 = fma(-s1, s1, y);
+  const double s = (y == 0.0) ? y : fma(d1, h1, s1);
+  const double ss = s * s, sserr = fma(s, s, -ss);
+  const double t1 = y - ss;
+  const double rem = t1 + (((y - t1) - ss) - sserr);
+  const double s2 = s * 2.0;
+  const double q = __builtin_amdgcn_rcp(s2);
+  const double q1 = fma(fma(-s2, q, 1.0), q, q);
+  const double q2 = fma(fma(-s2, q1, 1.0), q1, q1);
+  const double c0 = rem * q2;
+  const double corr = (y == 0.0) ? 0.0 : fma(fma(-s2, c0, rem), q2, c0);
+  const double hi = s + corr, lo = corr - (hi - s);
+  const double neg = fma(0x1.dd9ad336a0500p+0, 0x1.af154eeb562d6p+0, fma(hi, r, hi) * -2.0);
+  const double pos = (hi + fma(hi, r, lo)) * 2.0;
+  double bigv = x < 0.0 ? neg : pos;
+  bigv = x == -1.0 ? 0x1.921fb54442d18p+1 : bigv;
+  bigv = x == 1.0 ? 0.0 : bigv;
+  return big ? bigv : small;
+#else
+  return acos(x);
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // satellite_function.py:161-255 calculate_orbital_elements (6-element branch)
 // returns 0, or -4 (e == 0: circular branch) / -5 (parabolic branch): the
@@ -112,12 +166,12 @@ SATENV_HD int orbital_elements(double mu, double R0, double R1, double R2, doubl
   const double h = norm3(H0, H1, H2);
   const double N0 = 0.0 * H2 - 1.0 * H1, N1 = 1.0 * H0 - 0.0 * H2, N2 = 0.0 * H1 - 0.0 * H0;
   const double n = norm3(N0, N1, N2);
-  out.i = acos(dot3(0.0, 0.0, 1.0, H0, H1, H2) / h);       // :210
-  double omega = (n != 0.0) ? acos(dot3(N0, N1, N2, E0, E1, E2) / n / e) : 0.0;   // :214-217
+  out.i = acos_sl(dot3(0.0, 0.0, 1.0, H0, H1, H2) / h);       // :210
+  double omega = (n != 0.0) ? acos_sl(dot3(N0, N1, N2, E0, E1, E2) / n / e) : 0.0;   // :214-217
   if (dot3(0.0, 0.0, 1.0, E0, E1, E2) < 0.0) omega = kTwoPi - omega;               // :221
-  double Omega = (n != 0.0) ? acos(dot3(1.0, 0.0, 0.0, N0, N1, N2) / n) : 0.0;      // :230-233
+  double Omega = (n != 0.0) ? acos_sl(dot3(1.0, 0.0, 0.0, N0, N1, N2) / n) : 0.0;      // :230-233
   if (dot3(0.0, 1.0, 0.0, N0, N1, N2) < 0.0) Omega = kTwoPi - Omega;                // :237
-  double f = acos(dot3(E0, E1, E2, R0, R1, R2) / e / r_norm);                       // :242
+  double f = acos_sl(dot3(E0, E1, E2, R0, R1, R2) / e / r_norm);                       // :242
   if (r_dot_v < 0.0) f = kTwoPi - f;                                                // :243
   out.omega = omega;
   out.Omega = Omega;
@@ -356,8 +410,8 @@ SATENV_HD void rf_setup(const Pursuer& P, double f_c, RfSolve& q) {
   else { const double beta = atan(q0); sb = sin(beta); cb = cos(beta); }
   q.dvm = sqrt(P.dv2 - P.u * pow2(P.X) * pow2(sb) / P.p);                        // :470
   double theta = 0.0;
-  if ((-kTwoPi <= d && d < -kPi) || (0.0 <= d && d < kPi)) theta = acos(cos(d) * 1.0);          // :473
-  else if ((-kPi <= d && d < 0.0) || (kPi <= d && d < kTwoPi)) theta = kTwoPi - acos(cos(d) * 1.0);
+  if ((-kTwoPi <= d && d < -kPi) || (0.0 <= d && d < kPi)) theta = acos_sl(cos(d) * 1.0);          // :473
+  else if ((-kPi <= d && d < 0.0) || (kPi <= d && d < kTwoPi)) theta = kTwoPi - acos_sl(cos(d) * 1.0);
   sincos(theta, &q.st, &q.ct);
   q.vx0 = P.sq * P.e * P.sf0;                                                    // :518
   q.vy0 = P.sq * P.X * cb;                                                       // :519

@@ -413,6 +413,13 @@ __global__ void __launch_bounds__(256) sincos_kernel(int64_t n, const double* __
   co[i] = c;
 }
 
+__global__ void __launch_bounds__(256) acos_kernel(int64_t n, const double* __restrict__ x, double* __restrict__ out,
+                                                   int32_t use_library) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = use_library ? acos(x[i]) : acos_sl(x[i]);
+}
+
 // batched RK4 two-body + J2 propagation (轨道外推-龙格库塔算法.py), SoA [6][n]
 __global__ void __launch_bounds__(256) rk4_j2_kernel(int64_t n, const double* __restrict__ in, double h,
                                                      int32_t steps, double* __restrict__ out) {
@@ -890,6 +897,13 @@ int satenv_sincos(int64_t n, const double* x, double* s_out, double* c_out, int3
   if (n <= 0 || !x || !s_out || !c_out) return fail(SATENV_ERR_ARG, "satenv_sincos: bad args");
   hipLaunchKernelGGL(sincos_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, x, s_out, c_out,
                      use_library);
+  HIP_TRY(hipGetLastError());
+  return SATENV_OK;
+}
+
+int satenv_acos(int64_t n, const double* x, double* out, int32_t use_library, void* stream) {
+  if (n <= 0 || !x || !out) return fail(SATENV_ERR_ARG, "satenv_acos: bad args");
+  hipLaunchKernelGGL(acos_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, x, out, use_library);
   HIP_TRY(hipGetLastError());
   return SATENV_OK;
 }

@@ -75,6 +75,7 @@ _SIGS = {
     "satenv_danger_zone": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_solve_alpha": ([_i64, _vp, _vp, _vp], C.c_int),
     "satenv_sincos": ([_i64, _vp, _vp, _vp, _i32, _vp], C.c_int),
+    "satenv_acos": ([_i64, _vp, _vp, _i32, _vp], C.c_int),
     "satenv_rk4_j2": ([_i64, _vp, C.c_double, _i32, _vp, _vp], C.c_int),
     "satenv_reachable_domain": ([_i64, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_surrogate_blob_bytes": ([], C.c_int),

@@ -88,6 +88,30 @@ def test_straight_line_sincos_is_the_library_sincos(satrl_env):
     assert s.tolist() == [1.0, -1.0] and c.tolist() == [float.fromhex("0x1.1a62633145c07p-54")] * 2
 
 
+def test_straight_line_acos_is_the_library_acos(satrl_env):
+    """The orbital elements' and rf theta's acos (satenv_device.h acos_sl, a
+    branch-free transcription of OCML's acos) == the device library's
+    acos(), bitwise: uniform in [-1, 1], dense near +-1/2 (the arm switch)
+    and +-1, tiny magnitudes, out-of-domain values, signed zeros, +-1 exactly,
+    inf and NaN."""
+    from satrl import _lib
+    g = np.random.default_rng(5)
+    parts = [g.uniform(-1.0, 1.0, 1000000), 0.5 + g.normal(0, 1e-9, 100000), -0.5 + g.normal(0, 1e-9, 100000),
+             1.0 - np.abs(g.normal(0, 1e-7, 100000)), -1.0 + np.abs(g.normal(0, 1e-7, 100000)),
+             np.sign(g.normal(size=100000)) * 10.0 ** g.uniform(-300, 0, 100000),
+             np.array([0.0, -0.0, 0.5, -0.5, np.nextafter(0.5, 0), np.nextafter(-0.5, 0), 1.0, -1.0,
+                       np.nextafter(1.0, 0), np.nextafter(-1.0, 0), 1.0 + 2 ** -52, -1.0 - 2 ** -52, 2.0, -3.0,
+                       5e-324, -5e-324, np.inf, -np.inf, np.nan])]
+    x = torch.tensor(np.concatenate(parts), dtype=torch.float64, device="cuda")
+    n = x.numel()
+    res = []
+    for lib_flag in (0, 1):
+        out = torch.empty(n, dtype=torch.float64, device="cuda")
+        _lib.check(_lib.lib().satenv_acos(n, _lib.ptr(x), _lib.ptr(out), lib_flag, _lib.stream_ptr()), "satenv_acos")
+        res.append(out.cpu().numpy().view(np.int64))
+    assert np.array_equal(res[0], res[1]), int((res[0] != res[1]).sum())
+
+
 def test_danger_zone_counts(satrl_env, oracle):
     from satrl import _lib
     d = golden("dz_cases")
