@@ -76,6 +76,11 @@ int satrl_ppo_dw2_lib(int H, int mb, int net, int S, const float* H1, const floa
  * run sums dW2 with the same tiles.                                        */
 int satrl_ppo_dw2_lib_pin(int H, int mb, int net, int S, int algo_index, const char* kernel);
 int satrl_ppo_dw2_lib_plan_info(int H, int mb, int net, int S, int* algo_index, char* kernel, int kernel_len);
+/* Plan tooling (tools/dw2_pin.py): up to `cap` solutions of the shape that
+ * repeat their output bit for bit, fastest first by back-to-back time on
+ * scratch slabs (us, nullable); returns how many (< 0 on error).  Outside
+ * capture: it allocates and synchronises.                                  */
+int satrl_ppo_dw2_lib_candidates(int H, int mb, int net, int S, int* algo_index, float* us, int cap);
 
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block

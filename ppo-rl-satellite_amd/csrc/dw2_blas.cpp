@@ -200,6 +200,55 @@ bool tune(int H, int mb, int S, int nb, Plan& p) {
   return false;
 }
 
+// every supported solution of the shape timed back to back on scratch slabs,
+// fastest first; the first `det_check` of them also checked to repeat their
+// output bit for bit (non-repeating ones are dropped)
+struct Timed { float us; int index; };
+bool make_descriptors(int H, int mb, int S, int nb, Plan& p);
+std::vector<Timed> candidates(int H, int mb, int S, int nb, int det_check) {
+  std::vector<Timed> out;
+  Plan p;
+  if (!make_descriptors(H, mb, S, nb, p)) return out;
+  if (g_all.empty() &&
+      hipblaslt_ext::getAllAlgos(g_lt, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_N, HIPBLAS_OP_T, HIP_R_32F,
+                                 HIP_R_32F, HIP_R_32F, HIP_R_32F, HIPBLAS_COMPUTE_32F, g_all) != HIPBLAS_STATUS_SUCCESS)
+    return out;
+  Scratch sc;
+  const size_t an = (size_t)nb * mb * H, dn = (size_t)nb * S * H * H;
+  if (hipMalloc(&sc.a, an * 4) != hipSuccess || hipMalloc(&sc.b, an * 4) != hipSuccess ||
+      hipMalloc(&sc.d, dn * 4) != hipSuccess || hipStreamCreateWithFlags(&sc.st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&sc.e0) != hipSuccess || hipEventCreate(&sc.e1) != hipSuccess || hipMalloc(&sc.ws, kWsCap) != hipSuccess)
+    return out;
+  const unsigned gb = (unsigned)((an + 255) / 256);
+  hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(256), 0, sc.st, sc.a, (int64_t)an, 0x1234u);
+  hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(256), 0, sc.st, sc.b, (int64_t)an, 0x9e37u);
+  const float alpha = 1.0f, beta = 0.0f;
+  std::vector<std::pair<Timed, hipblasLtMatmulAlgo_t>> all;
+  for (auto& r : g_all) {
+    size_t w = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, r.algo, w) !=
+            HIPBLAS_STATUS_SUCCESS || w > kWsCap)
+      continue;
+    const float us = time_algo(p, r.algo, w, sc, dn, nullptr);
+    if (us > 0.0f) all.push_back({{us, hipblaslt_ext::getIndexFromAlgo(r.algo)}, r.algo});
+  }
+  std::sort(all.begin(), all.end(), [](const auto& x, const auto& y) { return x.first.us < y.first.us; });
+  int checked = 0;
+  for (auto& c : all) {
+    if (checked < det_check) {
+      bool det = false;
+      size_t w = 0;
+      hipblaslt_ext::matmulIsAlgoSupported(g_lt, p.md, &alpha, p.la, p.lb, &beta, p.lc, p.lc, c.second, w);
+      ++checked;
+      if (time_algo(p, c.second, w, sc, dn, &det) > 0.0f && det) out.push_back(c.first);
+    }
+  }
+  for (auto l : {p.la, p.lb, p.lc})
+    if (l) hipblasLtMatrixLayoutDestroy(l);
+  if (p.md) hipblasLtMatmulDescDestroy(p.md);
+  return out;
+}
+
 bool make_descriptors(int H, int mb, int S, int nb, Plan& p) {
   if (!g_lt && hipblasLtCreate(&g_lt) != HIPBLAS_STATUS_SUCCESS) {
     satrl_ppo_set_error("hipblasLtCreate");
@@ -350,6 +399,18 @@ int satrl_ppo_dw2_lib_pin(int H, int mb, int net, int S, int algo_index, const c
   if (!args_ok(H, mb, net, S) || algo_index < 0) return -1;
   std::lock_guard<std::mutex> lk(g_mu);
   return plan_locked(H, mb, S, net < 0 ? 2 : 1, algo_index, kernel) ? 0 : -3;
+}
+
+int satrl_ppo_dw2_lib_candidates(int H, int mb, int net, int S, int* algo_index, float* us, int cap) {
+  if (!args_ok(H, mb, net, S) || !algo_index || cap < 1) return -1;
+  std::lock_guard<std::mutex> lk(g_mu);
+  const auto c = candidates(H, mb, S, net < 0 ? 2 : 1, cap);
+  const int n = (int)std::min<size_t>(c.size(), (size_t)cap);
+  for (int k = 0; k < n; ++k) {
+    algo_index[k] = c[k].index;
+    if (us) us[k] = c[k].us;
+  }
+  return n;
 }
 
 int satrl_ppo_dw2_lib_plan_info(int H, int mb, int net, int S, int* algo_index, char* kernel, int kernel_len) {

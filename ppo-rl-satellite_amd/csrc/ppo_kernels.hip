@@ -250,7 +250,7 @@ __device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4
 #define SATRL_RP_BPD 2
 #endif
 #ifndef SATRL_RP_EARLYB
-#define SATRL_RP_EARLYB 0   // measured: no gain (30.6 vs 30.6 us; in-graph 55.5 vs 55.6)
+#define SATRL_RP_EARLYB 0   // measured: no gain, with __syncthreads (30.6 vs 30.6 us) or LDS-only barriers (r3)
 #endif
 #ifndef SATRL_RP_EARLYD
 #define SATRL_RP_EARLYD 1   // 30.4 -> 29.8 us, in-graph 55.6 -> 54.7
@@ -363,6 +363,25 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
   }
 }
 
+// Workgroup barrier of the MLP kernels' phases.  With SATRL_RP_LDSBAR (a dev
+// A/B knob, off) it orders only LDS (fence workgroup/"local" + s_barrier):
+// __syncthreads() also drains every outstanding global access, so the H1 /
+// dZ2 / slab stores and the weight chunks a phase issues early for the next
+// one (phase B's first W2 chunks, phase D's first W2T chunks) would be waited
+// for at every barrier instead of staying in flight across it.
+#ifndef SATRL_RP_LDSBAR
+#define SATRL_RP_LDSBAR 0   // r3: LDS-only barriers, alone and with SATRL_RP_EARLYB: no gain
+#endif
+__device__ __forceinline__ void rp_barrier() {
+#if SATRL_RP_LDSBAR
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#else
+  __syncthreads();
+#endif
+}
+
 // Shared-memory block and forward pass (phases A, B and the output-layer dot
 // products of C) common to rowpass_kernel and policy_kernel, so the rollout's
 // policy/value forward and the update's forward are the same instructions in
@@ -436,7 +455,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
       w3[t][0] = P[L.W3c + n]; w3[t][1] = 0.0f; w3[t][2] = 0.0f;
     }
   }
-  __syncthreads();
+  rp_barrier();
   PHASE_PROBE(9);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -465,7 +484,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
     }
   if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
   PHASE_PROBE(11);
-  __syncthreads();
+  rp_barrier();
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
@@ -520,7 +539,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         for (int j = 0; j < 4; ++j) sm.osum[w][16 * rt + 4 * lg + j][q] = ps[(q * RT + rt) * 4 + j];
     }
   }
-  __syncthreads();
+  rp_barrier();
   PHASE_PROBE(3);
 }
 
@@ -669,7 +688,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
       }
     }
   }
-  __syncthreads();
+  rp_barrier();
   PHASE_PROBE(4);
   float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
   float d2v[RT][CT][4];
@@ -716,7 +735,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   if (net == 0) tail(std::true_type{});
   else tail(std::false_type{});
   store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
-  __syncthreads();
+  rp_barrier();
   PHASE_PROBE(5);
 
   // ---- D: dH1 = dZ2 W2 -------------------------------------------------------

@@ -111,6 +111,7 @@ _SIGS = {
     "satrl_ppo_dw2_lib": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_int64, _vp], C.c_int),
     "satrl_ppo_dw2_lib_pin": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p], C.c_int),
     "satrl_ppo_dw2_lib_plan_info": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.c_char_p, C.c_int], C.c_int),
+    "satrl_ppo_dw2_lib_candidates": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, C.c_int], C.c_int),
     "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
