@@ -41,8 +41,10 @@ python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$ROOT/profiles"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o run -- \
     python3 "$ROOT/bench.py" --profile-tag "$TAG" > "$OUT/bench.json" 2> "$OUT/bench.err"
 rm -f "$OUT/bench/run_kernel_trace.csv" "$OUT/env_rollout/run_kernel_trace.csv"
-python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$OUT/profiles"
+# the committed summaries first, then this run's (the fresh bench stats must win)
+mkdir -p "$OUT/profiles"
 cp "$ROOT"/profiles/"${TAG}"_*.json "$OUT/profiles/" 2>/dev/null || true
 cp "$ROOT"/profiles/"${TAG}"_*.csv "$OUT/profiles/" 2>/dev/null || true
+python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$OUT/profiles"
 cp "$OUT/profiles/${TAG}_bench_kernel_stats.csv" "$ROOT/profiles/"
 tail -1 "$OUT/bench.json"
