@@ -110,6 +110,33 @@ __device__ __forceinline__ int net_of(const Layout& L, int64_t e, int H) {
 // ---------------------------------------------------------------------------
 using f4 = __attribute__((ext_vector_type(4))) float;
 
+// Write-through (sc1) stores for what the next launch of the chain reads: an
+// agent-scope relaxed atomic store is a plain global_store with sc1, so the
+// line goes on to memory as it is written instead of staying dirty in this
+// XCD's L2 until the end-of-kernel write-back (MI355X_MICROARCH.md
+// "boundary": + B / 6 TB/s behind B dirty bytes).  Bit mask: 1 rowpass H1 /
+// dZ2, 2 rowpass slabs, 4 reduce G, 8 Adam P/M/V/W2T.
+#ifndef SATRL_WT
+#define SATRL_WT 0
+#endif
+template <int BIT>
+__device__ __forceinline__ void st_out(float* p, float v) {
+  if constexpr ((SATRL_WT & BIT) != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <int BIT>
+__device__ __forceinline__ void st_out4(float4* p, float4 v) {
+  if constexpr ((SATRL_WT & BIT) != 0) {
+    float* q = reinterpret_cast<float*>(p);
+    __hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *p = v;
+  }
+}
+
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -252,6 +279,13 @@ __device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4
 #ifndef SATRL_RP_EARLYB
 #define SATRL_RP_EARLYB 0   // measured: no gain, with __syncthreads (30.6 vs 30.6 us) or LDS-only barriers (r3)
 #endif
+#ifndef SATRL_RP_PRIO
+// rowpass: s_setprio 1 while a wave runs its phase-B (bit 1) / phase-D (bit 2)
+// MFMA stream, 0 after it, so the VALU tail of the waves that are done (fc2
+// tanh and output dots after B, phase E after D) issues only in the gaps of
+// the younger waves' MFMA streams instead of ahead of them (oldest first)
+#define SATRL_RP_PRIO 0
+#endif
 #ifndef SATRL_RP_EARLYD
 #define SATRL_RP_EARLYD 1   // 30.4 -> 29.8 us, in-graph 55.6 -> 54.7
 #endif
@@ -293,6 +327,11 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
     // fully unrolled so every buffer index is static
     constexpr int NB = kBPD + 1;
     float4 bb[NB][CT][2], aa[2][RT][2];
+#if defined(SATRL_RP_FAKE_FEED)
+    // timing probe only (numerically wrong): operands made in registers, no
+    // loads -- bit 1 the B (weight) operand, bit 2 the LDS A operand
+    auto fake4 = [&](int c) { const float v = 1e-3f * (float)(i + c); return make_float4(v, v, v, v); };
+#endif
 #ifdef SATRL_RP_FAKE_LDS_B
     if constexpr (false) {
 #else
@@ -306,11 +345,34 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
 #pragma unroll
       for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB_, bb[c]);
     }
+#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 1)
+#pragma unroll
+    for (int c = 0; c < kBPD; ++c)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) { bb[c][t][0] = fake4(c + t); bb[c][t][1] = fake4(c + t + 2); }
+#endif
+#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 2)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) { aa[0][rt][0] = fake4(rt); aa[0][rt][1] = fake4(rt + 1); }
+#else
     a_chunk<LDA, RT>(ap, aa[0]);
+#endif
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
+#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 1)
+      if (c + kBPD < NC)
+#pragma unroll
+        for (int t = 0; t < CT; ++t) { bb[(c + kBPD) % NB][t][0] = fake4(c + t); bb[(c + kBPD) % NB][t][1] = fake4(c + t + 2); }
+#else
       if (c + kBPD < NC) b_chunk<CT>(bp + 32 * (c + kBPD), LDB_, bb[(c + kBPD) % NB]);
+#endif
+#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 2)
+      if (c + 1 < NC)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) { aa[(c + 1) % 2][rt][0] = fake4(c + rt); aa[(c + 1) % 2][rt][1] = fake4(c + rt + 3); }
+#else
       if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
+#endif
 #ifdef SATRL_RP_CHUNK_SYNC
       // timing variant: the workgroup's waves meet every SATRL_RP_CHUNK_SYNC
       // chunks, so the waves of a SIMD interleave their MFMA streams instead of
@@ -349,7 +411,7 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
 #pragma unroll
       for (int t = 0; t < CT; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) out[(int64_t)(16 * rt + 4 * lg + j) * ld + n0 + 16 * t + li] = v[rt][t][j];
+        for (int j = 0; j < 4; ++j) st_out<1>(&out[(int64_t)(16 * rt + 4 * lg + j) * ld + n0 + 16 * t + li], v[rt][t][j]);
   } else {
 #pragma unroll
     for (int rt = 0; rt < R / 16; ++rt)
@@ -358,7 +420,7 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 16 * rt + 4 * lg + j;
-          if (r < nvalid) out[(int64_t)r * ld + n0 + 16 * t + li] = v[rt][t][j];
+          if (r < nvalid) st_out<1>(&out[(int64_t)r * ld + n0 + 16 * t + li], v[rt][t][j]);
         }
   }
 }
@@ -488,7 +550,9 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
+  if constexpr (APRE && (SATRL_RP_PRIO & 1)) __builtin_amdgcn_s_setprio(1);
   mfma_rows<H, LDA, H, RT, CT, APRE, EB>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
+  if constexpr (APRE && (SATRL_RP_PRIO & 1)) __builtin_amdgcn_s_setprio(0);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -726,9 +790,12 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
 #pragma unroll
       for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
       if (lg == 0) {
-        tp[net * H + n] = cb2;                                     // db2
-        if constexpr (ACT) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }   // dW3a
-        else tp[5 * H + 8 + n] = cw[0];                            // dW3c
+        st_out<2>(&tp[net * H + n], cb2);                          // db2
+        if constexpr (ACT) {                                       // dW3a
+          st_out<2>(&tp[2 * H + n], cw[0]); st_out<2>(&tp[3 * H + n], cw[1]); st_out<2>(&tp[4 * H + n], cw[2]);
+        } else {
+          st_out<2>(&tp[5 * H + 8 + n], cw[0]);                    // dW3c
+        }
       }
     }
   };
@@ -743,7 +810,9 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
+  if constexpr ((SATRL_RP_PRIO & 2) != 0) __builtin_amdgcn_s_setprio(1);
   mfma_rows<H, LDA, H, RT, CT, true, SATRL_RP_EARLYD>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
+  if constexpr ((SATRL_RP_PRIO & 2) != 0) __builtin_amdgcn_s_setprio(0);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
@@ -767,7 +836,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
       const int kp = 16 * hb + li;
       if (kp < 20) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) pw[(int64_t)(n0 + 16 * t + 4 * lg + j) * 20 + kp] = d[j];
+        for (int j = 0; j < 4; ++j) st_out<2>(&pw[(int64_t)(n0 + 16 * t + 4 * lg + j) * 20 + kp], d[j]);
       }
     }
   }
@@ -1350,7 +1419,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCH1>(reinterpret_cast<const float4*>(p1), n4, g.nw1, col, valid, red);
-      if (lead && valid) G4[L.W1 / 4 + col] = v;
+      if (lead && valid) st_out4<4>(&G4[L.W1 / 4 + col], v);
     } else if (lead && valid) {
       v = G4[L.W1 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.W1 / 4 + col] = v; }
@@ -1369,7 +1438,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCHt>(reinterpret_cast<const float4*>(pt), n4, g.nwg, col, valid, red);
-      if (lead && valid) G4[L.b2 / 4 + col] = v;
+      if (lead && valid) st_out4<4>(&G4[L.b2 / 4 + col], v);
     } else if (lead && valid) {
       v = G4[L.b2 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.b2 / 4 + col] = v; }
@@ -1404,7 +1473,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
     if (mode & 1) {
       v = chunk_sum4<kRedCH2>(reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4, HH4, g.S,
                               col - net * HH4, valid, red);
-      if (lead && valid) G4[col] = v;
+      if (lead && valid) st_out4<4>(&G4[col], v);
     } else if (lead && valid) {
       v = G4[col];
       if (world > 1) { v = f4div(v, (float)world); G4[col] = v; }
@@ -1540,9 +1609,9 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.z = adam_elem(g.z, m.z, v.z, p.z, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.w = adam_elem(g.w, m.w, v.w, p.w, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  P4[e4] = pn;
-  M4[e4] = m;
-  V4[e4] = v;
+  st_out4<8>(&P4[e4], pn);
+  st_out4<8>(&M4[e4], m);
+  st_out4<8>(&V4[e4], v);
   if ((int)blockIdx.x < nbw && W2T != nullptr) {                   // keep fc2.weight^T for the dH1 MFMA
     const int nl = t >> 3, kl = (t & 7) * 4;
     tile[nl][kl] = pn.x; tile[nl][kl + 1] = pn.y; tile[nl][kl + 2] = pn.z; tile[nl][kl + 3] = pn.w;
@@ -1551,7 +1620,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
     const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
     // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
     const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
-    reinterpret_cast<float4*>(W2T)[((int64_t)net * H * H + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
+    st_out4<8>(&reinterpret_cast<float4*>(W2T)[((int64_t)net * H * H + (int64_t)(k0 + nl) * H + n0 + kl) / 4], o);
   }
 }
 
