@@ -264,6 +264,7 @@ class FusedMinibatch:
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
         self.split = bool(split_chains) and learner.pg is None
+        self.offset_cycles = int(os.environ.get("SATRL_CHAIN_OFFSET", "0"))   # dev knob (split chains)
         H, dev = learner.H, learner.device
         nwg, nblk = C.c_int64(), C.c_int64()
         check(_lib.lib().satrl_ppo_sizes(H, self.mb, C.byref(nwg), C.byref(nblk)), "satrl_ppo_sizes")
@@ -445,6 +446,11 @@ class FusedMinibatch:
         self.side.wait_stream(cur)
         fn(0)
         with torch.cuda.stream(self.side):
+            if self.offset_cycles > 0:
+                # the critic chain starts this many shader cycles behind the actor's
+                # (a GPU spin), so one net's rowpass runs beside the other's
+                # dW2 / reduce / Adam instead of in lockstep with its rowpass
+                torch.cuda._sleep(self.offset_cycles)
             fn(1)
         cur.wait_stream(self.side)
 
