@@ -697,6 +697,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
           // (the forward expression of gaussian_act, bit for bit: logp_old)
           logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - hcs[1][d]) - kLogSqrt2Pi;
         }
+        PHASE_PROBE(12);
         const float lsum = (logp[0] + logp[1]) + logp[2];
         const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
         const float ratio = expf(lsum - lold);
@@ -722,6 +723,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
+    PHASE_PROBE(13);
 #pragma unroll
     for (int q = 0; q < 4; ++q) dz3s[r][q] = dz[q];
     // the block's b3a / log_std / b3c partials: sums over its R rows, reduced
@@ -737,6 +739,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
         red[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(red[q]), 0)) +
                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(red[q]), 16));
     }
+    PHASE_PROBE(14);
     if (r == 0) {
       if (net == 0) {
 #pragma unroll
