@@ -33,3 +33,34 @@ def test_bench_two_ranks_one_device():
     assert dp["world"] == 2 and dp["backend"] == "gloo"
     sl = dp["configs3_semantics_slice"]
     assert sl["rows_per_rank"] == 2048 and sl["us_per_global_minibatch_step"] > 0
+
+
+def test_bench_one_gpu_line_keeps_the_contract():
+    """The N = 1 line the driver records: one JSON line with the contract's
+    keys, the rowpass roofline (achieved = FLOP per launch / launch time,
+    frac = achieved / peak) and a bounded CPU baseline of the same workload."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--num-envs", "1024", "--horizon", "64",
+                        "--epochs", "1", "--minibatch", "4096", "--steps", "1", "--warmup", "1",
+                        "--kernel-iters", "10", "--cpu-baseline-seconds", "1"],
+                       env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert out["metric"] == base["metric"] and out["unit"] == "env-steps/s"
+    assert out["n_gpus"] == 1 and out["steps"] == 1 and out["warmup"] == 1
+    assert out["higher_is_better"] is True and out["scaling"] == "weak" and out["vs_baseline"] is None
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert abs(out["value"] - 1024 * 64 / (out["ms_per_step"] / 1e3)) <= 1e-6 * out["value"]
+    assert "workload" in out["config"] and out["config"]["parallelism"] == "dp1"
+    rf = out["roofline"]
+    assert rf["bound"] == "mfma" and rf["unit"] == "TFLOP/s" and rf["peak"] == 157.3
+    assert rf["achieved"] > 0 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    assert abs(rf["achieved"] - rf["flop_per_launch"] / rf["avg_launch_us"] / 1e6) <= 1e-6 * rf["achieved"]
+    cb = out["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference") and cb["sample"]
