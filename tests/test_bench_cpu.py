@@ -80,18 +80,19 @@ def _run_bench(*argv, env=None, timeout=180):
                           text=True, timeout=timeout)
 
 
-def test_gpus_n_launches_n_ranks_and_rank0_reports_once():
-    """`bench.py --gpus 2` (no launcher) starts 2 ranks itself; the process
-    group has 2 ranks, the max-over-ranks timing and the report run, and
+@pytest.mark.parametrize("n", [2, 4])
+def test_gpus_n_launches_n_ranks_and_rank0_reports_once(n):
+    """`bench.py --gpus N` (no launcher) starts N ranks itself; the process
+    group has N ranks, the max-over-ranks timing and the report run, and
     exactly one JSON line comes out (rank 0's), with n_gpus from the group."""
     import json
-    r = _run_bench("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1")
+    r = _run_bench("--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2 and out["steps"] == 3 and out["dry_run"]
-    assert out["config"]["parallelism"] == "dp2"
+    assert out["n_gpus"] == n and out["ranks_seen"] == n and out["steps"] == 3 and out["dry_run"]
+    assert out["config"]["parallelism"] == f"dp{n}"
 
 
 def test_gpus_1_stays_one_process():
