@@ -121,7 +121,7 @@ class Comm:
         rc = _lib().ncclCommGetAsyncError(self._comm, C.byref(err))
         return rc if rc not in (0, _NCCL_IN_PROGRESS) else err.value
 
-    def wait(self, deadline_s: float, stream=None, poll_s: float = 0.005):
+    def wait(self, deadline_s: float, stream=None, poll_s: float = 0.001):
         """Host watchdog between graph replays: block until the work queued so
         far on `stream` (default: the current one) has finished, polling
         ncclCommGetAsyncError meanwhile.  An RCCL error, or no completion
