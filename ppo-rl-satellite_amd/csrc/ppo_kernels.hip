@@ -208,24 +208,36 @@ __device__ __forceinline__ float tanh_f32(float x) {
 #endif
 }
 
-template <int CT>
+// The k mapping of a 32-wide chunk (fc2 / dH1 phases): lane group g holds
+// k = 8g + 4h + e (SATRL_RP_KMAP 0: each lane's two float4 adjacent, so a
+// wave-instruction touches every 128-B row segment at a 32-B stride) or
+// k = 16h + 4g + e (1: each float4 instruction reads 64 contiguous bytes per
+// row).  The MFMA sequence groups k differently, so the two are different
+// f32 roundings of the same sums; rollout and update share the mapping.
+#ifndef SATRL_RP_KMAP
+#define SATRL_RP_KMAP 0
+#endif
+constexpr int kGOff = SATRL_RP_KMAP ? 4 : 8;    // floats between lane groups
+constexpr int kHOff = SATRL_RP_KMAP ? 16 : 4;   // floats between a lane's two float4
+
+template <int CT, int HOFF = kHOff>
 __device__ __forceinline__ void b_chunk(const float* __restrict__ bp, int LDB, float4 (&b)[CT][2]) {
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     b[t][0] = *reinterpret_cast<const float4*>(bp + 16 * t * LDB);
-    b[t][1] = *reinterpret_cast<const float4*>(bp + 16 * t * LDB + 4);
+    b[t][1] = *reinterpret_cast<const float4*>(bp + 16 * t * LDB + HOFF);
   }
   __builtin_amdgcn_sched_barrier(0);   // keep the prefetch where it is issued
 }
 
-template <int LDA, int RT, int CT>
+template <int LDA, int RT, int CT, int HOFF = kHOff>
 __device__ __forceinline__ void mfma_chunk(const float* __restrict__ ap, const float4 (&b)[CT][2],
                                            f4 (&acc)[RT][CT]) {
   float4 a[RT][2];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     a[rt][0] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA);
-    a[rt][1] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA + 4);
+    a[rt][1] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA + HOFF);
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -246,7 +258,7 @@ __device__ __forceinline__ void a_chunk(const float* __restrict__ ap, float4 (&a
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     a[rt][0] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA);
-    a[rt][1] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA + 4);
+    a[rt][1] = *reinterpret_cast<const float4*>(ap + 16 * rt * LDA + kHOff);
   }
   __builtin_amdgcn_sched_barrier(0);
 }
@@ -301,31 +313,33 @@ struct WPre {
 template <int LDB, int CT>
 __device__ __forceinline__ void mfma_rows_pre(const float* __restrict__ B, int n0, WPre<CT>& pre) {
   const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
+  const float* bp = B + (int64_t)(n0 + i) * LDB + kGOff * g;
+  constexpr int BPD = kBPD < LDB / 32 ? kBPD : LDB / 32;      // (K = LDB here: W2 / W2T rows)
 #pragma unroll
-  for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, pre.bb[c]);
+  for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, pre.bb[c]);
 }
 
 template <int K, int LDA, int LDB, int RT, int CT, bool APRE, bool PRE = false>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
                                           f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr) {
   constexpr int NC = K / 32;
-  static_assert(NC % 2 == 0 && NC >= kBPD, "chunk pairs");
+  constexpr int BPD = kBPD < NC ? kBPD : NC;                     // prefetch distance in chunks
+  static_assert(NC % 2 == 0, "chunk pairs");
   static_assert(APRE || !PRE, "early-issued chunks feed the APRE path");
   const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const float* ap = A + i * LDA + 8 * g;
-  const float* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
+  const float* ap = A + i * LDA + kGOff * g;
+  const float* bp = B + (int64_t)(n0 + i) * LDB + kGOff * g;
   if constexpr (APRE) {
 #ifdef SATRL_RP_FAKE_LDS_B
     // timing probe only (numerically wrong): the B operand read from LDS (the A
     // image), i.e. the MFMA phases with a perfect on-chip weight feed
-    bp = A + i * LDA + 8 * g;
+    bp = A + i * LDA + kGOff * g;
     constexpr int LDB_ = LDA;
 #else
     constexpr int LDB_ = LDB;
 #endif
     // fully unrolled so every buffer index is static
-    constexpr int NB = kBPD + 1;
+    constexpr int NB = BPD + 1;
     float4 bb[NB][CT][2], aa[2][RT][2];
 #if defined(SATRL_RP_FAKE_FEED)
     // timing probe only (numerically wrong): operands made in registers, no
@@ -338,16 +352,16 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
     if constexpr (PRE) {
 #endif
 #pragma unroll
-      for (int c = 0; c < kBPD; ++c)
+      for (int c = 0; c < BPD; ++c)
 #pragma unroll
         for (int t = 0; t < CT; ++t) { bb[c][t][0] = pre->bb[c][t][0]; bb[c][t][1] = pre->bb[c][t][1]; }
     } else {
 #pragma unroll
-      for (int c = 0; c < kBPD; ++c) b_chunk<CT>(bp + 32 * c, LDB_, bb[c]);
+      for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB_, bb[c]);
     }
 #if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 1)
 #pragma unroll
-    for (int c = 0; c < kBPD; ++c)
+    for (int c = 0; c < BPD; ++c)
 #pragma unroll
       for (int t = 0; t < CT; ++t) { bb[c][t][0] = fake4(c + t); bb[c][t][1] = fake4(c + t + 2); }
 #endif
@@ -360,11 +374,11 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
 #if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 1)
-      if (c + kBPD < NC)
+      if (c + BPD < NC)
 #pragma unroll
-        for (int t = 0; t < CT; ++t) { bb[(c + kBPD) % NB][t][0] = fake4(c + t); bb[(c + kBPD) % NB][t][1] = fake4(c + t + 2); }
+        for (int t = 0; t < CT; ++t) { bb[(c + BPD) % NB][t][0] = fake4(c + t); bb[(c + BPD) % NB][t][1] = fake4(c + t + 2); }
 #else
-      if (c + kBPD < NC) b_chunk<CT>(bp + 32 * (c + kBPD), LDB_, bb[(c + kBPD) % NB]);
+      if (c + BPD < NC) b_chunk<CT>(bp + 32 * (c + BPD), LDB_, bb[(c + BPD) % NB]);
 #endif
 #if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 2)
       if (c + 1 < NC)
@@ -523,7 +537,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_chunk<LDS_S, RT, CT>(&sm.S[li][8 * lg], bw1, acc);
+  mfma_chunk<LDS_S, RT, CT, 4>(&sm.S[li][8 * lg], bw1, acc);
   // phase B's first W2 chunks go out now: their latency overlaps the fc1 tanh,
   // the H1 stores and the barrier
   constexpr bool EB = APRE && SATRL_RP_EARLYB;
@@ -970,7 +984,7 @@ __global__ void __launch_bounds__(1024, 1) rowpass_dual_kernel(int mb, const flo
   float h1[1][CT][4];
 #pragma unroll
   for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_chunk<LDS_S, 1, CT>(&S[li][8 * lg], bw1, acc);
+  mfma_chunk<LDS_S, 1, CT, 4>(&S[li][8 * lg], bw1, acc);
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const int n = n0 + 16 * t + li;
