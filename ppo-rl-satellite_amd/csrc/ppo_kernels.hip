@@ -291,6 +291,13 @@ __device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4
 #ifndef SATRL_RP_EARLYB
 #define SATRL_RP_EARLYB 0   // measured: no gain, with __syncthreads (30.6 vs 30.6 us) or LDS-only barriers (r3)
 #endif
+#ifndef SATRL_RP_LATE_STORES
+// rowpass: issue the H1 (bit 1) / dZ2 (bit 2) global stores after the next
+// MFMA phase instead of before it (vmcnt counts loads and stores in issue
+// order, so a phase's waits for its weight chunks would otherwise also wait
+// for the stores issued ahead of them)
+#define SATRL_RP_LATE_STORES 0
+#endif
 #ifndef SATRL_RP_PRIO
 // rowpass: s_setprio 1 while a wave runs its phase-B (bit 1) / phase-D (bit 2)
 // MFMA stream, 0 after it, so the VALU tail of the waves that are done (fc2
@@ -558,7 +565,8 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
       }
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
-  if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
+  if (!(SATRL_RP_LATE_STORES & 1) && h1out != nullptr)
+    store_rows<R, CT>(h1out, H, n0, nvalid, h1);                       // straight-line unless ragged
   PHASE_PROBE(11);
   rp_barrier();
   PHASE_PROBE(1);
@@ -567,6 +575,9 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   if constexpr (APRE && (SATRL_RP_PRIO & 1)) __builtin_amdgcn_s_setprio(1);
   mfma_rows<H, LDA, H, RT, CT, APRE, EB>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   if constexpr (APRE && (SATRL_RP_PRIO & 1)) __builtin_amdgcn_s_setprio(0);
+  // (late: behind phase B's weight loads, so none of B's in-order vmcnt
+  // waits also waits for these stores to complete)
+  if ((SATRL_RP_LATE_STORES & 1) && h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -818,7 +829,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   };
   if (net == 0) tail(std::true_type{});
   else tail(std::false_type{});
-  store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
+  if (!(SATRL_RP_LATE_STORES & 2)) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   rp_barrier();
   PHASE_PROBE(5);
 
@@ -830,6 +841,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   if constexpr ((SATRL_RP_PRIO & 2) != 0) __builtin_amdgcn_s_setprio(1);
   mfma_rows<H, LDA, H, RT, CT, true, SATRL_RP_EARLYD>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   if constexpr ((SATRL_RP_PRIO & 2) != 0) __builtin_amdgcn_s_setprio(0);
+  if (SATRL_RP_LATE_STORES & 2) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
