@@ -332,6 +332,15 @@ def test_autoreset_block_geometries_vs_oracle(satrl_env, oracle, n):
     assert ties <= max(2, counted // 20000), (ties, counted)
 
 
+def test_autoreset_full_size_vs_oracle(satrl_env, oracle):
+    """configs[3]'s total env count (65536, 512 workgroups of 128 lanes) step-
+    locked to the oracle for 8 steps, episodes ending at step 5 and resetting
+    in-kernel: the same bars at the BASELINE's largest size."""
+    n = 65536
+    ties, counted = _locked_autoreset_rollout(satrl_env, oracle, n, 8, 65536 + 1, 15000.0, 5, "autoreset n=65536")
+    assert ties <= max(2, counted // 20000), (ties, counted)
+
+
 def test_env_rk45_cw_mode_vs_reference_solve_ivp(satrl_env):
     """propagator 2 (satellite_function.py:783-839: the CW orbit_ode by
     scipy solve_ivp RK45, dense output at the 100-s step) on the GPU vs the
