@@ -130,6 +130,22 @@ def test_gae_restatement(oracle):
     assert np.array_equal(adv, u["adv"].reshape(-1))
 
 
+def test_gae_vectorised_restatement_equals_the_per_env_scan(oracle):
+    """gae_time_major_vec (the full-size checker) is the per-env scan bit
+    for bit: on the reference's own buffer as one column, and on random
+    [T, N] tables with episode ends."""
+    u = golden("update_case")
+    col = [np.asarray(u[k], np.float32).reshape(-1, 1) for k in ("r", "vs", "vs_", "dw", "done")]
+    assert np.array_equal(oracle.gae_time_major_vec(*col)[:, 0], u["adv"].reshape(-1))
+    rng = np.random.default_rng(5)
+    T, N = 301, 67
+    r = rng.normal(0, 3, (T, N)).astype(np.float32)
+    v = rng.normal(0, 10, (T + 1, N)).astype(np.float32)
+    d = (rng.uniform(size=(T, N)) < 0.05).astype(np.float32)
+    assert np.array_equal(oracle.gae_time_major_vec(r, v[:-1], v[1:], d, d),
+                          oracle.gae_time_major(r, v[:-1], v[1:], d, d))
+
+
 def test_stm_matches_reference_matrix(oracle):
     import math
     omega = math.sqrt(3.986e14 / (42164000 ** 3))

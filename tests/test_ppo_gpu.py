@@ -31,6 +31,22 @@ def test_gae_kernel_bitexact(oracle):
     assert np.array_equal(vt.cpu().numpy(), (ref + v[:-1]).astype(np.float32))
 
 
+def test_gae_kernel_bitexact_full_size(oracle):
+    """BASELINE configs[2]'s buffer (T 2048 x 16384 envs) through the HIP
+    scan, bit for bit against the oracle's vectorised scan."""
+    from satrl.ppo import gae
+    rng = np.random.default_rng(1)
+    T, N = 2048, 16384
+    r = rng.normal(0, 3, (T, N)).astype(np.float32)
+    v = rng.normal(0, 10, (T + 1, N)).astype(np.float32)
+    d = (rng.uniform(size=(T, N)) < 0.002).astype(np.uint8)
+    adv, vt = gae(torch.tensor(r, device="cuda"), torch.tensor(d, device="cuda"), torch.tensor(v, device="cuda"),
+                  0.99, 0.95)
+    ref = oracle.gae_time_major_vec(r, v[:-1], v[1:], d.astype(np.float32), d.astype(np.float32))
+    assert np.array_equal(adv.cpu().numpy(), ref)
+    assert np.array_equal(vt.cpu().numpy(), (ref + v[:-1]).astype(np.float32))
+
+
 def test_gae_kernel_on_reference_buffer():
     """update_case: the reference's flat buffer as one env column."""
     from satrl.ppo import _gae_explicit
