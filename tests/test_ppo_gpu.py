@@ -440,9 +440,11 @@ def test_update_graph_groups_equal_eager():
         assert torch.equal(a, b)
 
 
-def test_policy_act_and_value_kernels():
+@pytest.mark.parametrize("N", [1000, 65536])
+def test_policy_act_and_value_kernels(N):
     """satrl_policy_act / satrl_policy_value vs the torch modules + satrl_gaussian_sample
-    (same Philox draw); every row independent of N and of its position (bitwise)."""
+    (same Philox draw); every row independent of N and of its position (bitwise).
+    N 65536: configs[3]'s total env count in one launch."""
     from satrl.ppo import PPOLearner, gaussian_sample, policy_act, policy_value
     torch.manual_seed(5)
     args = _args(hidden_width=256)
@@ -452,7 +454,6 @@ def test_policy_act_and_value_kernels():
         for L in (Lp, Le):
             for p in list(L.actor.parameters()) + list(L.critic.parameters()):
                 p.add_(torch.randn_like(p) * 0.05)
-    N = 1000
     g = torch.Generator(device="cuda").manual_seed(2)
     obs = torch.randn((N, 18), device="cuda", generator=g)
     sb = torch.tensor([7], dtype=torch.int64, device="cuda")
