@@ -262,3 +262,31 @@ def test_per_gpu_minibatch_variant_and_labels():
     for k in range(64 * 24 // 256):
         assert torch.equal(torch.bincount(blk[k * 256:(k + 1) * 256], minlength=8),
                            torch.full((8,), 32, device=perm.device))
+
+
+def test_rollout_sharding_invariant_at_full_size():
+    """BASELINE configs[2]'s env count, H 256: one 16384-env rollout equals two
+    8192-env shards (global env ids 0-8191 and 8192-16383, same seed) bit for
+    bit -- obs, rewards, done flags, actions and log-probs over 24 steps with
+    episodes ending and resetting in-kernel."""
+    sys.path.insert(0, PKG_DIR)
+    from satrl.trainer import VecTrainer, args_param
+
+    def collect(n, offset):
+        args = args_param(batch_size=n * 24, mini_batch_size=4096, hidden_width=256, K_epochs=1, num_envs=n,
+                          horizon=24, max_episode_steps=9, seed=3, rollout_graph_chunk=8, chkpt_dir="/tmp")
+        tr = VecTrainer(args, flag=0, d_capture=15000.0, env_offset=offset)
+        tr.collect()
+        torch.cuda.synchronize()
+        b = tr.buf
+        out = [x.cpu().numpy() for x in (b.obs, b.rew, b.done, b.act, b.logp)]
+        del tr
+        return out
+
+    full = collect(16384, 0)
+    halves = [collect(8192, 0), collect(8192, 8192)]
+    import numpy as np
+    for k, name in enumerate(("obs", "rew", "done", "act", "logp")):
+        got = np.concatenate([halves[0][k], halves[1][k]], axis=1)
+        assert np.array_equal(got, full[k]), name
+    assert full[2].any()                                  # episodes did end inside the window
