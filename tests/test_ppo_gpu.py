@@ -353,6 +353,34 @@ def test_vec_trainer_iteration_and_determinism():
     assert s1[0] > 0           # episodes finished (max_episode_steps=20 < 64 steps)
 
 
+def test_full_size_iteration_is_bitwise_reproducible():
+    """BASELINE configs[2] as the bench runs it (16384 envs x 2048 steps,
+    H 256, minibatch 4096, 10 epochs = 81 920 Adam steps through the update's
+    graphs): two trainers from the same seed end the iteration with the same
+    parameters, Adam moments and buffer bit for bit (no atomics, pinned dW2
+    plan), and the update moved the parameters."""
+    import gc
+    from satrl.trainer import VecTrainer
+    outs = []
+    for _ in range(2):
+        args = _args(batch_size=16384 * 2048, mini_batch_size=4096, hidden_width=256, K_epochs=10, num_envs=16384,
+                     horizon=2048, max_episode_steps=1000, seed=11, rollout_graph_chunk=64, update_graph_group=64)
+        tr = VecTrainer(args, flag=0, d_capture=15000.0)
+        p0 = tr.learner.P.clone()
+        st = tr.iteration()
+        torch.cuda.synchronize()
+        assert tr.env.check_errors() == 0
+        outs.append((p0, tr.learner.P.clone(), tr.learner.M.clone(), tr.learner.V.clone(), tr.buf.rew.clone(), st))
+        del tr
+        gc.collect()
+        torch.cuda.empty_cache()
+    (p0a, pa, ma, va, ra, sa), (p0b, pb, mb_, vb, rb, sb) = outs
+    assert torch.equal(p0a, p0b)
+    assert torch.equal(pa, pb) and torch.equal(ma, mb_) and torch.equal(va, vb) and torch.equal(ra, rb)
+    assert not torch.equal(pa, p0a) and torch.isfinite(pa).all()
+    assert sa[0] > 0           # episodes finished (max_episode_steps 1000 < 2048 steps)
+
+
 def test_vec_trainer_graph_vs_eager_rollout():
     from satrl.trainer import VecTrainer
     res = []
