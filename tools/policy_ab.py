@@ -18,19 +18,25 @@ from satrl.trainer import args_param  # noqa: E402
 a = args_param(hidden_width=256, chkpt_dir="/tmp")
 Lp, Le = PPOLearner(a, "pursuer", use_graph=False), PPOLearner(a, "evader", use_graph=False)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-for N in (16384, 65536):
+for N in (16384, 65536, 2049 * 16384):          # the last: the update's values pass over T + 1 steps
+    big = N > 65536
     obs = torch.randn((N, 18), device="cuda") * 1e5
-    a0, l0, a1, l1 = (torch.empty((N, 3), device="cuda") for _ in range(4))
+    a0, l0, a1, l1 = (torch.empty((N, 3), device="cuda") for _ in range(4)) if not big else (None,) * 4
     v = torch.empty(N, device="cuda")
     res = []
-    for fn in (lambda: policy_act(256, obs, Lp.P, Le.P, 1.6, 0, 0, 0, a0, l0, a1, l1),
-               lambda: policy_value(256, obs, Lp.P, v)):
-        for _ in range(5):
+    fns = ([] if big else [lambda: policy_act(256, obs, Lp.P, Le.P, 1.6, 0, 0, 0, a0, l0, a1, l1)]) + \
+          [lambda: policy_value(256, obs, Lp.P, v)]
+    for fn in fns:
+        reps = 3 if big else 50
+        for _ in range(2 if big else 5):
             fn()
         e0.record()
-        for _ in range(50):
+        for _ in range(reps):
             fn()
         e1.record()
         torch.cuda.synchronize()
-        res.append(e0.elapsed_time(e1) * 1e3 / 50)
-    print(f"{os.path.basename(_L.LIB_PATH)} N={N}: act {res[0]:8.2f} us  value {res[1]:8.2f} us")
+        res.append(e0.elapsed_time(e1) * 1e3 / reps)
+    if big:
+        print(f"{os.path.basename(_L.LIB_PATH)} N={N}: value {res[0] / 1e3:8.2f} ms")
+    else:
+        print(f"{os.path.basename(_L.LIB_PATH)} N={N}: act {res[0]:8.2f} us  value {res[1]:8.2f} us")
