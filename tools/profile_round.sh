@@ -26,6 +26,10 @@ pmc pmc_env_fetch FETCH_SIZE -- "$W/env_workload.py" 40
 pmc pmc_env_write WRITE_SIZE -- "$W/env_workload.py" 40
 pmc pmc_mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/rowpass_workload.py" 40
 pmc pmc_policy_mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/policy_workload.py" 40
+# the post-rowpass chain (hipBLASLt dW2, reduce, Adam) of eager minibatch steps
+pmc pmc_step_fetch FETCH_SIZE -- "$W/step_workload.py" 40
+pmc pmc_step_write WRITE_SIZE -- "$W/step_workload.py" 40
+pmc pmc_step_mfma SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/step_workload.py" 40
 # FP64 VALU work of the env step: the F64 instruction counters this rocprofv3 lists (<= 7 SQ + GRBM)
 F64=$(grep -o 'SQ_INSTS_VALU_[A-Z0-9_]*F64' "$OUT/avail.txt" | sort -u | head -7 | tr '\n' ' ')
 if [ -n "$F64" ]; then

@@ -84,6 +84,38 @@ def main():
         with open(os.path.join(prof, f"{tag}_rowpass_mfma_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res))
+    sf = os.path.join(d, "pmc_step_fetch", "run_counter_collection.csv")
+    sw = os.path.join(d, "pmc_step_write", "run_counter_collection.csv")
+    sm = os.path.join(d, "pmc_step_mfma", "run_counter_collection.csv")
+    if os.path.exists(sf) and os.path.exists(sw) and os.path.exists(sm):
+        # the post-rowpass chain per launch: HBM bytes (FETCH x2 + WRITE) against
+        # the algorithmic bytes, and matrix-core busy cycles (dW2 only has MFMA work)
+        H, mb, S, nwg = 256, 4096, 4, 128
+        tot = 2 * H * H + 2 * H * 20 + 6 * H + 12            # flat layout incl. pads (satrl_ppo_layout)
+        alg = {"Cijk": 2 * 2 * mb * H * 4 + 2 * S * H * H * 4,
+               "reduce_kernel": (2 * S * H * H + nwg * 2 * H * 20 + nwg * (6 * H + 12)) * 4 + tot * 4,
+               "adam_kernel": 4 * tot * 4 + 3 * tot * 4 + 2 * H * H * 4}
+        chain = {}
+        for sub in ("Cijk", "reduce_kernel", "adam_kernel"):
+            f_kb, nf = pmc_per_dispatch(sf, sub, "FETCH_SIZE")
+            w_kb, nw = pmc_per_dispatch(sw, sub, "WRITE_SIZE")
+            busy, nb = pmc_per_dispatch(sm, sub, "SQ_VALU_MFMA_BUSY_CYCLES")
+            grbm, ng = pmc_per_dispatch(sm, sub, "GRBM_GUI_ACTIVE")
+            hbm = (2 * f_kb + w_kb) * 1024.0 if f_kb is not None and w_kb is not None else None
+            chain[sub] = {"dispatches": [nf, nw, nb, ng], "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
+                          "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg[sub],
+                          "traffic_over_algorithmic": hbm / alg[sub] if hbm else None,
+                          "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
+                          "mfma_busy_frac_dispatch_window": busy / (grbm / 8.0 * 1024) if busy and grbm else None}
+        res = {"kernels": chain, "hidden": H, "minibatch": mb, "dw2_splits": S,
+               "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
+               "definition": "per-dispatch medians; Cijk = the hipBLASLt dW2 GEMM (1.07 GFLOP per launch); "
+                             "mfma_busy_frac as in the rowpass summary, over the --pmc dispatch window (a lower "
+                             "bound for short dispatches)",
+               "workload": "tools/step_workload.py (eager minibatch steps)"}
+        with open(os.path.join(prof, f"{tag}_chain_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
     pol = os.path.join(d, "pmc_policy_mfma", "run_counter_collection.csv")
     if os.path.exists(pol):
         # the rollout's policy kernel (both agents' forward, 16384 rows each): per row and
