@@ -39,18 +39,8 @@ __device__ unsigned long long g_probe[512][16][16][2];
 #define PHASE_PROBE(k) do {} while (0)
 #endif
 
-#ifndef SATRL_RP_ROWS
-#define SATRL_RP_ROWS 32
-#endif
-#ifndef SATRL_RP_NW256
-#define SATRL_RP_NW256 16
-#endif
-constexpr int kRows = SATRL_RP_ROWS;   // minibatch rows per rowpass workgroup (and per partial slab)
-constexpr int kNW256 = SATRL_RP_NW256; // waves per rowpass workgroup at H = 256
-// rowpass workgroups resident per CU the register allocation must allow (the
-// 8-wave 16-row dev variant runs two per CU)
-template <int R, int NW>
-constexpr int rp_wg_per_cu() { return R == 16 && NW == 8 ? 2 : 1; }
+constexpr int kRows = 32;     // minibatch rows per rowpass workgroup (and per partial slab)
+constexpr int kNW256 = 16;    // waves per rowpass workgroup at H = 256
 // short minibatches at H = 256 (configs[3]: 512 rows per rank; ragged tails)
 // run 16-row workgroups of the same 16 waves, one 16-row tile each: twice the
 // workgroups on the chip, and every row's arithmetic -- the forward's MFMA
@@ -110,33 +100,6 @@ __device__ __forceinline__ int net_of(const Layout& L, int64_t e, int H) {
 // ---------------------------------------------------------------------------
 using f4 = __attribute__((ext_vector_type(4))) float;
 
-// Write-through (sc1) stores for what the next launch of the chain reads: an
-// agent-scope relaxed atomic store is a plain global_store with sc1, so the
-// line goes on to memory as it is written instead of staying dirty in this
-// XCD's L2 until the end-of-kernel write-back (MI355X_MICROARCH.md
-// "boundary": + B / 6 TB/s behind B dirty bytes).  Bit mask: 1 rowpass H1 /
-// dZ2, 2 rowpass slabs, 4 reduce G, 8 Adam P/M/V/W2T.
-#ifndef SATRL_WT
-#define SATRL_WT 0
-#endif
-template <int BIT>
-__device__ __forceinline__ void st_out(float* p, float v) {
-  if constexpr ((SATRL_WT & BIT) != 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <int BIT>
-__device__ __forceinline__ void st_out4(float4* p, float4 v) {
-  if constexpr ((SATRL_WT & BIT) != 0) {
-    float* q = reinterpret_cast<float*>(p);
-    __hip_atomic_store(q, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
-
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -191,11 +154,7 @@ __device__ __forceinline__ void row16_sum_n(float (&v)[NV]) {
 // accurate exp and IEEE division take ~3x that.  Every MLP kernel (rollout
 // policy/value, update rowpass) calls this one function, so logp_old from the
 // rollout still equals the update's recomputation bit for bit.
-// SATRL_LIB_TANH (development A/B only) switches back to the library tanhf.
 __device__ __forceinline__ float tanh_f32(float x) {
-#ifdef SATRL_LIB_TANH
-  return tanhf(x);
-#else
   const float y = fabsf(x), z = x * x;
   float p = fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f);
   p = fmaf(p, z, -5.37397155531e-2f);
@@ -205,20 +164,15 @@ __device__ __forceinline__ float tanh_f32(float x) {
   const float e = __builtin_amdgcn_exp2f(y * 2.8853900817779268f);        // e^{2|x|}; inf -> rcp 0 -> 1
   const float big = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
   return y < 0.625f ? small : copysignf(big, x);                          // NaN -> big arm -> NaN
-#endif
 }
 
 // The k mapping of a 32-wide chunk (fc2 / dH1 phases): lane group g holds
-// k = 8g + 4h + e (SATRL_RP_KMAP 0: each lane's two float4 adjacent, so a
-// wave-instruction touches every 128-B row segment at a 32-B stride) or
-// k = 16h + 4g + e (1: each float4 instruction reads 64 contiguous bytes per
-// row).  The MFMA sequence groups k differently, so the two are different
-// f32 roundings of the same sums; rollout and update share the mapping.
-#ifndef SATRL_RP_KMAP
-#define SATRL_RP_KMAP 0
-#endif
-constexpr int kGOff = SATRL_RP_KMAP ? 4 : 8;    // floats between lane groups
-constexpr int kHOff = SATRL_RP_KMAP ? 16 : 4;   // floats between a lane's two float4
+// k = 8g + 4h + e, each lane's two float4 adjacent, so a wave-instruction
+// touches every 128-B row segment at a 32-B stride (k = 16h + 4g + e, 64
+// contiguous bytes per float4 instruction, measured no faster: EXPERIMENTS.md
+// round 3).  Rollout and update share the mapping, hence the f32 rounding.
+constexpr int kGOff = 8;   // floats between lane groups
+constexpr int kHOff = 4;   // floats between a lane's two float4
 
 template <int CT, int HOFF = kHOff>
 __device__ __forceinline__ void b_chunk(const float* __restrict__ bp, int LDB, float4 (&b)[CT][2]) {
@@ -285,34 +239,12 @@ __device__ __forceinline__ void mfma_regs(const float4 (&a)[RT][2], const float4
 // allow two 16-wave workgroups per CU; APRE: 59 -> 63 us per rollout step, B
 // two ahead alone: 64 us).  The MFMA sequence, hence every result bit, is the
 // same on every path.
-#ifndef SATRL_RP_BPD
-#define SATRL_RP_BPD 2
-#endif
-#ifndef SATRL_RP_EARLYB
-#define SATRL_RP_EARLYB 0   // measured: no gain, with __syncthreads (30.6 vs 30.6 us) or LDS-only barriers (r3)
-#endif
-#ifndef SATRL_RP_LATE_STORES
-// rowpass: issue the H1 (bit 1) / dZ2 (bit 2) global stores after the next
-// MFMA phase instead of before it (vmcnt counts loads and stores in issue
-// order, so a phase's waits for its weight chunks would otherwise also wait
-// for the stores issued ahead of them)
-#define SATRL_RP_LATE_STORES 0
-#endif
-#ifndef SATRL_RP_PRIO
-// rowpass: s_setprio 1 while a wave runs its phase-B (bit 1) / phase-D (bit 2)
-// MFMA stream, 0 after it, so the VALU tail of the waves that are done (fc2
-// tanh and output dots after B, phase E after D) issues only in the gaps of
-// the younger waves' MFMA streams instead of ahead of them (oldest first)
-#define SATRL_RP_PRIO 0
-#endif
-#ifndef SATRL_RP_EARLYD
-#define SATRL_RP_EARLYD 1   // 30.4 -> 29.8 us, in-graph 55.6 -> 54.7
-#endif
 // APRE path: B chunks kBPD ahead (kBPD + 1 register buffers; distance 2
 // measured best: 30.7 us per rowpass against 32.5 at 1, 31.0 at 3, 31.7 at 4).
 // The first kBPD chunks can be issued early, before the phase's barrier, into
-// a WPre (mfma_rows_pre), and handed to mfma_rows<..., PRE = true>.
-constexpr int kBPD = SATRL_RP_BPD;
+// a WPre (mfma_rows_pre), and handed to mfma_rows<..., PRE = true> (phase D:
+// 30.4 -> 29.8 us; the same for phase B measured no gain).
+constexpr int kBPD = 2;
 template <int CT>
 struct WPre {
   float4 bb[kBPD][CT][2];
@@ -326,9 +258,15 @@ __device__ __forceinline__ void mfma_rows_pre(const float* __restrict__ B, int n
   for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, pre.bb[c]);
 }
 
-template <int K, int LDA, int LDB, int RT, int CT, bool APRE, bool PRE = false>
+// no VALU filler (mfma_rows' fill(c) is called per chunk, APRE path only)
+struct NoFill {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <int K, int LDA, int LDB, int RT, int CT, bool APRE, bool PRE = false, class Fill = NoFill>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
-                                          f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr) {
+                                          f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr,
+                                          const Fill& fill = Fill{}) {
   constexpr int NC = K / 32;
   constexpr int BPD = kBPD < NC ? kBPD : NC;                     // prefetch distance in chunks
   static_assert(NC % 2 == 0, "chunk pairs");
@@ -337,69 +275,24 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   const float* ap = A + i * LDA + kGOff * g;
   const float* bp = B + (int64_t)(n0 + i) * LDB + kGOff * g;
   if constexpr (APRE) {
-#ifdef SATRL_RP_FAKE_LDS_B
-    // timing probe only (numerically wrong): the B operand read from LDS (the A
-    // image), i.e. the MFMA phases with a perfect on-chip weight feed
-    bp = A + i * LDA + kGOff * g;
-    constexpr int LDB_ = LDA;
-#else
-    constexpr int LDB_ = LDB;
-#endif
     // fully unrolled so every buffer index is static
     constexpr int NB = BPD + 1;
     float4 bb[NB][CT][2], aa[2][RT][2];
-#if defined(SATRL_RP_FAKE_FEED)
-    // timing probe only (numerically wrong): operands made in registers, no
-    // loads -- bit 1 the B (weight) operand, bit 2 the LDS A operand
-    auto fake4 = [&](int c) { const float v = 1e-3f * (float)(i + c); return make_float4(v, v, v, v); };
-#endif
-#ifdef SATRL_RP_FAKE_LDS_B
-    if constexpr (false) {
-#else
     if constexpr (PRE) {
-#endif
 #pragma unroll
       for (int c = 0; c < BPD; ++c)
 #pragma unroll
         for (int t = 0; t < CT; ++t) { bb[c][t][0] = pre->bb[c][t][0]; bb[c][t][1] = pre->bb[c][t][1]; }
     } else {
 #pragma unroll
-      for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB_, bb[c]);
+      for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
     }
-#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 1)
-#pragma unroll
-    for (int c = 0; c < BPD; ++c)
-#pragma unroll
-      for (int t = 0; t < CT; ++t) { bb[c][t][0] = fake4(c + t); bb[c][t][1] = fake4(c + t + 2); }
-#endif
-#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 2)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) { aa[0][rt][0] = fake4(rt); aa[0][rt][1] = fake4(rt + 1); }
-#else
     a_chunk<LDA, RT>(ap, aa[0]);
-#endif
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 1)
-      if (c + BPD < NC)
-#pragma unroll
-        for (int t = 0; t < CT; ++t) { bb[(c + BPD) % NB][t][0] = fake4(c + t); bb[(c + BPD) % NB][t][1] = fake4(c + t + 2); }
-#else
-      if (c + BPD < NC) b_chunk<CT>(bp + 32 * (c + BPD), LDB_, bb[(c + BPD) % NB]);
-#endif
-#if defined(SATRL_RP_FAKE_FEED) && (SATRL_RP_FAKE_FEED & 2)
-      if (c + 1 < NC)
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) { aa[(c + 1) % 2][rt][0] = fake4(c + rt); aa[(c + 1) % 2][rt][1] = fake4(c + rt + 3); }
-#else
+      if (c + BPD < NC) b_chunk<CT>(bp + 32 * (c + BPD), LDB, bb[(c + BPD) % NB]);
       if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
-#endif
-#ifdef SATRL_RP_CHUNK_SYNC
-      // timing variant: the workgroup's waves meet every SATRL_RP_CHUNK_SYNC
-      // chunks, so the waves of a SIMD interleave their MFMA streams instead of
-      // running them oldest first (each wave's prefetch then covers 4x longer)
-      if (c > 0 && c % SATRL_RP_CHUNK_SYNC == 0) __builtin_amdgcn_s_barrier();
-#endif
+      fill(c);                                   // the caller's VALU work for this chunk's MFMA gaps
       mfma_regs<RT, CT>(aa[c % 2], bb[c % NB], acc);
     }
   } else {
@@ -432,7 +325,7 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
 #pragma unroll
       for (int t = 0; t < CT; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) st_out<1>(&out[(int64_t)(16 * rt + 4 * lg + j) * ld + n0 + 16 * t + li], v[rt][t][j]);
+        for (int j = 0; j < 4; ++j) out[(int64_t)(16 * rt + 4 * lg + j) * ld + n0 + 16 * t + li] = v[rt][t][j];
   } else {
 #pragma unroll
     for (int rt = 0; rt < R / 16; ++rt)
@@ -441,29 +334,15 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 16 * rt + 4 * lg + j;
-          if (r < nvalid) st_out<1>(&out[(int64_t)r * ld + n0 + 16 * t + li], v[rt][t][j]);
+          if (r < nvalid) out[(int64_t)r * ld + n0 + 16 * t + li] = v[rt][t][j];
         }
   }
 }
 
-// Workgroup barrier of the MLP kernels' phases.  With SATRL_RP_LDSBAR (a dev
-// A/B knob, off) it orders only LDS (fence workgroup/"local" + s_barrier):
-// __syncthreads() also drains every outstanding global access, so the H1 /
-// dZ2 / slab stores and the weight chunks a phase issues early for the next
-// one (phase B's first W2 chunks, phase D's first W2T chunks) would be waited
-// for at every barrier instead of staying in flight across it.
-#ifndef SATRL_RP_LDSBAR
-#define SATRL_RP_LDSBAR 0   // r3: LDS-only barriers, alone and with SATRL_RP_EARLYB: no gain
-#endif
-__device__ __forceinline__ void rp_barrier() {
-#if SATRL_RP_LDSBAR
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#else
-  __syncthreads();
-#endif
-}
+// Workgroup barrier of the MLP kernels' phases (__syncthreads: LDS-only
+// barriers that leave the global stores and early weight chunks in flight
+// measured no faster, EXPERIMENTS.md round 3).
+__device__ __forceinline__ void rp_barrier() { __syncthreads(); }
 
 // Shared-memory block and forward pass (phases A, B and the output-layer dot
 // products of C) common to rowpass_kernel and policy_kernel, so the rollout's
@@ -507,17 +386,12 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
       const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
       bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
       bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-#ifdef SATRL_RP_FAKE_GATHER
-      (void)bp;                                  // timing probe only: no W1 loads
-      bw1[t][0] = make_float4(0.01f, 0.02f, 0.f, 0.f);
-#else
       if (lg < 2) {
         bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
         bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
       } else if (lg == 2) {
         bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
       }
-#endif
     }
   }
   gather(tid, NT);
@@ -545,11 +419,6 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
   mfma_chunk<LDS_S, RT, CT, 4>(&sm.S[li][8 * lg], bw1, acc);
-  // phase B's first W2 chunks go out now: their latency overlaps the fc1 tanh,
-  // the H1 stores and the barrier
-  constexpr bool EB = APRE && SATRL_RP_EARLYB;
-  WPre<CT> preB;
-  if constexpr (EB) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   PHASE_PROBE(10);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -565,19 +434,13 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
       }
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
-  if (!(SATRL_RP_LATE_STORES & 1) && h1out != nullptr)
-    store_rows<R, CT>(h1out, H, n0, nvalid, h1);                       // straight-line unless ragged
+  if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
   PHASE_PROBE(11);
   rp_barrier();
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  if constexpr (APRE && (SATRL_RP_PRIO & 1)) __builtin_amdgcn_s_setprio(1);
-  mfma_rows<H, LDA, H, RT, CT, APRE, EB>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
-  if constexpr (APRE && (SATRL_RP_PRIO & 1)) __builtin_amdgcn_s_setprio(0);
-  // (late: behind phase B's weight loads, so none of B's in-order vmcnt
-  // waits also waits for these stores to complete)
-  if ((SATRL_RP_LATE_STORES & 1) && h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);
+  mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -642,7 +505,7 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
 }
 
 template <int H, int NW, int R = kRows>
-__global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 256)) rowpass_kernel(int mb, const float* __restrict__ src,
+__global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const float* __restrict__ W2T, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
@@ -685,11 +548,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   auto gather = [&](int t0, int nt) {
     for (int q = t0; q < R * 26; q += nt) {
       const int r = q / 26, c = q % 26, row = r0 + r;
-#ifdef SATRL_RP_FAKE_GATHER
-      const float v = row < mb ? 0.001f * (float)(c + r) : 0.0f;   // timing probe only: no row loads
-#else
       const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
-#endif
       if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
     }
     if (t0 < 3) {
@@ -703,7 +562,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
-  if constexpr (SATRL_RP_EARLYD) mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
+  mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -818,18 +677,18 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
 #pragma unroll
       for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
       if (lg == 0) {
-        st_out<2>(&tp[net * H + n], cb2);                          // db2
+        tp[net * H + n] = cb2;                          // db2
         if constexpr (ACT) {                                       // dW3a
-          st_out<2>(&tp[2 * H + n], cw[0]); st_out<2>(&tp[3 * H + n], cw[1]); st_out<2>(&tp[4 * H + n], cw[2]);
+          tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2];
         } else {
-          st_out<2>(&tp[5 * H + 8 + n], cw[0]);                    // dW3c
+          tp[5 * H + 8 + n] = cw[0];                    // dW3c
         }
       }
     }
   };
   if (net == 0) tail(std::true_type{});
   else tail(std::false_type{});
-  if (!(SATRL_RP_LATE_STORES & 2)) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
+  store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   rp_barrier();
   PHASE_PROBE(5);
 
@@ -838,10 +697,7 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  if constexpr ((SATRL_RP_PRIO & 2) != 0) __builtin_amdgcn_s_setprio(1);
-  mfma_rows<H, LDA, H, RT, CT, true, SATRL_RP_EARLYD>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
-  if constexpr ((SATRL_RP_PRIO & 2) != 0) __builtin_amdgcn_s_setprio(0);
-  if (SATRL_RP_LATE_STORES & 2) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
+  mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
@@ -865,325 +721,11 @@ __global__ void __launch_bounds__(NW * 64, (rp_wg_per_cu<R, NW>() * NW * 64 / 25
       const int kp = 16 * hb + li;
       if (kp < 20) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) st_out<2>(&pw[(int64_t)(n0 + 16 * t + 4 * lg + j) * 20 + kp], d[j]);
-      }
-    }
-  }
-  PHASE_PROBE(7);
-}
-
-// ---------------------------------------------------------------------------
-// rowpass_dual: the same row-parallel step with ONE workgroup per 16-row block
-// and BOTH nets (H = 256): waves 0-7 the actor, 8-15 the critic, each wave
-// one 16-row tile x two 16-column tiles of its net.  The two nets share only
-// the gathered rows, so after one workgroup barrier each net runs its phases
-// on its own 8-wave barrier (an LDS counter), and the matrix pipe of every
-// SIMD (two actor + two critic waves) is shared by whichever net is in an
-// MFMA phase: the non-MFMA phases of one net (fc1 tanh, the output layer, the
-// loss head, the tail partials, dZ1/[dW1|db1]) run beside the other net's
-// fc2 / dH1 MFMA streams instead of leaving the pipe idle, as they do when a
-// workgroup owns one net.  Every row's arithmetic is that of rowpass_kernel
-// <256, 16, 16> (the forward's MFMA order, the output-layer sums as sixteen
-// 16-column partials in column order, the head, the tail and [dW1|db1] sums
-// over the block's rows): the outputs are bitwise those of the 16-row
-// kernel, so logp still equals the rollout's bit for bit.
-// ---------------------------------------------------------------------------
-#ifndef SATRL_RP_DUAL_PRIO
-#define SATRL_RP_DUAL_PRIO 0   // s_setprio for waves in their MFMA phases (dev A/B)
-#endif
-#ifndef SATRL_RP_DUAL_TOKEN
-#define SATRL_RP_DUAL_TOKEN 0  // MFMA phases strictly alternate B_a, B_c, D_a, D_c (dev A/B)
-#endif
-
-// wait (bounded) until the counter reaches target, without arriving
-__device__ __forceinline__ void net_wait(const unsigned* cnt, unsigned target) {
-  for (int it = 0; it < (1 << 22); ++it) {
-    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// one net's 8 waves meet: each wave's lane 0 adds 1 to the net's LDS counter
-// after its LDS writes, then the wave waits for `target` arrivals (a bounded
-// spin: a lost arrival ends the wait instead of hanging the workgroup)
-__device__ __forceinline__ void net_sync(unsigned* cnt, unsigned target) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (int it = 0; it < (1 << 22); ++it) {
-    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <int H>
-__global__ void __launch_bounds__(1024, 1) rowpass_dual_kernel(int mb, const float* __restrict__ src,
-                                                               const int64_t* __restrict__ idx,
-                                                               const float* __restrict__ P,
-                                                               const float* __restrict__ W2T, float epsilon,
-                                                               float ent_coef, float max_action,
-                                                               float* __restrict__ H1g, float* __restrict__ dZ2g,
-                                                               float* __restrict__ ptail, float* __restrict__ pw1) {
-  constexpr int R = 16, NWN = 8, CT = H / 16 / NWN, LDA = H + 4, LDS_S = 36, NT = 1024;
-  static_assert(CT == 2, "two 16-column tiles per wave");
-  const Layout L = layout(H);
-  __shared__ __attribute__((aligned(16))) float S[R][LDS_S];     // [s(18) | 1 | 0...] per row
-  __shared__ float ax[R][8];                                     // a, logp_old, adv, v_target
-  __shared__ __attribute__((aligned(16))) float hs[2][R][LDA];   // per net: tanh(fc1), then dZ2
-  __shared__ float osum[2][2 * NWN][R][3];                       // per net: 16-column output-layer partials
-  __shared__ float dz3s[2][R][4];
-  __shared__ float hcs[3][3];
-  __shared__ unsigned nbar[2];
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
-  const int net = w >> 3, wn = w & 7, n0 = wn * (H / NWN);
-  const int rb = blockIdx.x, r0 = rb * R, nvalid = mb - r0;
-  unsigned* bar = &nbar[net];
-  unsigned gen = 0;
-
-  // ---- gather (shared by both nets), this wave's W1aug rows ---------------------
-  float4 bw1[CT][2];
-  {
-    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
-      bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
-      bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lg < 2) {
-        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
-        bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
-      } else if (lg == 2) {
-        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
-      }
-    }
-  }
-  float hb3[3], hls[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) { hb3[d] = P[L.b3a + d]; hls[d] = P[L.ls + d]; }
-  const float hb3c = P[L.b3c];
-  for (int q = tid; q < R * 26; q += NT) {
-    const int r = q / 26, c = q % 26, row = r0 + r;
-    const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
-    if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;
-  }
-  for (int q = tid; q < R * (LDS_S - 18); q += NT) {
-    const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
-    S[r][c] = (c == 18 && r < nvalid) ? 1.0f : 0.0f;
-  }
-  if (tid < 3) {
-    const float ls = tid == 0 ? hls[0] : (tid == 1 ? hls[1] : hls[2]);
-    const float sd = expf(ls), var = sd * sd;
-    hcs[0][tid] = var;
-    hcs[1][tid] = logf(sd);
-    hcs[2][tid] = 1.0f / var;
-  }
-  if (tid < 2) nbar[tid] = 0u;
-  float b2v[CT], w3[CT][3];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int n = n0 + 16 * t + li;
-    b2v[t] = P[L.b2 + net * H + n];
-    if (net == 0) {
-      w3[t][0] = P[L.W3a + n]; w3[t][1] = P[L.W3a + H + n]; w3[t][2] = P[L.W3a + 2 * H + n];
-    } else {
-      w3[t][0] = P[L.W3c + n]; w3[t][1] = 0.0f; w3[t][2] = 0.0f;
-    }
-  }
-  __syncthreads();                                               // the only workgroup-wide barrier
-
-  // ---- A: fc1 on MFMA, tanh -> registers, LDS, H1 (HBM) --------------------------
-  f4 acc[1][CT];
-  float h1[1][CT][4];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_chunk<LDS_S, 1, CT, 4>(&S[li][8 * lg], bw1, acc);
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int n = n0 + 16 * t + li;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float h = tanh_f32(acc[0][t][j]);
-      h1[0][t][j] = h;
-      hs[net][4 * lg + j][n] = h;
-    }
-    acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-  }
-  store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, nvalid, h1);
-  net_sync(bar, gen += NWN);
-
-  // ---- B: Z2 = H1 W2^T ------------------------------------------------------------
-  if (SATRL_RP_DUAL_TOKEN && net == 1) net_wait(&nbar[0], 2 * NWN);   // after the actor's B
-  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(1);
-  mfma_rows<H, LDA, H, 1, CT, true>(&hs[net][0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
-  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(0);
-
-  // ---- C (forward): tanh(fc2), output-layer partials per 16-column tile ------------
-  {
-    float ps[3 * CT * 4];
-#pragma unroll
-    for (int k = 0; k < 3 * CT * 4; ++k) ps[k] = 0.0f;
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float h = tanh_f32(acc[0][t][j] + b2v[t]);
-        acc[0][t][j] = h;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) ps[(q * CT + t) * 4 + j] = fmaf(h, w3[t][q], 0.0f);
-      }
-    if (net == 0) {
-      row16_sum_n<3 * CT * 4>(ps);
-    } else {
-      float p0[CT * 4];
-#pragma unroll
-      for (int k = 0; k < CT * 4; ++k) p0[k] = ps[k];
-      row16_sum_n<CT * 4>(p0);
-#pragma unroll
-      for (int k = 0; k < CT * 4; ++k) ps[k] = p0[k];
-    }
-    if (li == 0) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        if (q >= (net == 0 ? 3 : 1)) break;
-#pragma unroll
-        for (int t = 0; t < CT; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) osum[net][CT * wn + t][4 * lg + j][q] = ps[(q * CT + t) * 4 + j];
-      }
-    }
-  }
-  net_sync(bar, gen += NWN);
-
-  // ---- C: the net's loss head (16 lanes of the net's first wave) -----------------
-  if (wn == 0 && l < R) {
-    const int r = l, row = r0 + r;
-    float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
-    if (row < mb) {
-      const float inv = 1.0f / (float)mb;
-      if (net == 0) {
-        float th[3], mu[3], dv[3], var[3], logp[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          th[d] = tanh_f32(out_sum<2 * NWN, R>(osum[0], r, d) + hb3[d]);
-          mu[d] = max_action * th[d];
-          var[d] = hcs[0][d];
-          dv[d] = ax[r][d] - mu[d];
-          logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - hcs[1][d]) - kLogSqrt2Pi;
-        }
-        const float lsum = (logp[0] + logp[1]) + logp[2];
-        const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
-        const float ratio = expf(lsum - lold);
-        const float adv = ax[r][6];
-        const float s1 = ratio * adv;
-        const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
-        const float s2 = cr * adv;
-        const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-        const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
-        const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
-        const float dmin = -inv;
-        const float dratio = dmin * g1 * adv + dmin * g2 * adv * inside;
-        const float dlsum = dratio * ratio;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const float dvv = dv[d] * hcs[2][d];
-          const float dmu = dlsum * dvv;
-          dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
-          dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
-        }
-      } else {
-        const float vc = out_sum<2 * NWN, R>(osum[1], r, 0) + hb3c;
-        dz[3] = 2.0f * inv * (vc - ax[r][7]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dz3s[net][r][q] = dz[q];
-    float* tp = ptail + (int64_t)rb * L.tail;
-    float red[7] = {dz[0], dz[1], dz[2], dls[0], dls[1], dls[2], dz[3]};
-    row16_sum_n<7>(red);
-    if (r == 0) {
-      if (net == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          tp[5 * H + q] = red[q];
-          tp[5 * H + 4 + q] = red[3 + q];
-        }
-        tp[5 * H + 3] = 0.0f;
-        tp[5 * H + 7] = 0.0f;
-      } else {
-        tp[6 * H + 8] = red[6];
-        tp[6 * H + 9] = 0.0f; tp[6 * H + 10] = 0.0f; tp[6 * H + 11] = 0.0f;
-      }
-    }
-  }
-  net_sync(bar, gen += NWN);
-
-  // ---- C: dZ2 (LDS over this net's tanh(fc1) image, HBM), db2 / dW3 partials --------
-  {
-    float* tp = ptail + (int64_t)rb * L.tail;
-    float d2v[1][CT][4];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int n = n0 + 16 * t + li;
-      float cb2 = 0.f, cw[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * lg + j;
-        const float h = acc[0][t][j];
-        float dh;
-        if (net == 0) dh = (dz3s[0][r][0] * w3[t][0] + dz3s[0][r][1] * w3[t][1]) + dz3s[0][r][2] * w3[t][2];
-        else dh = dz3s[1][r][3] * w3[t][0];
-        const float d2 = dh * (1.0f - h * h);
-        hs[net][r][n] = d2;
-        d2v[0][t][j] = d2;
-        cb2 += d2;
-        if (net == 0) {
-          cw[0] = fmaf(dz3s[0][r][0], h, cw[0]); cw[1] = fmaf(dz3s[0][r][1], h, cw[1]);
-          cw[2] = fmaf(dz3s[0][r][2], h, cw[2]);
-        } else {
-          cw[0] = fmaf(dz3s[1][r][3], h, cw[0]);
-        }
-      }
-      cb2 = xor32_sum(xor16_sum(cb2));
-      cw[0] = xor32_sum(xor16_sum(cw[0]));
-      if (net == 0) { cw[1] = xor32_sum(xor16_sum(cw[1])); cw[2] = xor32_sum(xor16_sum(cw[2])); }
-      if (lg == 0) {
-        tp[net * H + n] = cb2;
-        if (net == 0) { tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2]; }
-        else tp[5 * H + 8 + n] = cw[0];
-      }
-    }
-    store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, nvalid, d2v);
-  }
-  net_sync(bar, gen += NWN);
-
-  // ---- D: dH1 = dZ2 W2 ---------------------------------------------------------------
-#pragma unroll
-  for (int t = 0; t < CT; ++t) acc[0][t] = f4{0.f, 0.f, 0.f, 0.f};
-  if (SATRL_RP_DUAL_TOKEN) net_wait(&nbar[1 - net], net == 0 ? 2 * NWN : 5 * NWN);   // after the other's B / D
-  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(1);
-  mfma_rows<H, LDA, H, 1, CT, true>(&hs[net][0][0], W2T + (int64_t)net * H * H, n0, acc);
-  if (SATRL_RP_DUAL_PRIO) __builtin_amdgcn_s_setprio(0);
-  if (SATRL_RP_DUAL_TOKEN && net == 0 && (threadIdx.x & 63) == 0)                   // the actor's D is done
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-
-  // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1] = dZ1^T [S | 1] ----------------------------
-  float* pw = pw1 + (int64_t)rb * 2 * H * 20 + (int64_t)net * H * 20;
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[0][t][j] = acc[0][t][j] * (1.0f - h1[0][t][j] * h1[0][t][j]);
-#pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
-      f4 d = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[0][t][kk], S[4 * lg + kk][16 * hb + li], d);
-      const int kp = 16 * hb + li;
-      if (kp < 20) {
-#pragma unroll
         for (int j = 0; j < 4; ++j) pw[(int64_t)(n0 + 16 * t + 4 * lg + j) * 20 + kp] = d[j];
       }
     }
   }
+  PHASE_PROBE(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -1198,14 +740,8 @@ __global__ void __launch_bounds__(1024, 1) rowpass_dual_kernel(int mb, const flo
 // rows per policy/value workgroup (64-row tiles measured 62 vs 58.5 us per
 // rollout step at 16k envs: fewer, larger workgroups lose more to the tail
 // than the halved weight ingest saves)
-#ifndef SATRL_POL_ROWS
-#define SATRL_POL_ROWS 32
-#endif
-#ifndef SATRL_POL_NW256
-#define SATRL_POL_NW256 16
-#endif
-constexpr int kPolRows = SATRL_POL_ROWS;   // rows per policy workgroup
-constexpr int kPolNW = SATRL_POL_NW256;    // waves per policy workgroup at H = 256
+constexpr int kPolRows = 32;   // rows per policy workgroup
+constexpr int kPolNW = 16;     // waves per policy workgroup at H = 256
 
 template <int H, int NW, int MODE>
 __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float* __restrict__ obs,
@@ -1264,10 +800,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
 // b -> split b % S: with S = 8 every split's 16 tiles share one XCD's L2.
 // Every sum has a fixed order.
 // ---------------------------------------------------------------------------
-#ifndef SATRL_DW2_DEPTH
-#define SATRL_DW2_DEPTH 4
-#endif
-constexpr int kDwKC = 32, kDwD = SATRL_DW2_DEPTH;
+constexpr int kDwKC = 32, kDwD = 4;   // rows per chunk, ring slots (4/6/8 slots measured alike)
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 template <int H>
@@ -1353,13 +886,7 @@ int dw2_splits(int H, int mb, int net) {
 // latency rounds), then chunk 0 adds the CH partials in order.
 // ---------------------------------------------------------------------------
 struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
-#ifndef SATRL_RED_CH1
-#define SATRL_RED_CH1 8
-#endif
-#ifndef SATRL_RED_CHT
-#define SATRL_RED_CHT 32
-#endif
-constexpr int kRedCH1 = SATRL_RED_CH1, kRedCHt = SATRL_RED_CHT, kRedCH2 = 4;
+constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;   // chunks per column: W1, tail, W2 regions
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -1448,7 +975,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCH1>(reinterpret_cast<const float4*>(p1), n4, g.nw1, col, valid, red);
-      if (lead && valid) st_out4<4>(&G4[L.W1 / 4 + col], v);
+      if (lead && valid) G4[L.W1 / 4 + col] = v;
     } else if (lead && valid) {
       v = G4[L.W1 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.W1 / 4 + col] = v; }
@@ -1467,7 +994,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCHt>(reinterpret_cast<const float4*>(pt), n4, g.nwg, col, valid, red);
-      if (lead && valid) st_out4<4>(&G4[L.b2 / 4 + col], v);
+      if (lead && valid) G4[L.b2 / 4 + col] = v;
     } else if (lead && valid) {
       v = G4[L.b2 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.b2 / 4 + col] = v; }
@@ -1502,7 +1029,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
     if (mode & 1) {
       v = chunk_sum4<kRedCH2>(reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4, HH4, g.S,
                               col - net * HH4, valid, red);
-      if (lead && valid) st_out4<4>(&G4[col], v);
+      if (lead && valid) G4[col] = v;
     } else if (lead && valid) {
       v = G4[col];
       if (world > 1) { v = f4div(v, (float)world); G4[col] = v; }
@@ -1533,9 +1060,6 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
 // float4 per thread, and the updated tile goes out transposed through LDS
 // into W2T (coalesced).  Blocks [nbw, ...): the rest of the layout, float4.
 // ---------------------------------------------------------------------------
-#ifndef SATRL_ADAM_EARLY
-#define SATRL_ADAM_EARLY 1
-#endif
 __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float step_size,
                                            float bc2s, float w1, float w2, float beta2, float eps, int use_clip) {
   if (use_clip) g = g * coef;                                      // grads.mul_(clip_coef_clamped)
@@ -1572,7 +1096,6 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
     net = live ? net_of(L, e4 * 4, H) : 0;
     live = live && (net_sel < 0 || net == net_sel);
   }
-#if SATRL_ADAM_EARLY
   // the norm partials' loads go out first, this thread's G/M/V/P right
   // behind them: the fold below waits only for the partials (vmcnt is in
   // order), so the operand latency overlaps the fold
@@ -1601,10 +1124,6 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   if (nblk > 1024) {                                               // (not at the sizes in use)
     for (int k = t + 1024; k < nblk; k += 256) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
   }
-#else
-  double a = 0.0, c = 0.0;
-  for (int k = t; k < nblk; k += blockDim.x) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
-#endif
   block_sum2(a, c, sh);
   // every thread folds the same partials in the same order, so each derives
   // its own net's constants (no second barrier)
@@ -1624,23 +1143,14 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
   if (!live) return;                                               // (W1.. tail blocks only: no barrier follows)
-#if !SATRL_ADAM_EARLY
-  const float4* G4 = reinterpret_cast<const float4*>(G);
-  float4* P4 = reinterpret_cast<float4*>(P);
-  float4* M4 = reinterpret_cast<float4*>(M);
-  float4* V4 = reinterpret_cast<float4*>(V);
-  const float4 g = G4[e4];
-  float4 m = M4[e4], v = V4[e4];
-  const float4 p = P4[e4];
-#endif
   float4 pn;
   pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.z = adam_elem(g.z, m.z, v.z, p.z, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.w = adam_elem(g.w, m.w, v.w, p.w, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  st_out4<8>(&P4[e4], pn);
-  st_out4<8>(&M4[e4], m);
-  st_out4<8>(&V4[e4], v);
+  P4[e4] = pn;
+  M4[e4] = m;
+  V4[e4] = v;
   if ((int)blockIdx.x < nbw && W2T != nullptr) {                   // keep fc2.weight^T for the dH1 MFMA
     const int nl = t >> 3, kl = (t & 7) * 4;
     tile[nl][kl] = pn.x; tile[nl][kl + 1] = pn.y; tile[nl][kl + 2] = pn.z; tile[nl][kl + 3] = pn.w;
@@ -1649,7 +1159,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
     const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
     // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
     const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
-    st_out4<8>(&reinterpret_cast<float4*>(W2T)[((int64_t)net * H * H + (int64_t)(k0 + nl) * H + n0 + kl) / 4], o);
+    reinterpret_cast<float4*>(W2T)[((int64_t)net * H * H + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
   }
 }
 
@@ -1682,16 +1192,7 @@ int short_mb() {
   }();
   return v;
 }
-// the dual-net rowpass at H = 256 (SATRL_RP_DUAL=1): 16-row blocks at every mb
-bool dual_rowpass() {
-  static const bool v = [] {
-    const char* e = std::getenv("SATRL_RP_DUAL");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
 int rows_per_wg(int H, int mb) {
-  if (H == 256 && dual_rowpass()) return kRowsShort;
   return (H == 256 && kRows == 32 && mb <= short_mb()) ? kRowsShort : kRows;
 }
 int n_head_wg(int H, int mb) {
@@ -1702,7 +1203,6 @@ int n_w1_wg(int H, int mb) { return n_head_wg(H, mb); }
 // slab capacity a minibatch of mb rows needs, and any shorter one (a ragged
 // tail of a minibatch above the short threshold can have more row blocks)
 int n_head_wg_cap(int H, int mb) {
-  if (H == 256 && dual_rowpass()) return n_head_wg(H, mb);
   const int m = mb < short_mb() ? mb : short_mb();
   const int a = n_head_wg(H, mb), b = m > 0 ? n_head_wg(H, m) : 0;
   return a > b ? a : b;
@@ -1775,10 +1275,7 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
                        max_action, H1, dZ2, ptail, pw1, net);
-  else if (net < 0 && dual_rowpass())
-    hipLaunchKernelGGL((rowpass_dual_kernel<256>), dim3(n_head_wg(H, mb)), dim3(1024), 0, s, mb, src, idx, P, W2T,
-                       epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1);
-  else if (R == kRowsShort && kRows != kRowsShort)
+  else if (R == kRowsShort)
     hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, mb, src, idx, P, W2T, epsilon,
                        ent_coef, max_action, H1, dZ2, ptail, pw1, net);
   else

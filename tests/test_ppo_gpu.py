@@ -588,66 +588,3 @@ def test_dw2_lib_vs_fp64_and_deterministic(mb, S, net):
             continue
         err = (outs[0][n].double() - ref[n]).abs().max().item()
         assert err <= 1e-5 * ref[n].abs().max().item() + 1e-4, err
-
-
-def _dual_vs_single(mb, q):
-    """(in a fresh process with SATRL_RP_DUAL=1) the dual-net rowpass (net -1)
-    and the 16-row single-net kernel (net 0, then net 1) on the same rows."""
-    import os
-    os.environ["SATRL_RP_DUAL"] = "1"
-    import sys
-    from conftest import PKG_DIR
-    sys.path.insert(0, PKG_DIR)
-    from satrl.ppo import FusedMinibatch, PPOLearner
-    from satrl.trainer import args_param
-    torch.cuda.set_device(0)
-    torch.manual_seed(11)
-    args = args_param(hidden_width=256, mini_batch_size=mb, batch_size=8192, chkpt_dir="/tmp")
-    args.state_dim, args.action_dim, args.max_action = 18, 3, 1.6
-    L = PPOLearner(args, "pursuer", device="cuda:0", use_graph=False)
-    with torch.no_grad():
-        for p in list(L.actor.parameters()) + list(L.critic.parameters()):
-            p.add_(torch.randn_like(p) * 0.05)
-    L.sync_w2t()
-    g = torch.Generator(device="cuda:0").manual_seed(1)
-    B = 8192
-    src = torch.zeros((B, 32), device="cuda:0")
-    src[:, 0:18] = torch.randn((B, 18), device="cuda:0", generator=g)
-    src[:, 18:21] = torch.rand((B, 3), device="cuda:0", generator=g) * 3.2 - 1.6
-    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda:0", generator=g)
-    src[:, 24] = torch.randn(B, device="cuda:0", generator=g)
-    src[:, 25] = torch.randn(B, device="cuda:0", generator=g) * 5
-    idx = torch.randperm(B, device="cuda:0", generator=g)[:mb]
-    st = FusedMinibatch(L, mb, 1, use_graph=False)
-    outs = []
-    for nets in ((-1,), (0, 1)):
-        for b in (st.H1, st.dZ2, st.ptail, st.pw1):
-            b.fill_(float("nan"))
-        for net in nets:
-            st.rowpass(src, idx, net=net)
-        torch.cuda.synchronize()
-        n = 2 * mb * 256
-        nblk = (mb + 15) // 16
-        outs.append([st.H1[:n].cpu(), st.dZ2[:n].cpu(), st.ptail[:nblk * (6 * 256 + 12)].cpu(),
-                     st.pw1[:nblk * 2 * 256 * 20].cpu()])
-    q.put([(torch.equal(a, b) or torch.equal(torch.nan_to_num(a, 7.0), torch.nan_to_num(b, 7.0)),
-            bool(torch.isfinite(a[:a.numel()]).any())) for a, b in zip(*outs)])
-
-
-@pytest.mark.parametrize("mb", [4096, 512, 777])
-def test_dual_rowpass_bitwise_equals_16row_kernel(mb):
-    """rowpass_dual_kernel (one workgroup per 16-row block and both nets,
-    each net on its own 8-wave LDS barrier) writes H1, dZ2 and every partial
-    slab bit for bit as the 16-row single-net kernel run once per net -- so
-    logp_old still equals the rollout's recomputation bit for bit; 777 has a
-    ragged last block."""
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_dual_vs_single, args=(mb, q))
-    p.start()
-    res = q.get(timeout=300)
-    p.join(timeout=60)
-    assert p.exitcode == 0
-    assert all(eq for eq, _ in res), res
-    assert all(fin for _, fin in res)

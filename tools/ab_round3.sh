@@ -2,8 +2,9 @@
 # Round-3 A/B measurements of the rowpass / update chain, in
 # two halves: `build` here (hipcc cross-compiles the dev variants into
 # tools/_probe/, they travel with the tree), `run` on the GPU box (gpurun).
-# Every variant is a dev build of the same sources with extra defines; none is
-# the product.  Timing tools: rowpass_ab.py (rowpass alone, back to back),
+# Every variant is a dev build of round 3's ppo_kernels.hip (git ca3c6c3, where
+# the timing-only knobs below still live; the product source dropped them in
+# round 4) with extra defines; none is the product.  Timing tools: rowpass_ab.py (rowpass alone, back to back),
 # minibatch_time.py (in-graph step), phase_probe.py (per-wave stamps).
 #
 #   bash tools/ab_round3.sh build
@@ -26,8 +27,11 @@ VARIANTS=(
 )
 case "${1:-}" in
   build)
+    mkdir -p tools/_probe/r3
+    git show ca3c6c3:ppo-rl-satellite_amd/csrc/ppo_kernels.hip > tools/_probe/r3/ppo_kernels.hip
     for v in "${VARIANTS[@]}"; do
-      make -s -C ppo-rl-satellite_amd/csrc variant VNAME="${v%%:*}" VDEFS="${v#*:}"
+      make -s -C ppo-rl-satellite_amd/csrc variant VNAME="${v%%:*}" VSRC=../../tools/_probe/r3/ppo_kernels.hip \
+          VDEFS="${v#*:}"
     done
     make -s -C ppo-rl-satellite_amd/csrc probe
     ;;

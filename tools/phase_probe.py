@@ -35,7 +35,9 @@ if os.environ.get("SATRL_BLAS"):                       # dev A/B: torch's BLAS b
     print("blas:", torch.backends.cuda.preferred_blas_library())
 from satrl.trainer import args_param  # noqa: E402
 
-H, mb = 256, 4096
+H, mb = int(os.environ.get("PROBE_H", "256")), int(os.environ.get("PROBE_MB", "4096"))
+NWV = H // 16                                   # waves per rowpass workgroup
+print("H", H, "mb", mb)
 a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=16 * mb, chkpt_dir="/tmp")
 L = PPOLearner(a, "pursuer", use_graph=False)
 L.sync_w2t()
@@ -54,10 +56,10 @@ if probe:
     assert lib.satrl_probe_read(buf.ctypes.data) == 0
     b = buf.astype(np.int64)                     # [wg][stamp][wave][realtime, shader clock]
     order = [0, 8, 9, 10, 11, 1, 2, 3, 12, 13, 14, 4, 5, 6, 7]   # 12-14: inside the loss head (wave 0)
-    b = b[:2 * (mb // 32)]                       # the launched workgroups only
+    b = b[:2 * (mb // 32), :, :NWV]               # the launched workgroups and waves only
     t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
     print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
-          "(median over workgroups), waves 0..15; actor rows then critic rows")
+          "(median over workgroups), waves 0..%d; actor rows then critic rows" % (NWV - 1))
     for net, sl in (("actor", slice(0, None, 2)), ("critic", slice(1, None, 2))):
         print(f"  {net}")
         for k in order:
@@ -70,7 +72,7 @@ if probe:
             ck0 = b[wg, 0, :, 1].min()
             for k in order:
                 print(f"   {k:2d}: " + "  ".join(f"{int(b[wg, k, w_, 0] - rt0):6d}/{int(b[wg, k, w_, 1] - ck0):7d}"
-                                             for w_ in (0, 4, 8, 15)))
+                                             for w_ in sorted({0, NWV // 4, NWV // 2, NWV - 1})))
     nwg = 2 * (mb // 32)
     ws0 = b[:nwg, 0, :, 0].min(axis=1)
     en = b[:nwg, 7, :, 0].max(axis=1)

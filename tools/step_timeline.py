@@ -18,7 +18,7 @@ def run():
     sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
     from satrl.ppo import PPOLearner
     from satrl.trainer import args_param
-    H, mb = 256, 4096
+    H, mb = int(os.environ.get("PROBE_H", "256")), int(os.environ.get("PROBE_MB", "4096"))
     a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=16 * mb, chkpt_dir="/tmp")
     L = PPOLearner(a, "pursuer")
     L.sync_w2t()
