@@ -464,14 +464,15 @@ def run(a, world):
     t_rest = timed_run(a.kernel_iters, lambda k: st.step(stage, None, skip_rowpass=True), 40.0)
     rowpass_us = t_chain - t_rest
     rowpass_ev_us, rowpass_med = timed_pairs(a.kernel_iters, lambda k, ev: st.step(stage, None, events=ev), 60.0)
-    rowpass_flop = st.rowpass_flops(a.hidden, mb_local)
+    rowpass_flop = st.step_kernel_flops(mb_local)        # + the fused dW2 product at H = 64
     rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
     # warm-L2 figure: back-to-back rowpass launches alone (W2/W2T stay in L2)
+    rp_launch = st.rowpass_dw2 if st.fused_dw2 else st.rowpass
     for _ in range(10):
-        st.rowpass(stage, None)
+        rp_launch(stage, None)
     e0.record()
     for _ in range(a.kernel_iters):
-        st.rowpass(stage, None)
+        rp_launch(stage, None)
     e1.record()
     torch.cuda.synchronize()
     b2b_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
@@ -800,7 +801,9 @@ def run(a, world):
             "env_kernel_env_steps_per_s": a.num_envs / (env_us * 1e-6),
             "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
             "episodes_finished_total": float(stats[0]),
-            "roofline": {"kernel": f"satrl_ppo_rowpass<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA 16x16x4)",
+            "roofline": {"kernel": (f"satrl_ppo_rowpass_dw2<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA "
+                                    "16x16x4; the dW2 product fused in)" if st.fused_dw2 else
+                                    f"satrl_ppo_rowpass<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA 16x16x4)"),
                          "bound": "mfma",
                          "achieved": rowpass_flop / (head_us * 1e-6) / 1e12, "peak": FP32_MFMA_PEAK_TFS,
                          "unit": "TFLOP/s",

@@ -119,6 +119,28 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream);
 
+/* The same launch for the actor's probability ratios: ratio f32 [mb]
+ * (row order of the minibatch) receives exp(logp(a|s) - logp_old) of every
+ * row as the loss head computes it (ppo_continuous.py:220); the other
+ * outputs are satrl_ppo_rowpass's.  The parity hook of the identity "the
+ * first epoch's first minibatch recomputes the rollout's log-probs bit for
+ * bit", i.e. every ratio == 1.0f exactly.  net must include the actor.    */
+int satrl_ppo_rowpass_ratio(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
+                            const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
+                            float* ptail, float* pw1, float* ratio, void* stream);
+
+/* H = 64 / 128 (BASELINE configs[1]): the rowpass with the dW2 product fused
+ * in.  Each workgroup multiplies its own 32 rows' dZ2^T H1 out of LDS and
+ * writes that partial as split-K slab (its row block) of p2 [2][S][H][H],
+ * S = satrl_ppo_row_blocks(H, mb); H1 / dZ2 are not written.  The slabs are
+ * bitwise satrl_ppo_dw2's at that S (one 32-row chunk per split, the same
+ * MFMA sequence), so satrl_ppo_reduce(..., S, ...) gives the same G; the
+ * minibatch step is three launches (rowpass_dw2, reduce, adam).            */
+int satrl_ppo_row_blocks(int H, int mb);
+int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
+                          const float* W2T, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
+                          float* pw1, void* stream);
+
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result
  * is independent of N and of the sharding, and the rollout's log-probs equal
  * the update's first recomputation bit for bit.

@@ -258,15 +258,9 @@ __device__ __forceinline__ void mfma_rows_pre(const float* __restrict__ B, int n
   for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, pre.bb[c]);
 }
 
-// no VALU filler (mfma_rows' fill(c) is called per chunk, APRE path only)
-struct NoFill {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-
-template <int K, int LDA, int LDB, int RT, int CT, bool APRE, bool PRE = false, class Fill = NoFill>
+template <int K, int LDA, int LDB, int RT, int CT, bool APRE, bool PRE = false>
 __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const float* __restrict__ B, int n0,
-                                          f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr,
-                                          const Fill& fill = Fill{}) {
+                                          f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr) {
   constexpr int NC = K / 32;
   constexpr int BPD = kBPD < NC ? kBPD : NC;                     // prefetch distance in chunks
   static_assert(NC % 2 == 0, "chunk pairs");
@@ -292,7 +286,6 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
     for (int c = 0; c < NC; ++c) {
       if (c + BPD < NC) b_chunk<CT>(bp + 32 * (c + BPD), LDB, bb[(c + BPD) % NB]);
       if (c + 1 < NC) a_chunk<LDA, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
-      fill(c);                                   // the caller's VALU work for this chunk's MFMA gaps
       mfma_regs<RT, CT>(aa[c % 2], bb[c % NB], acc);
     }
   } else {
@@ -377,21 +370,28 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 
   // ---- A: gather, fc1 on MFMA ------------------------------------------------
   // this wave's W1aug rows [n][20] (k 0..19, zero-padded to 32; lane group g
-  // takes k = 8g .. 8g+7), issued first so they overlap the row gather
-  float4 bw1[CT][2];
+  // takes k = 8g .. 8g+7), issued first so they overlap the row gather.  The
+  // loads are unconditional (in-row offsets clamped) and the zero padding is
+  // selected only after the gather's barrier: a load inside a lane-group
+  // branch made the wave wait for it before issuing its row loads
+  // The fc2 bias and output-layer weights of this wave's columns (used in C)
+  // go out with them: __syncthreads drains every outstanding load, so loads
+  // issued after the gather would hold up the barrier below
+  float4 w1raw[CT][2];
+  float b2v[CT], w3raw[CT][3];
   {
     const float* W1 = P + L.W1 + (int64_t)net * H * 20;
+    const int o0 = lg < 2 ? 8 * lg : 16, o1 = lg < 2 ? 8 * lg + 4 : 16;
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
-      const float* bp = W1 + (int64_t)(n0 + 16 * t + li) * 20;
-      bw1[t][0] = make_float4(0.f, 0.f, 0.f, 0.f);
-      bw1[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lg < 2) {
-        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 8 * lg);
-        bw1[t][1] = *reinterpret_cast<const float4*>(bp + 8 * lg + 4);
-      } else if (lg == 2) {
-        bw1[t][0] = *reinterpret_cast<const float4*>(bp + 16);
-      }
+      const int n = n0 + 16 * t + li;
+      const float* bp = W1 + (int64_t)n * 20;
+      w1raw[t][0] = *reinterpret_cast<const float4*>(bp + o0);
+      w1raw[t][1] = *reinterpret_cast<const float4*>(bp + o1);
+      b2v[t] = P[L.b2 + net * H + n];
+      w3raw[t][0] = P[(net == 0 ? L.W3a : L.W3c) + n];
+      w3raw[t][1] = P[L.W3a + H + n];
+      w3raw[t][2] = P[L.W3a + 2 * H + n];
     }
   }
   gather(tid, NT);
@@ -400,20 +400,18 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
     sm.S[r][c] = (c == 18 && r < nvalid) ? 1.0f : 0.0f;           // bias column of W1aug, zero pad
   }
   PHASE_PROBE(8);
-  // fc2 bias and output-layer weights of this wave's columns (used in C)
-  float b2v[CT];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int n = n0 + 16 * t + li;
-    b2v[t] = P[L.b2 + net * H + n];
-    if (net == 0) {
-      w3[t][0] = P[L.W3a + n]; w3[t][1] = P[L.W3a + H + n]; w3[t][2] = P[L.W3a + 2 * H + n];
-    } else {
-      w3[t][0] = P[L.W3c + n]; w3[t][1] = 0.0f; w3[t][2] = 0.0f;
-    }
-  }
   rp_barrier();
   PHASE_PROBE(9);
+  float4 bw1[CT][2];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    bw1[t][0] = lg < 3 ? w1raw[t][0] : z4;
+    bw1[t][1] = lg < 2 ? w1raw[t][1] : z4;
+    w3[t][0] = w3raw[t][0];                                       // actor: mean_layer rows, critic: fc3
+    w3[t][1] = net == 0 ? w3raw[t][1] : 0.0f;
+    w3[t][2] = net == 0 ? w3raw[t][2] : 0.0f;
+  }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -504,14 +502,16 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
   return od;
 }
 
-template <int H, int NW, int R = kRows>
+template <int H, int NW, int R = kRows, bool FDW2 = false>
 __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const float* __restrict__ W2T, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
-                                                      float* __restrict__ pw1, int net_sel) {
-  constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW;
+                                                      float* __restrict__ pw1, int net_sel, float* __restrict__ p2,
+                                                      int S2, float* __restrict__ ratio_out) {
+  constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
+  static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
   __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
@@ -530,36 +530,73 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   }
 #endif
   PHASE_PROBE(0);
-  // the head's output-layer bias / log_std (uniform: scalar loads issued now,
-  // long landed when the head runs)
-  float hb3[3], hls[3];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) { hb3[d] = P[L.b3a + d]; hls[d] = P[L.ls + d]; }
-  const float hb3c = P[L.b3c];
-  // the actor head's per-dimension constants (var = exp(log_std)^2, log std,
-  // 1/var), off the head's dependency chain: lanes 0-2 compute them into LDS
-  // right after issuing their row gather (the barriers of the forward pass
-  // publish them)
+  // The head's scalars (mean_layer bias, log_std, fc3 bias) and its
+  // per-dimension constants (var = exp(log_std)^2, log std, 1/var), off the
+  // head's dependency chain: lanes 0-3 of the last wave (no row load of its
+  // own at H = 256) load them as per-lane vector loads and compute the
+  // constants into LDS during the gather (the barriers of the forward pass
+  // publish them).  Uniform scalar loads of P here would make the wave's
+  // first s_waitcnt lgkmcnt -- the one for the kernel arguments -- wait for
+  // them before any row load is issued.
   __shared__ float hcs[3][3];
+  __shared__ float hb3s[4];                                        // b3a[0..2], b3c
+  const int hd = tid - (NT - 64);                                  // head-scalar lane of the last wave
+  float hls_d = 0.0f, hb3_d = 0.0f;
+  if (hd >= 0 && hd < 4) {
+    hb3_d = P[hd < 3 ? L.b3a + hd : L.b3c];
+    hls_d = P[L.ls + (hd < 3 ? hd : 0)];
+  }
 
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
   auto gather = [&](int t0, int nt) {
-    for (int q = t0; q < R * 26; q += nt) {
-      const int r = q / 26, c = q % 26, row = r0 + r;
-      const float v = row < mb ? src[(idx ? idx[row] : (int64_t)row) * 32 + c] : 0.0f;
-      if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;           // s | a, logp_old, adv, v_target
-    }
-    if (t0 < 3) {
-      const float ls = t0 == 0 ? hls[0] : (t0 == 1 ? hls[1] : hls[2]);
-      const float sd = expf(ls), var = sd * sd;
-      hcs[0][t0] = var;
-      hcs[1][t0] = logf(sd);
-      hcs[2][t0] = 1.0f / var;
+    auto head_consts = [&] {
+      // (opaque to the compiler and ordered after the row loads: otherwise it
+      // hoists this arithmetic next to its loads at the top of the kernel,
+      // and the whole wave waits for them before issuing any row load)
+      asm volatile("" : "+v"(hls_d), "+v"(hb3_d)::"memory");
+      if (hd >= 0 && hd < 4) {
+        hb3s[hd] = hb3_d;
+        if (hd < 3) {
+          const float sd = expf(hls_d), var = sd * sd;
+          hcs[0][hd] = var;
+          hcs[1][hd] = logf(sd);
+          hcs[2][hd] = 1.0f / var;
+        }
+      }
+    };
+    if (idx == nullptr) {
+      // contiguous (staged) rows: one 16-B load per thread covers the block's
+      // R x 32 floats, all in flight at once (a loop of dependent scalar
+      // loads took four load round trips at H = 64's 256 threads)
+      // (branch-free: rows past the minibatch load its last row, zeroed below)
+      static_assert(R * 8 <= NT, "one float4 per thread");
+      const int r = (t0 >> 3) & (R - 1), c4 = t0 & 7, row = r0 + r;
+      const bool in = t0 < R * 8;
+      float4 v = reinterpret_cast<const float4*>(src)[(int64_t)(row < mb ? row : mb - 1) * 8 + c4];
+      head_consts();
+      if (row >= mb) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in) {
+        const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * c4 + e;                                  // s | a, logp_old, adv, v_target | pad
+          if (c < 18) S[r][c] = e4[e];
+          else if (c < 26) ax[r][c - 18] = e4[e];
+        }
+      }
+    } else {
+      for (int q = t0; q < R * 26; q += nt) {
+        const int r = q / 26, c = q % 26, row = r0 + r;
+        const float v = row < mb ? src[idx[row] * 32 + c] : 0.0f;
+        if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;
+      }
+      head_consts();
     }
   };
-  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, FDW2 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc,
+                              h1, w3);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
   mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
@@ -574,7 +611,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanh_f32(out_sum<NW, R>(sm.osum, r, d) + hb3[d]);
+          th[d] = tanh_f32(out_sum<NW, R>(sm.osum, r, d) + hb3s[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           var[d] = hcs[0][d];
           dv[d] = ax[r][d] - mu[d];
@@ -585,6 +622,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         const float lsum = (logp[0] + logp[1]) + logp[2];
         const float lold = (ax[r][3] + ax[r][4]) + ax[r][5];
         const float ratio = expf(lsum - lold);
+        if (ratio_out != nullptr) ratio_out[row] = ratio;          // (satrl_ppo_rowpass_ratio)
         const float adv = ax[r][6];
         const float s1 = ratio * adv;
         const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
@@ -603,7 +641,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
           dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        const float vc = out_sum<NW, R>(sm.osum, r, 0) + hb3c;
+        const float vc = out_sum<NW, R>(sm.osum, r, 0) + hb3s[3];
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
@@ -644,7 +682,9 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
   float d2v[RT][CT][4];
   // unswitched on the (workgroup-uniform) net: no per-element branches, and
-  // the critic skips the actor's three output columns
+  // the critic skips the actor's three output columns.  (Moving the db2 /
+  // dW3 partial sums into phase D's MFMA gaps measured slower: D +2.6 k
+  // cycles for 0.5 k saved here, EXPERIMENTS.md round 4.)
   auto tail = [&](auto actor) {
     constexpr bool ACT = decltype(actor)::value;
     constexpr int NC = ACT ? 3 : 1;
@@ -677,18 +717,18 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 #pragma unroll
       for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
       if (lg == 0) {
-        tp[net * H + n] = cb2;                          // db2
+        tp[net * H + n] = cb2;                                     // db2
         if constexpr (ACT) {                                       // dW3a
           tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2];
         } else {
-          tp[5 * H + 8 + n] = cw[0];                    // dW3c
+          tp[5 * H + 8 + n] = cw[0];                               // dW3c
         }
       }
     }
   };
   if (net == 0) tail(std::true_type{});
   else tail(std::false_type{});
-  store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
+  if constexpr (!FDW2) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   rp_barrier();
   PHASE_PROBE(5);
 
@@ -726,6 +766,37 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
     }
   }
   PHASE_PROBE(7);
+
+  // ---- F (FDW2, H <= 128): this block's dW2 partial = dZ2^T H1 over its rows ---
+  // straight from the LDS images (dzs, h1s), written as split-K slab rb of
+  // p2 [2][S2][H][H]: the MFMA sequence of dw2_kernel on one 32-row chunk
+  // (A[n][k] = dZ2[row][n], B[k][m] = H1[row][m], row = 4ks + lg; rows past
+  // the minibatch masked to 0), so the slab is bitwise dw2_kernel's with
+  // S = the row-block count -- without the H1 / dZ2 round trip through HBM
+  // and the dW2 launch.
+  if constexpr (FDW2) {
+    constexpr int MT = H / 16;
+    const int nvalid = mb - r0;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      f4 a2[MT];
+#pragma unroll
+      for (int j = 0; j < MT; ++j) a2[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < R / 4; ++ks) {
+        const int row = 4 * ks + lg;
+        float a = dzs[row][n0 + 16 * t + li];
+        if (row >= nvalid) a = 0.0f;
+#pragma unroll
+        for (int j = 0; j < MT; ++j) a2[j] = mfma4(a, sm.h1s[row][16 * j + li], a2[j]);
+      }
+      float* out = p2 + ((int64_t)net * S2 + rb) * H * H;
+#pragma unroll
+      for (int j = 0; j < MT; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(int64_t)(n0 + 16 * t + 4 * lg + q) * H + 16 * j + li] = a2[j][q];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -958,6 +1029,15 @@ __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
   for (int k = 0; k < nw; ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
 }
 
+// what a reduce thread ends with: the float4 of G it wrote (lead threads
+// only: live), its float4 index in the flat layout, and its net
+struct RedOut {
+  float4 v;
+  int64_t e4;
+  int net;
+  bool live;
+};
+
 // the W1 and tail parts of reduce (block b of the W1 region, or of the tail
 // after it: b counts from the first W1 block): sums the rowpass slabs into G
 // (mode & 1) or rescales G (world > 1), and adds this thread's squares to
@@ -965,7 +1045,7 @@ __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
 __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const RedGeom& g, int b, int mode,
                                                const float* __restrict__ p1, const float* __restrict__ pt,
                                                float4* __restrict__ G4, int world, float4* red, double& sa,
-                                               double& sc) {
+                                               double& sc, RedOut& o) {
   const int t = threadIdx.x;
   if (b < g.nb1) {                                                // W1: [nw1] slabs of 2*H*20
     constexpr int EB = 256 / kRedCH1;
@@ -986,6 +1066,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
       sa += crit ? 0.0 : q;
       sc += crit ? q : 0.0;
     }
+    o = RedOut{v, L.W1 / 4 + col, col * 4 >= (int64_t)H * 20 ? 1 : 0, lead && valid};
   } else {                                                        // tail: [nwg] slabs of 6H+12
     b -= g.nb1;
     constexpr int EB = 256 / kRedCHt;
@@ -999,27 +1080,23 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
       v = G4[L.b2 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.b2 / 4 + col] = v; }
     }
+    const bool crit = valid && net_of(L, L.b2 + col * 4, H);
     if (lead && valid) {
       const double q = sq4(v);
-      const bool crit = net_of(L, L.b2 + col * 4, H);
       sa += crit ? 0.0 : q;
       sc += crit ? q : 0.0;
     }
+    o = RedOut{v, L.b2 / 4 + col, crit ? 1 : 0, lead && valid};
   }
 }
 
-__global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode, const float* __restrict__ p2,
-                                                     const float* __restrict__ p1, const float* __restrict__ pt,
-                                                     float* __restrict__ G, double* __restrict__ nsq,
-                                                     double* __restrict__ steps, int world) {
-  const Layout L = layout(H);
-  __shared__ double sh[8];
-  __shared__ float4 red[256];
-  double sa = 0.0, sc = 0.0;
+// block b of reduce: the W2 region, else the W1 / tail regions
+__device__ __forceinline__ void reduce_block(int H, const Layout& L, const RedGeom& g, int b, int mode,
+                                             const float* __restrict__ p2, const float* __restrict__ p1,
+                                             const float* __restrict__ pt, float4* __restrict__ G4, int world,
+                                             float4* red, double& sa, double& sc, RedOut& o) {
   const int t = threadIdx.x;
   const int64_t HH4 = (int64_t)H * H / 4;
-  float4* G4 = reinterpret_cast<float4*>(G);
-  int b = blockIdx.x;
   if (b < g.nb2) {                                                // W2: [2][S] split-K slabs of H*H
     constexpr int EB = 256 / kRedCH2;
     const int64_t col = (g.net > 0 ? HH4 : 0) + (int64_t)b * EB + (t % EB);
@@ -1037,9 +1114,24 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
     if (lead && valid) {
       if (net) sc += sq4(v); else sa += sq4(v);
     }
+    o = RedOut{v, col, net, lead && valid};
   } else {
-    reduce_w1_tail(H, L, g, b - g.nb2, mode, p1, pt, G4, world, red, sa, sc);
+    reduce_w1_tail(H, L, g, b - g.nb2, mode, p1, pt, G4, world, red, sa, sc, o);
   }
+}
+
+__global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode, const float* __restrict__ p2,
+                                                     const float* __restrict__ p1, const float* __restrict__ pt,
+                                                     float* __restrict__ G, double* __restrict__ nsq,
+                                                     double* __restrict__ steps, int world) {
+  const Layout L = layout(H);
+  __shared__ double sh[8];
+  __shared__ float4 red[256];
+  double sa = 0.0, sc = 0.0;
+  const int t = threadIdx.x;
+  float4* G4 = reinterpret_cast<float4*>(G);
+  RedOut o;
+  reduce_block(H, L, g, blockIdx.x, mode, p2, p1, pt, G4, world, red, sa, sc, o);
   if (mode & 2) {
     block_sum2(sa, sc, sh);
     if (t == 0) {
@@ -1260,34 +1352,65 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
   return 0;
 }
 
+// every rowpass launch: fdw2 (H <= 128) writes the block's dW2 partial to p2
+// instead of H1 / dZ2; ratio (nullable) receives the actor's per-row ratio
+static int launch_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
+                          const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
+                          float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream) {
+  const int R = rows_per_wg(H, mb), nrb = n_head_wg(H, mb);
+  dim3 g((net < 0 ? 2 : 1) * nrb);   // (row block, net) pairs, or row blocks of one net
+  hipStream_t s = (hipStream_t)stream;
+  // waves per workgroup: one 16-column tile per wave for both 16-row tiles
+#define RP_ARGS mb, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio
+  if (H == 64 && fdw2)
+    hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true>), g, dim3(256), 0, s, RP_ARGS);
+  else if (H == 64)
+    hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, RP_ARGS);
+  else if (H == 128 && fdw2)
+    hipLaunchKernelGGL((rowpass_kernel<128, 8, kRows, true>), g, dim3(512), 0, s, RP_ARGS);
+  else if (H == 128)
+    hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, RP_ARGS);
+  else if (R == kRowsShort)
+    hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, RP_ARGS);
+  else
+    hipLaunchKernelGGL((rowpass_kernel<256, kNW256>), g, dim3(kNW256 * 64), 0, s, RP_ARGS);
+#undef RP_ARGS
+  LAUNCH_CHECK();
+  return 0;
+}
+
 int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const float* W2T,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream) {
   if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1)
     return -1;
-  const int R = rows_per_wg(H, mb);
-  dim3 g((net < 0 ? 2 : 1) * n_head_wg(H, mb));   // (row block, net) pairs, or row blocks of one net
-  hipStream_t s = (hipStream_t)stream;
-  // waves per workgroup: one 16-column tile per wave for both 16-row tiles
-  if (H == 64)
-    hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
-                       max_action, H1, dZ2, ptail, pw1, net);
-  else if (H == 128)
-    hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
-                       max_action, H1, dZ2, ptail, pw1, net);
-  else if (R == kRowsShort)
-    hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, mb, src, idx, P, W2T, epsilon,
-                       ent_coef, max_action, H1, dZ2, ptail, pw1, net);
-  else
-    hipLaunchKernelGGL((rowpass_kernel<256, kNW256>), g, dim3(kNW256 * 64), 0, s, mb, src, idx, P, W2T, epsilon, ent_coef,
-                       max_action, H1, dZ2, ptail, pw1, net);
-  LAUNCH_CHECK();
-  return 0;
+  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, nullptr,
+                        nullptr, false, stream);
 }
 
+int satrl_ppo_rowpass_ratio(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
+                            const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
+                            float* ptail, float* pw1, float* ratio, void* stream) {
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1 ||
+      !ratio)
+    return -1;
+  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, nullptr,
+                        ratio, false, stream);
+}
 
+int satrl_ppo_row_blocks(int H, int mb) {
+  if (!valid_h(H) || mb <= 0) return -1;
+  return n_head_wg(H, mb);
+}
 
-
+int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
+                          const float* W2T, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
+                          float* pw1, void* stream) {
+  if ((H != 64 && H != 128) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !p2 || !ptail || !pw1)
+    return -1;
+  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
+                        nullptr, true, stream);
+}
 
 int satrl_ppo_dw2_splits(int H, int mb) {
   if (!valid_h(H) || mb <= 0) return -1;

@@ -118,6 +118,11 @@ _SIGS = {
                         C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp,
                            _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_rowpass_ratio": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
+                                 _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_row_blocks": ([C.c_int, C.c_int], C.c_int),
+    "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
+                               _vp, _vp, _vp], C.c_int),
     "satrl_policy_act": ([C.c_int, _i64, _vp, _vp, _vp, C.c_float, C.c_uint64, _i64, C.c_uint64, _vp, _vp, _vp, _vp,
                           _vp, _vp], C.c_int),
     "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),

@@ -260,7 +260,10 @@ class FusedMinibatch:
         self.lib_gemm = learner.H >= 256
         if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob
             self.lib_gemm = os.environ["SATRL_DW2_LIB"] == "1"
-        self.S = self.splits(learner.H, self.mb)
+        # H = 64 (configs[1]): the rowpass multiplies each block's dW2 partial
+        # out of LDS itself (satrl_ppo_rowpass_dw2), bitwise the dw2_kernel's
+        # one-chunk splits, so a minibatch step is three launches instead of four
+        self.fused_dw2 = learner.H == 64 and not self.lib_gemm
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
         self.split = bool(split_chains) and learner.pg is None
@@ -269,6 +272,7 @@ class FusedMinibatch:
         nwg, nblk = C.c_int64(), C.c_int64()
         check(_lib.lib().satrl_ppo_sizes(H, self.mb, C.byref(nwg), C.byref(nblk)), "satrl_ppo_sizes")
         self.nwg, self.nblk = nwg.value, nblk.value
+        self.S = self.splits(learner.H, self.mb)
         f32 = dict(dtype=torch.float32, device=dev)
         self.H1 = torch.empty(2 * self.mb * H, **f32)
         self.dZ2 = torch.empty(2 * self.mb * H, **f32)
@@ -316,6 +320,38 @@ class FusedMinibatch:
                   "satrl_ppo_rowpass")
         return H1, dZ2
 
+    def rowpass_dw2(self, src, idx, mb=None, net=-1):
+        """satrl_ppo_rowpass_dw2 (H = 64): the rowpass with each block's dW2
+        partial written as split-K slab of p2 (no H1 / dZ2 stores)."""
+        L = self.L
+        mb = self.mb if mb is None else int(mb)
+        check(_lib.lib().satrl_ppo_rowpass_dw2(L.H, mb, int(net), ptr(src), None if idx is None else ptr(idx),
+                                               ptr(L.P), ptr(L.W2T), float(L.epsilon), float(L.entropy_coef),
+                                               float(L.max_action), ptr(self.p2), ptr(self.ptail), ptr(self.pw1),
+                                               stream_ptr()), "satrl_ppo_rowpass_dw2")
+
+    def rowpass_ratio(self, src, idx, ratio, mb=None, net=-1):
+        """satrl_ppo_rowpass_ratio: satrl_ppo_rowpass that also writes the
+        actor's probability ratio exp(logp - logp_old) per row into `ratio`."""
+        L = self.L
+        H = L.H
+        mb = self.mb if mb is None else int(mb)
+        n = 2 * mb * H
+        _lib.require_cuda(ratio, torch.float32, (mb,), "ratio")
+        check(_lib.lib().satrl_ppo_rowpass_ratio(H, mb, int(net), ptr(src), None if idx is None else ptr(idx),
+                                                 ptr(L.P), ptr(L.W2T), float(L.epsilon), float(L.entropy_coef),
+                                                 float(L.max_action), ptr(self.H1[:n]), ptr(self.dZ2[:n]),
+                                                 ptr(self.ptail), ptr(self.pw1), ptr(ratio), stream_ptr()),
+              "satrl_ppo_rowpass_ratio")
+        return ratio
+
+    def step_kernel_flops(self, mb=None):
+        """Algorithmic FLOPs of the step's first launch: the rowpass, plus the
+        dW2 product (2 H^2 per row and net) where it is fused in (H = 64)."""
+        mb = self.mb if mb is None else int(mb)
+        H = self.L.H
+        return self.rowpass_flops(H, mb) + (2 * 2 * H * H * mb if self.fused_dw2 else 0)
+
     @staticmethod
     def rowpass_flops(H, mb):
         """Algorithmic FLOPs of one rowpass launch over both nets (DESIGN.md
@@ -329,10 +365,17 @@ class FusedMinibatch:
         """Upper bound of splits(H, mb) over every mb (the p2 capacity)."""
         if self.lib_gemm:
             return max(self.S, 4)
+        if self.fused_dw2:
+            return self.nwg                  # row blocks of the longest minibatch at or below mb
         return max(self.S, 256 // (2 * (H // 64) ** 2))
 
     def splits(self, H, mb):
         """split-K ways of the dW2 product for a minibatch of mb rows."""
+        if self.fused_dw2:
+            S = _lib.lib().satrl_ppo_row_blocks(int(H), int(mb))      # one slab per rowpass row block
+            if S < 1:
+                raise _lib.NativeError(f"satrl_ppo_row_blocks({H}, {mb}) failed")
+            return S
         if self.lib_gemm:
             S = int(os.environ.get("SATRL_DW2_SPLITS", "4"))          # dev A/B knob; 4 measured best
             return S if mb % S == 0 else 1
@@ -413,16 +456,21 @@ class FusedMinibatch:
         if skip_rowpass:
             n = 2 * mb * H
             H1, dZ2 = self.H1[:n], self.dZ2[:n]
+        elif self.fused_dw2:
+            self.rowpass_dw2(src, idx, mb, net)
+            H1 = dZ2 = None
         else:
             H1, dZ2 = self.rowpass(src, idx, mb, net)
         if events is not None:
             events[1].record()
         if L.pg is None:
-            self._dw2(H1, dZ2, mb, S, net)
+            if not self.fused_dw2:
+                self._dw2(H1, dZ2, mb, S, net)
             check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
-            self._dw2(H1, dZ2, mb, S, net)
+            if not self.fused_dw2:
+                self._dw2(H1, dZ2, mb, S, net)
             check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        None, None, sp), "satrl_ppo_reduce")
             # one bucket, both nets: SUM over the ranks, then G /= world and the norms in one launch

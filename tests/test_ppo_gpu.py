@@ -468,14 +468,16 @@ def test_update_graph_groups_equal_eager():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("N", [1000, 65536])
-def test_policy_act_and_value_kernels(N):
+@pytest.mark.parametrize("H,N", [(256, 1000), (256, 65536), (64, 4096), (64, 65536)])
+def test_policy_act_and_value_kernels(H, N):
     """satrl_policy_act / satrl_policy_value vs the torch modules + satrl_gaussian_sample
     (same Philox draw); every row independent of N and of its position (bitwise).
-    N 65536: configs[3]'s total env count in one launch."""
+    N 65536: configs[3]'s total env count in one launch; H 64 at N 4096:
+    configs[1]'s rollout kernels (policy_kernel<64, 4, 0/1>,
+    ppo_continuous.py:61-101, 176-189)."""
     from satrl.ppo import PPOLearner, gaussian_sample, policy_act, policy_value
     torch.manual_seed(5)
-    args = _args(hidden_width=256)
+    args = _args(hidden_width=H)
     Lp = PPOLearner(args, "pursuer", use_graph=False)
     Le = PPOLearner(args, "evader", use_graph=False)
     with torch.no_grad():
@@ -486,7 +488,7 @@ def test_policy_act_and_value_kernels(N):
     obs = torch.randn((N, 18), device="cuda", generator=g)
     sb = torch.tensor([7], dtype=torch.int64, device="cuda")
     out = [torch.empty((N, 3), device="cuda") for _ in range(4)]
-    policy_act(256, obs, Lp.P, Le.P, 1.6, 123, 4096, 5, *out, step_base=sb)
+    policy_act(H, obs, Lp.P, Le.P, 1.6, 123, 4096, 5, *out, step_base=sb)
     with torch.no_grad():
         for k, L in enumerate((Lp, Le)):
             mean = L.actor(obs)
@@ -494,15 +496,15 @@ def test_policy_act_and_value_kernels(N):
             assert torch.allclose(out[2 * k], a_ref, rtol=1e-5, atol=1e-5)
             assert torch.allclose(out[2 * k + 1], lp_ref, rtol=1e-4, atol=1e-4)
         v = torch.empty(N, device="cuda")
-        policy_value(256, obs, Lp.P, v)
+        policy_value(H, obs, Lp.P, v)
         assert torch.allclose(v, Lp.critic(obs).reshape(-1), rtol=1e-5, atol=1e-5)
     # rows are independent of N / position: a sub-block with the matching env offset
     sub = [torch.empty((37, 3), device="cuda") for _ in range(4)]
-    policy_act(256, obs[100:137].contiguous(), Lp.P, Le.P, 1.6, 123, 4096 + 100, 5, *sub, step_base=sb)
+    policy_act(H, obs[100:137].contiguous(), Lp.P, Le.P, 1.6, 123, 4096 + 100, 5, *sub, step_base=sb)
     for a, b in zip(out, sub):
         assert torch.equal(a[100:137], b)
     v2 = torch.empty(37, device="cuda")
-    policy_value(256, obs[100:137].contiguous(), Lp.P, v2)
+    policy_value(H, obs[100:137].contiguous(), Lp.P, v2)
     assert torch.equal(v[100:137], v2)
 
 
@@ -588,3 +590,79 @@ def test_dw2_lib_vs_fp64_and_deterministic(mb, S, net):
             continue
         err = (outs[0][n].double() - ref[n]).abs().max().item()
         assert err <= 1e-5 * ref[n].abs().max().item() + 1e-4, err
+
+
+@pytest.mark.parametrize("mb,contig", [(4096, True), (777, False), (256, True)])
+def test_fused_dw2_rowpass_bitwise_equals_separate(mb, contig):
+    """H 64 (configs[1]): satrl_ppo_rowpass_dw2 writes each 32-row block's
+    dW2 partial out of LDS as split-K slab `row block` of p2 -- bitwise the
+    slabs satrl_ppo_rowpass + satrl_ppo_dw2 write at S = the row-block count
+    -- and the same [dW1|db1] / tail slabs, so the reduced G is bitwise the
+    four-launch step's (ppo_continuous.py:227-239).  777: a ragged last
+    block on the index-gather path; 4096 / 256: staged contiguous rows."""
+    import satrl._lib as _L
+    from satrl.ppo import PPOLearner
+    torch.manual_seed(3)
+    B = 8192
+    args = _args(hidden_width=64, mini_batch_size=mb, batch_size=B)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    with torch.no_grad():
+        for p in list(L.actor.parameters()) + list(L.critic.parameters()):
+            p.add_(torch.randn_like(p) * 0.05)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(4)
+    src = torch.randn((B, 32), device="cuda", generator=g)
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+    idx = None if contig else torch.randperm(B, device="cuda", generator=g)[:mb]
+    st = L.stepper(mb)
+    assert st.fused_dw2 and st.S == (mb + 31) // 32
+    lib, sp, S = _L.lib(), _L.stream_ptr(), st.S
+    outs = []
+    for fused in (False, True):
+        for b in (st.p2, st.ptail, st.pw1):
+            b.fill_(float("nan"))
+        if fused:
+            st.rowpass_dw2(src, idx)
+        else:
+            H1, dZ2 = st.rowpass(src, idx)
+            _L.check(lib.satrl_ppo_dw2(64, mb, -1, S, _L.ptr(H1), _L.ptr(dZ2), _L.ptr(st.p2), sp), "satrl_ppo_dw2")
+        G = torch.full_like(L.G, float("nan"))
+        nsq = torch.zeros_like(st.nsq[0])
+        _L.check(lib.satrl_ppo_reduce(64, mb, -1, S, 3, _L.ptr(st.p2), _L.ptr(st.pw1), _L.ptr(st.ptail), _L.ptr(G),
+                                      _L.ptr(nsq), _L.ptr(L.steps), sp), "satrl_ppo_reduce")
+        torch.cuda.synchronize()
+        outs.append([st.p2[:2 * S * 64 * 64].clone(), st.ptail[:S * (6 * 64 + 12)].clone(),
+                     st.pw1[:S * 2 * 64 * 20].clone(), G, nsq])
+    for a, b in zip(*outs):
+        assert bool(torch.isfinite(a).all()) and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("H,mb", [(64, 4096), (256, 4096), (256, 512)])
+def test_rollout_logp_equals_update_recomputation(H, mb):
+    """The rollout's stored log-probs (policy_kernel, satrl_policy_act) are
+    what the update's first recomputation gives, bit for bit: on the first
+    minibatch of the first epoch, before any Adam step, every row's ratio
+    exp(logp - logp_old) is exactly 1.0f (ppo_continuous.py:176-189 stores
+    a_logprob, :216-220 recomputes it).  Both the staged-row and the
+    index-gather paths of the rowpass; H 256 mb 512 runs the 16-row kernel."""
+    from satrl.trainer import VecTrainer
+    N, T = 1024, 16
+    args = _args(batch_size=N * T, mini_batch_size=mb, hidden_width=H, K_epochs=1, num_envs=N, horizon=T,
+                 max_episode_steps=12, seed=9, rollout_graph_chunk=8, update_graph_group=2)
+    tr = VecTrainer(args, flag=0, d_capture=15000.0)
+    tr.collect()
+    tr.compute_advantages()
+    perm = tr.epoch_perm()
+    L = tr.learner
+    L.sync_w2t()
+    st = L.stepper(mb)
+    idx = perm[:mb].contiguous()
+    staged = tr.buf.packed[idx].contiguous()
+    for src, ix in ((tr.buf.packed, idx), (staged, None)):
+        ratio = torch.full((mb,), float("nan"), device="cuda")
+        st.rowpass_ratio(src, ix, ratio)
+        torch.cuda.synchronize()
+        bad = (ratio != 1.0).nonzero().reshape(-1)
+        assert bad.numel() == 0, (bad[:8].tolist(), ratio[bad[:8]].tolist())
+
+

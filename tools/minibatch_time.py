@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Development tool (not shipped, not a test): in-graph time of one fused
-minibatch step (rowpass -> dW2 -> reduce -> Adam) at H 256 for the given
-minibatch sizes, replaying the update's graphs over a 16-minibatch epoch.
+minibatch step (rowpass -> dW2 -> reduce -> Adam) at H 256 (PROBE_H sets
+another width) for the given minibatch sizes, replaying the update's graphs
+over a 16-minibatch epoch; SATRL_LIB_PATH selects a library build.
 Usage: python tools/minibatch_time.py 512 1024 2048 4096"""
 import os
 import sys
@@ -13,9 +14,10 @@ sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
 from satrl.ppo import PPOLearner  # noqa: E402
 from satrl.trainer import args_param  # noqa: E402
 
+H = int(os.environ.get("PROBE_H", "256"))
 for mb in [int(x) for x in sys.argv[1:]] or [4096]:
     B = 16 * mb
-    a = args_param(hidden_width=256, mini_batch_size=mb, batch_size=B, chkpt_dir="/tmp")
+    a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=B, chkpt_dir="/tmp")
     L = PPOLearner(a, "pursuer", graph_group=16)
     g = torch.Generator(device="cuda").manual_seed(0)
     src = torch.randn((B, 32), device="cuda", generator=g)
@@ -32,5 +34,5 @@ for mb in [int(x) for x in sys.argv[1:]] or [4096]:
         st.run(src, perm)
     e1.record()
     torch.cuda.synchronize()
-    print(f"mb {mb:5d}: {e0.elapsed_time(e1) * 1e3 / (n * 16):7.2f} us per minibatch step "
+    print(f"H {H} mb {mb:5d}: {e0.elapsed_time(e1) * 1e3 / (n * 16):7.2f} us per minibatch step "
           f"(SATRL_RP_SHORT_MB={os.environ.get('SATRL_RP_SHORT_MB', 'default')})", flush=True)

@@ -45,8 +45,16 @@ g = torch.Generator(device="cuda").manual_seed(0)
 src = torch.randn((16 * mb, 32), device="cuda", generator=g)
 src[:, 21:24] = -1.0 - torch.rand((16 * mb, 3), device="cuda", generator=g)
 st = L.stepper(mb)
-for _ in range(5):
-    st.rowpass(src, None)
+if os.environ.get("PROBE_CHAIN"):
+    # the stamps of the last rowpass of graph-replayed minibatch steps (the
+    # update's own conditions: Adam has just rewritten the weights)
+    perm = torch.randperm(16 * mb, device="cuda", generator=g)
+    for _ in range(3):
+        st.run(src, perm)
+    print("stamps: the last rowpass of graph-replayed minibatch steps")
+else:
+    for _ in range(5):
+        st.rowpass_dw2(src, None) if st.fused_dw2 else st.rowpass(src, None)
 torch.cuda.synchronize()
 
 if probe:

@@ -10,6 +10,7 @@ OUT=$ROOT/gpurun_out/r4_probe
 mkdir -p "$OUT"
 for H in ${PROBE_HS:-64 256}; do
   PROBE_H=$H timeout -k 10 120 python3 tools/phase_probe.py probe > "$OUT/phase_h$H.txt" 2>&1
+  PROBE_H=$H PROBE_CHAIN=1 timeout -k 10 120 python3 tools/phase_probe.py probe > "$OUT/phase_chain_h$H.txt" 2>&1
   ( cd /tmp && export TMPDIR=/tmp && PROBE_H=$H REPS=10 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv \
       -d "$OUT/tl_h$H" -o run -- python3 "$ROOT/tools/step_timeline.py" run > "$OUT/tl_h$H.log" 2>&1 )
   CSV=$(find "$OUT/tl_h$H" -name '*kernel_trace.csv')
