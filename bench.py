@@ -869,7 +869,9 @@ def run(a, world):
                                 "env_rk45_cw_avg_launch_us": env_rk45_us,
                                 "env_rk45_cw_env_steps_per_s": a.num_envs / (env_rk45_us * 1e-6),
                                 "note": "rk4_cw: propagator 1 (RK4, 10 substeps); rk45_cw: propagator 2, the "
-                                        "reference's solve_ivp RK45 on orbit_ode (satellite_function.py:783-839)"},
+                                        "reference's solve_ivp RK45 on orbit_ode (satellite_function.py:783-839); "
+                                        "RK4 stage weights: launch-uniform, held in scalar registers (an LDS table "
+                                        "would hold the same doubles and add a load per use)"},
                 "surrogate": {"kernel": "satenv_surrogate (ImprovedNN 5-256-128-64-10, bf16 MFMA 16x16x32, f32 acc)",
                               "in_rollout": bool(a.surrogate), "avg_launch_us": sur_us,
                               "env_steps_per_s": a.num_envs / (sur_us * 1e-6), "bound": "mfma",

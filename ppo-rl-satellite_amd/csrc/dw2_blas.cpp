@@ -205,9 +205,16 @@ bool tune(int H, int mb, int S, int nb, Plan& p) {
 // output bit for bit (non-repeating ones are dropped)
 struct Timed { float us; int index; };
 bool make_descriptors(int H, int mb, int S, int nb, Plan& p);
+void release(Plan& p);
+// destroys a scratch plan's descriptors on every exit path
+struct PlanGuard {
+  Plan& p;
+  ~PlanGuard() { release(p); }
+};
 std::vector<Timed> candidates(int H, int mb, int S, int nb, int det_check) {
   std::vector<Timed> out;
   Plan p;
+  PlanGuard guard{p};
   if (!make_descriptors(H, mb, S, nb, p)) return out;
   if (g_all.empty() &&
       hipblaslt_ext::getAllAlgos(g_lt, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_N, HIPBLAS_OP_T, HIP_R_32F,
@@ -243,9 +250,6 @@ std::vector<Timed> candidates(int H, int mb, int S, int nb, int det_check) {
       if (time_algo(p, c.second, w, sc, dn, &det) > 0.0f && det) out.push_back(c.first);
     }
   }
-  for (auto l : {p.la, p.lb, p.lc})
-    if (l) hipblasLtMatrixLayoutDestroy(l);
-  if (p.md) hipblasLtMatmulDescDestroy(p.md);
   return out;
 }
 

@@ -831,9 +831,25 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   const float* P = agent == 0 ? P0 : P1;
   const int nvalid = (int)(N - r0 < R ? N - r0 : R);
   auto gather = [&](int t0, int nt) {
-    for (int q = t0; q < R * 18; q += nt) {
-      const int r = q / 18, c = q % 18;
-      sm.S[r][c] = r < nvalid ? obs[(r0 + r) * 18 + c] : 0.0f;
+    const float* ob = obs + r0 * 18;
+    if (nvalid == R && (reinterpret_cast<uintptr_t>(ob) & 15) == 0) {
+      // a full block's R x 18 floats are one contiguous 16-B-aligned span:
+      // every float4 in flight at once (R * 18 / 4 <= one per thread)
+      static_assert(R * 18 / 4 <= 4 * 64, "one float4 per thread of the smallest workgroup");
+      if (t0 < R * 18 / 4) {
+        const float4 v = reinterpret_cast<const float4*>(ob)[t0];
+        const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = 4 * t0 + e;
+          sm.S[q / 18][q % 18] = e4[e];
+        }
+      }
+    } else {
+      for (int q = t0; q < R * 18; q += nt) {
+        const int r = q / 18, c = q % 18;
+        sm.S[r][c] = r < nvalid ? obs[(r0 + r) * 18 + c] : 0.0f;
+      }
     }
   };
   f4 acc[RT][CT];

@@ -596,9 +596,10 @@ SATENV_HD float norm3f(float a0, float a1, float a2) {
 // RK4 propagators.  rk4_step is the RungeKutta combination of
 // 轨道外推-龙格库塔算法.py:35-41 (K2 = f(r0 + h/2 K1), K3 = f(r0 + h/2 K2),
 // K4 = f(r0 + h K3), r1 = r0 + h/6 ((K1 + 2K2) + 2K3) + K4), elementwise in
-// that order.  The stage weights stay kernel-uniform scalars (SGPRs): a
-// Butcher table in LDS would add a load per stage and change the
-// reference's rounding order.
+// that order.  The stage weights (h/2, h, h/6 and the 2s) are uniform over a
+// launch, so they sit in scalar registers for the whole kernel -- on-chip,
+// read at no cost by every lane.  A Butcher table in LDS would hold the same
+// doubles (the same rounding) but add an LDS load and its wait per use.
 // ---------------------------------------------------------------------------
 template <class F>
 SATENV_HD void rk4_step(F f, const double (&r0)[6], double h, double (&out)[6]) {

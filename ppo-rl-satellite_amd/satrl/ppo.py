@@ -569,8 +569,19 @@ class FusedMinibatch:
             if self.graph is None or self._src_ptr != src.data_ptr():
                 self._capture(src)
             self.grp.zero_()
+            comm = self.L.comm
+            inflight = []
             for _ in range(nfull // G):
                 self.graph.replay()
+                if comm is not None:
+                    # RCCL watchdog between replays: at most two replays queued
+                    # ahead of the host, each waited for with the deadline while
+                    # ncclCommGetAsyncError is polled (rccl.Comm.wait_event)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    inflight.append(ev)
+                    if len(inflight) > 2:
+                        comm.wait_event(inflight.pop(0), _dist.dp_timeout_s())
             k = (nfull // G) * G
         while k < nfull:                      # the rest of the full minibatches, eagerly
             ng = min(G, nfull - k)

@@ -122,14 +122,22 @@ class Comm:
         return rc if rc not in (0, _NCCL_IN_PROGRESS) else err.value
 
     def wait(self, deadline_s: float, stream=None, poll_s: float = 0.001):
-        """Host watchdog between graph replays: block until the work queued so
-        far on `stream` (default: the current one) has finished, polling
-        ncclCommGetAsyncError meanwhile.  An RCCL error, or no completion
-        within deadline_s (a dead or stalled peer leaves this rank's
-        all-reduce kernels waiting forever), aborts the communicator
-        (ncclCommAbort ends its kernels) and raises CommError."""
+        """Host watchdog: block until the work queued so far on `stream`
+        (default: the current one) has finished, polling
+        ncclCommGetAsyncError meanwhile (wait_event)."""
         ev = torch.cuda.Event()
         ev.record(stream)
+        self.wait_event(ev, deadline_s, poll_s)
+
+    def wait_event(self, ev, deadline_s: float, poll_s: float = 0.001):
+        """Block until `ev` (a recorded torch.cuda.Event) has completed,
+        polling ncclCommGetAsyncError meanwhile.  An RCCL error, or no
+        completion within deadline_s (a dead or stalled peer leaves this
+        rank's all-reduce kernels waiting forever), aborts the communicator
+        (ncclCommAbort ends its kernels) and raises CommError.  The update
+        calls it between graph replays (FusedMinibatch.run keeps at most two
+        replays queued ahead of it), so a lost peer is caught within a
+        deadline of its replay, not after the whole update was queued."""
         t0 = time.monotonic()
         while not ev.query():
             err = self.async_error()

@@ -70,13 +70,18 @@ class Surrogate:
         if isinstance(state_dict, str) and state_dict == "trained":
             state_dict, self.scalers = load_trained()
         if state_dict is not None:
-            self.load_state_dict(state_dict)
+            self.load_state_dict(state_dict, scalers=self.scalers)
         self.net.to(self.device)
         self.blob = torch.empty(_lib.lib().satenv_surrogate_blob_bytes(), dtype=torch.uint8, device=self.device)
         self.pack()
 
-    def load_state_dict(self, sd):
-        """A state_dict or a path to one (loaded with weights_only=True)."""
+    def load_state_dict(self, sd, scalers=None):
+        """A state_dict or a path to one (loaded with weights_only=True).
+        `scalers` (in_mean, in_scale, out_mean, out_scale) go with these
+        weights; None loads them without scalers (identity), so weights
+        loaded into a Surrogate built from the trained net do not keep that
+        net's StandardScalers."""
+        self.scalers = None if scalers is None else tuple(scalers)
         if isinstance(sd, str):
             sd = torch.load(sd, map_location="cpu", weights_only=True)
         self.net.load_state_dict({k: v for k, v in sd.items() if not k.startswith("dropout")})

@@ -86,7 +86,8 @@ def test_c_host_matches_the_python_path(tmp_path):
     assert np.array_equal(dZ2.cpu().numpy(), _load(d, "ppo_dZ2.f32", np.float32, (2 * mb * H,)))
     st.step(src, None)
     torch.cuda.synchronize()
-    assert st.dw2_algo == plan["index"]
+    if st.dw2_source == "table":                 # the Python host pinned the table's solution
+        assert st.dw2_algo == plan["index"]
     out = {k: getattr(L, k).cpu().numpy() for k in ("G", "P", "M", "V", "W2T")}
     ref = {k: _load(d, f"ppo_{k}.f32", np.float32, out[k].shape) for k in out}
     assert np.array_equal(L.steps.cpu().numpy(), _load(d, "ppo_steps.f64", np.float64, (2,)))

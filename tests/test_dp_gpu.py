@@ -290,3 +290,27 @@ def test_rollout_sharding_invariant_at_full_size():
         got = np.concatenate([halves[0][k], halves[1][k]], axis=1)
         assert np.array_equal(got, full[k]), name
     assert full[2].any()                                  # episodes did end inside the window
+
+
+def test_comm_wait_deadline_and_async_error_raise():
+    """The RCCL watchdog (satrl.rccl.Comm.wait / wait_event): a stream that
+    does not finish within the deadline (a GPU spin standing in for a
+    collective stuck on a lost peer) raises CommError, and so does an
+    asynchronous communicator error; both abort the communicator (here: none
+    made, so abort is a no-op)."""
+    import ctypes as C
+
+    from satrl import rccl
+    c = rccl.Comm.__new__(rccl.Comm)
+    c._comm = C.c_void_p()
+    assert c.async_error() == 0
+    torch.cuda._sleep(int(2e9))                       # ~1 s of GPU spin on the current stream
+    with pytest.raises(rccl.CommError, match="stalled"):
+        c.wait(0.05)
+    torch.cuda.synchronize()
+    c.wait(5.0)                                       # finished work: returns
+    c.async_error = lambda: 3                         # ncclInternalError
+    torch.cuda._sleep(int(2e8))
+    with pytest.raises(rccl.CommError, match="asynchronous error"):
+        c.wait(60.0)
+    torch.cuda.synchronize()

@@ -171,3 +171,17 @@ def test_trained_improvednn_env_path(S, oracle):
     osc = torch.tensor(sur.scalers[3], device="cuda:0")
     assert torch.isfinite(out).all()
     assert ((out - ref).double().abs() / osc).max().item() < 1e-2
+
+
+def test_load_state_dict_drops_the_trained_scalers():
+    """Weights loaded into a Surrogate built from the trained net come
+    without that net's StandardScalers unless they are passed along."""
+    from satrl.surrogate import Surrogate
+    s = Surrogate(device="cuda:0", state_dict="trained")
+    assert s.scalers is not None
+    sd = {k: v.clone() for k, v in s.net.state_dict().items()}
+    sc = s.scalers
+    s.load_state_dict(sd)
+    assert s.scalers is None
+    s.load_state_dict(sd, scalers=sc)
+    assert s.scalers is not None and all(np.array_equal(a, b) for a, b in zip(s.scalers, sc))
