@@ -56,6 +56,10 @@ def parse():
                          "every rank steps --minibatch rows (global minibatch N x --minibatch); 'auto' (default) = "
                          "global for BASELINE configs[3] (65536 envs over 8 GPUs) and at N = 1, per_gpu for the "
                          "weak-scaling series of configs[2] (16384 envs per GPU at N = 2/4/8)")
+    ap.add_argument("--allreduce", choices=("rccl", "peer"), default="rccl",
+                    help="N > 1: the update's per-minibatch gradient all-reduce: RCCL (ncclAllReduce + reduce_dp in "
+                         "the graphs) or the peer kernel (satrl_ppo_allreduce_peer: two-shot over IPC-mapped "
+                         "buffers, fused with reduce_dp); the line times the other one beside it")
     ap.add_argument("--profile-tag", default="r3", help="profiles/<tag>_* files the rocprof cross-check fields read")
     ap.add_argument("--global-slice", type=int, default=256,
                     help="N > 1: minibatches of the configs[3]-semantics slice timed after the run (global "
@@ -371,7 +375,8 @@ def run(a, world):
     args = args_param(batch_size=a.num_envs * a.horizon, mini_batch_size=a.minibatch, hidden_width=a.hidden,
                       K_epochs=a.epochs, max_episode_steps=1000, num_envs=a.num_envs, horizon=a.horizon, seed=0,
                       max_train_steps=int(3e6), chkpt_dir="/tmp", surrogate=a.surrogate,
-                      update_graph_group=a.graph_group, dp_minibatch=a.dp_minibatch)
+                      update_graph_group=a.graph_group, dp_minibatch=a.dp_minibatch,
+                      allreduce=a.allreduce if pg is not None else "rccl")
     tr = VecTrainer(args, flag=0, d_capture=a.d_capture, pg=pg, env_offset=rank * a.num_envs)
 
     def barrier():
@@ -719,6 +724,7 @@ def run(a, world):
     dp_out = {}
     if pg is not None:
         dp = {"world": n_gpus, "backend": dist.get_backend(pg), "dp_minibatch": tr.dp_minibatch,
+              "allreduce": a.allreduce,
               "gradient_bucket_bytes": L.G.numel() * 4, "minibatch_step_us": t_chain,
               "dw2_plan": {"solution": st.dw2_algo if st.lib_gemm else None,
                            "source": getattr(st, "dw2_source", None) if st.lib_gemm else None}}
@@ -738,6 +744,35 @@ def run(a, world):
             dp["allreduce_timing"] = ("HIP events on the compute stream around kernel_iters back-to-back "
                                       "ncclAllReduce calls (satrl.rccl, the call the update's graphs capture), "
                                       "max over ranks")
+        # the peer all-reduce (fused with reduce_dp) on the same bucket, A/B beside RCCL
+        try:
+            from satrl.peer import PeerComm
+            peer = L.peer if L.peer is not None else PeerComm(pg, L.G.numel(), "cuda")
+            scratch = torch.randn(L.G.numel(), device="cuda")
+            nsq_s = torch.zeros_like(st.nsq[0])
+            steps_s = torch.zeros(2, dtype=torch.float64, device="cuda")
+            for _ in range(5):
+                peer.all_reduce_dp_(a.hidden, mb_local, scratch, nsq_s, steps_s)
+            barrier()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.kernel_iters):
+                peer.all_reduce_dp_(a.hidden, mb_local, scratch, nsq_s, steps_s)
+            e1.record()
+            torch.cuda.synchronize()
+            pr = torch.tensor([e0.elapsed_time(e1) * 1e3 / a.kernel_iters], dtype=torch.float64, device="cuda")
+            perr = torch.tensor([float(peer.error())], dtype=torch.float64, device="cuda")
+            dist.all_reduce(pr, op=dist.ReduceOp.MAX)
+            dist.all_reduce(perr, op=dist.ReduceOp.MAX)
+            dp["peer_allreduce_us"] = float(pr.item())
+            dp["peer_allreduce_error"] = bool(perr.item())
+            dp["peer_allreduce_timing"] = ("HIP events around kernel_iters back-to-back satrl_ppo_allreduce_peer "
+                                           "calls (the all-reduce of the gradient bucket fused with reduce_dp: "
+                                           "its norms and step counters), max over ranks")
+            if peer is not L.peer:
+                peer.close()
+        except Exception as exc:                       # noqa: BLE001 -- reported, not fatal to the line
+            dp["peer_allreduce_error"] = f"{type(exc).__name__}: {exc}"[:300]
         if a.global_slice > 0 and tr.dp_minibatch == "per_gpu" and a.minibatch % n_gpus == 0:
             mbg = a.minibatch // n_gpus
             stg = L.stepper(mbg)

@@ -13,12 +13,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
 
 #include "philox_device.h"
 #include "satrl_ppo.h"
+#include "satrl_peer.h"
 
 namespace {
 
@@ -1342,6 +1344,137 @@ bool valid_h(int H) { return H == 64 || H == 128 || H == 256; }
     if (e_ != hipSuccess) { g_err = hipGetErrorString(e_); return -2; }     \
   } while (0)
 
+// ---------------------------------------------------------------------------
+// peer_allreduce: the data-parallel gradient all-reduce of G over the W ranks
+// of one node without RCCL, fused with reduce_dp (G /= W, the per-block
+// squared norms, the step counters).  Each rank owns an exchange buffer that
+// every peer has mapped (IPC, uncached device memory); a value travels as
+// an 8-B granule {tag, f32} written by ONE 8-B system-scope store, so the
+// reader polls the granule itself -- no flag, no fence, no barrier
+// (MI355X_MICROARCH.md "Valid forms", the granule form).  Two shots:
+//   1 reduce-scatter push: every element goes to the rank that owns its
+//     slice (slice j = elements [j*sl, (j+1)*sl)), slot [this rank];
+//   2 the owner sums slot 0, 1, ... W-1 of each of its elements in rank
+//     order, divides by W (IEEE, as reduce_dp) and pushes the result to
+//     every rank's gather slot [owner];
+//   3 every rank polls its gather slots into G.
+// Each slice is summed once, in rank order, then broadcast, so every rank
+// gets identical bits (and, at W = 2, the bits of c10d's SUM / 2).  Phase
+// 3 hands out G exactly as reduce_kernel's blocks do (a float4 per lead
+// thread), so nsq is bitwise reduce_dp's.  The tag is the call count: block
+// b keeps its own counter in this rank's buffer and every call advances
+// every counter once, on every rank.  Waits are bounded (0.5 s of
+// s_memrealtime): a peer that never pushes sets the error word instead of
+// hanging the GPU.  Every block of every rank must be resident at once
+// (the grid is reduce_kernel's, a few blocks per CU).
+// ---------------------------------------------------------------------------
+constexpr int kPeerMaxW = 8, kPeerMaxBlocks = 1024;
+constexpr int64_t kPeerHdr = 4 * kPeerMaxBlocks + 256;           // epoch counters, error word
+struct PeerBufs {
+  unsigned long long* buf[kPeerMaxW];                              // every rank's buffer (this rank's own too)
+};
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+__host__ __device__ inline int64_t peer_slice(int64_t n, int world) { return (n + world - 1) / world; }
+__host__ __device__ inline int64_t peer_bytes(int64_t n, int world) {
+  return kPeerHdr + 2 * (int64_t)world * peer_slice(n, world) * 8;
+}
+
+__device__ __forceinline__ void peer_push(unsigned long long* base, int64_t word, unsigned tag, float v) {
+  __hip_atomic_store((gu64*)(base) + word, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// the value of a granule once its tag is `tag` (bounded wait)
+__device__ __forceinline__ float peer_pull(const unsigned long long* base, int64_t word, unsigned tag,
+                                           unsigned long long t0, bool& ok) {
+  const gu64* g = (const gu64*)(base) + word;
+  unsigned long long x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  while ((unsigned)(x >> 32) != tag) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) { ok = false; break; }   // 0.5 s at 100 MHz
+    __builtin_amdgcn_s_sleep(1);
+    x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  return __uint_as_float((unsigned)x);
+}
+
+__global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, int world, int rank, PeerBufs pb,
+                                                             float* __restrict__ G, double* __restrict__ nsq,
+                                                             double* __restrict__ steps) {
+  const Layout L = layout(H);
+  __shared__ double sh[8];
+  __shared__ unsigned tag_s;
+  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const int64_t n = L.total, sl = peer_slice(n, world);
+  unsigned long long* mine = pb.buf[rank];
+  const int64_t rs = kPeerHdr / 8, ag = rs + (int64_t)world * sl;  // word offsets of the two slot arrays
+  if (t == 0) {                                                    // this call's tag: block b's counter + 1
+    gu32* ep = (gu32*)(reinterpret_cast<unsigned*>(mine)) + b;
+    const unsigned e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+    __hip_atomic_store(ep, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    tag_s = e;
+  }
+  __syncthreads();
+  const unsigned tag = tag_s;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool ok = true;
+  // this thread's float4 of G, as reduce_kernel hands them out (lead threads)
+  int64_t col = -1;
+  if (b < g.nb2) {
+    if (t < 256 / kRedCH2) col = (int64_t)b * (256 / kRedCH2) + t;
+  } else if (b < g.nb2 + g.nb1) {
+    const int64_t c = (int64_t)(b - g.nb2) * (256 / kRedCH1) + t;
+    if (t < 256 / kRedCH1 && c < 2LL * H * 20 / 4) col = L.W1 / 4 + c;
+  } else {
+    const int64_t c = (int64_t)(b - g.nb2 - g.nb1) * (256 / kRedCHt) + t;
+    if (t < 256 / kRedCHt && c < L.tail / 4) col = L.b2 / 4 + c;
+  }
+  // 1: push this float4 to the owners' reduce-scatter slot [rank]
+  if (col >= 0) {
+    const float4 v = reinterpret_cast<const float4*>(G)[col];
+    const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = col * 4 + q, j = e / sl;
+      peer_push(pb.buf[j], rs + (int64_t)rank * sl + (e - j * sl), tag, e4[q]);
+    }
+  }
+  // 2: this rank's slice, summed in rank order, / world, to every gather slot [rank]
+  const int64_t mylen = min(sl, n - (int64_t)rank * sl);
+  for (int64_t k = (int64_t)b * 256 + t; k < mylen; k += (int64_t)nb * 256) {
+    float v = peer_pull(mine, rs + k, tag, t0, ok);
+    for (int j = 1; j < world; ++j) v += peer_pull(mine, rs + (int64_t)j * sl + k, tag, t0, ok);
+    v = v / (float)world;                                         // G.div_(world) (reduce_dp's IEEE division)
+    for (int j = 0; j < world; ++j) peer_push(pb.buf[j], ag + (int64_t)rank * sl + k, tag, v);
+  }
+  // 3: gather this float4 into G; its squares to the block's norm pair
+  double sa = 0.0, sc = 0.0;
+  if (col >= 0) {
+    float e4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = col * 4 + q, j = e / sl;
+      e4[q] = peer_pull(mine, ag + j * sl + (e - j * sl), tag, t0, ok);
+    }
+    const float4 v = make_float4(e4[0], e4[1], e4[2], e4[3]);
+    reinterpret_cast<float4*>(G)[col] = v;
+    const double q = sq4(v);
+    const bool crit = net_of(L, col * 4, H);
+    sa += crit ? 0.0 : q;
+    sc += crit ? q : 0.0;
+  }
+  if (!ok) {                                                       // a peer never pushed: flag it
+    gu64* err = (gu64*)(mine) + (4 * kPeerMaxBlocks) / 8;
+    __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  block_sum2(sa, sc, sh);
+  if (t == 0) {
+    nsq[2 * b] = sa;
+    nsq[2 * b + 1] = sc;
+    if (b == 0) { steps[0] += 1.0; steps[1] += 1.0; }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1466,6 +1599,71 @@ int satrl_ppo_reduce_dp(int H, int mb, int net, int world, float* G, double* nsq
   const RedGeom g = geom(H, mb, 1, net);
   hipLaunchKernelGGL(reduce_kernel, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, 2, nullptr, nullptr,
                      nullptr, G, nsq, steps, world);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int satrl_peer_buffer_bytes(int64_t n, int world, int64_t* bytes) {
+  if (n <= 0 || world < 1 || world > kPeerMaxW || !bytes) return -1;
+  *bytes = peer_bytes(n, world);
+  return 0;
+}
+
+int satrl_peer_alloc(int64_t bytes, void** buf, void* ipc_handle) {
+  if (bytes <= 0 || !buf || !ipc_handle) return -1;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) {
+    g_err = "satrl_peer_alloc: hipExtMallocWithFlags(uncached) failed";
+    return -2;
+  }
+  hipIpcMemHandle_t h;
+  if (hipMemset(p, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipIpcGetMemHandle(&h, p) != hipSuccess) {
+    (void)hipFree(p);
+    g_err = "satrl_peer_alloc: zeroing / hipIpcGetMemHandle failed";
+    return -2;
+  }
+  std::memcpy(ipc_handle, &h, sizeof(h));
+  *buf = p;
+  return 0;
+}
+
+int satrl_peer_open(const void* ipc_handle, void** buf) {
+  if (!ipc_handle || !buf) return -1;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, ipc_handle, sizeof(h));
+  if (hipIpcOpenMemHandle(buf, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    g_err = "satrl_peer_open: hipIpcOpenMemHandle failed";
+    return -2;
+  }
+  return 0;
+}
+
+int satrl_peer_close(void* buf) { return buf && hipIpcCloseMemHandle(buf) == hipSuccess ? 0 : -2; }
+int satrl_peer_free(void* buf) { return buf && hipFree(buf) == hipSuccess ? 0 : -2; }
+
+int satrl_peer_error(const void* buf, uint64_t* err) {
+  if (!buf || !err) return -1;
+  return hipMemcpy(err, static_cast<const char*>(buf) + 4 * kPeerMaxBlocks, 8, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -2;
+}
+
+int satrl_ppo_allreduce_peer(int H, int mb, int world, int rank, void* const* bufs, float* G, double* nsq,
+                             double* steps, void* stream) {
+  if (!valid_h(H) || mb <= 0 || world < 1 || world > kPeerMaxW || rank < 0 || rank >= world || !bufs || !G || !nsq ||
+      !steps)
+    return -1;
+  PeerBufs pb{};
+  for (int j = 0; j < world; ++j) {
+    if (!bufs[j]) return -1;
+    pb.buf[j] = static_cast<unsigned long long*>(bufs[j]);
+  }
+  const RedGeom g = geom(H, mb, 1, -1);
+  const int nb = n_blocks(g);
+  if (nb > kPeerMaxBlocks) return -1;
+  hipLaunchKernelGGL(peer_allreduce_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, H, g, world, rank, pb, G, nsq,
+                     steps);
   LAUNCH_CHECK();
   return 0;
 }

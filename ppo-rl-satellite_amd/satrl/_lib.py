@@ -123,6 +123,13 @@ _SIGS = {
     "satrl_ppo_row_blocks": ([C.c_int, C.c_int], C.c_int),
     "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                                _vp, _vp, _vp], C.c_int),
+    "satrl_peer_buffer_bytes": ([_i64, C.c_int, _vp], C.c_int),
+    "satrl_peer_alloc": ([_i64, _vp, _vp], C.c_int),
+    "satrl_peer_open": ([_vp, _vp], C.c_int),
+    "satrl_peer_close": ([_vp], C.c_int),
+    "satrl_peer_free": ([_vp], C.c_int),
+    "satrl_peer_error": ([_vp, _vp], C.c_int),
+    "satrl_ppo_allreduce_peer": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_policy_act": ([C.c_int, _i64, _vp, _vp, _vp, C.c_float, C.c_uint64, _i64, C.c_uint64, _vp, _vp, _vp, _vp,
                           _vp, _vp], C.c_int),
     "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),
@@ -160,7 +167,8 @@ def check(rc: int, what: str):
         L = lib()
         msg = (L.satenv_cpu_last_error() if what.startswith("satenv_cpu") else
                L.satenv_last_error() if what.startswith("satenv") else
-               L.satrl_ppo_last_error() if what.startswith("satrl_ppo") else L.satrl_last_error()).decode()
+               L.satrl_ppo_last_error() if what.startswith(("satrl_ppo", "satrl_peer")) else
+               L.satrl_last_error()).decode()
         raise NativeError(f"{what} failed ({rc}): {msg}")
 
 

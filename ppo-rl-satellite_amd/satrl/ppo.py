@@ -474,12 +474,15 @@ class FusedMinibatch:
             check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        None, None, sp), "satrl_ppo_reduce")
             # one bucket, both nets: SUM over the ranks, then G /= world and the norms in one launch
-            if L.comm is not None:
+            if L.peer is not None and net < 0:
+                L.peer.all_reduce_dp_(H, mb, L.G, nsq, L.steps)              # peer kernel, reduce_dp fused
+            elif L.comm is not None:
                 L.comm.all_reduce_sum_(L.G)                                   # RCCL on this stream (capturable)
             else:
                 _dist.sum_inplace_(L.G, L.pg)                                 # c10d (gloo in the CPU tests)
-            check(lib.satrl_ppo_reduce_dp(H, mb, net, _dist.world_size(L.pg), ptr(L.G), ptr(nsq), ptr(L.steps), sp),
-                  "satrl_ppo_reduce_dp")
+            if L.peer is None or net >= 0:
+                check(lib.satrl_ppo_reduce_dp(H, mb, net, _dist.world_size(L.pg), ptr(L.G), ptr(nsq), ptr(L.steps),
+                                              sp), "satrl_ppo_reduce_dp")
         check(lib.satrl_ppo_adam(H, mb, net, ptr(nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
                                  float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
                                  ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
@@ -558,7 +561,8 @@ class FusedMinibatch:
         nfull = B // mb
         if B % mb:
             self.plan_shape(B % mb)          # the ragged tail's dW2 plan, before any step of the epoch
-        graphable = self.use_graph and torch.cuda.is_available() and (self.L.pg is None or self.L.comm is not None)
+        graphable = self.use_graph and torch.cuda.is_available() and (self.L.pg is None or self.L.comm is not None
+                                                                       or self.L.peer is not None)
         k = 0
         if graphable and nfull >= G:
             if self.perm_buf is None or self.perm_buf.numel() < B:
@@ -643,7 +647,15 @@ class PPOLearner:
         self.pg = pg
         # RCCL communicator for the in-graph gradient all-reduce (None without a
         # process group, or on gloo: the c10d all-reduce then runs eagerly)
-        self.comm = _rccl.for_group(pg, self.device) if pg is not None and self.device.type == "cuda" else None
+        mode = getattr(args, "allreduce", "rccl")
+        if mode not in ("rccl", "peer"):
+            raise ValueError("allreduce must be 'rccl' or 'peer'")
+        on_gpus = pg is not None and self.device.type == "cuda"
+        self.comm = _rccl.for_group(pg, self.device) if on_gpus and mode == "rccl" else None
+        self.peer = None
+        if on_gpus and mode == "peer":
+            from .peer import PeerComm
+            self.peer = PeerComm(pg, ppo_layout(int(args.hidden_width))["total"], self.device)
         self.graph_group = graph_group
         self.use_graph = use_graph
         # CPU init with the reference's RNG consumption order (actor, then critic)
@@ -757,6 +769,8 @@ class PPOLearner:
             else:
                 perm = perms(ep) if callable(perms) else perms[ep]     # a callable draws each epoch's order lazily
             st.run(src, perm)
+        if self.peer is not None:
+            self.peer.check()                # a peer's value never arrived: the update is invalid
         if self.use_lr_decay:
             self.lr_decay(total_steps)
 

@@ -36,7 +36,7 @@ class args_param:  # noqa: N801
                  use_lr_decay=True, use_grad_clip=True, use_orthogonal_init=True, set_adam_eps=True, use_tanh=True,
                  chkpt_dir="/mnt/datab/home/yuanwenzheng/PICTURE1",
                  num_envs=1, horizon=None, seed=0, rollout_graph_chunk=64, update_graph_group=64, device=None,
-                 surrogate=False, dp_minibatch="global", minibatch_sampler=None):
+                 surrogate=False, dp_minibatch="global", minibatch_sampler=None, allreduce="rccl"):
         self.max_train_steps = max_train_steps
         self.evaluate_freq = evaluate_freq
         self.save_freq = save_freq
@@ -89,6 +89,11 @@ class args_param:  # noqa: N801
         # global minibatches (None: uniform on one process, stratified under
         # "global" data parallelism)
         self.minibatch_sampler = minibatch_sampler
+        # the per-minibatch gradient all-reduce under data parallelism on GPUs:
+        # "rccl" (ncclAllReduce + reduce_dp, in the update's graphs) or "peer"
+        # (satrl_ppo_allreduce_peer: a two-shot reduce-scatter + all-gather
+        # over IPC-mapped buffers, fused with reduce_dp; satrl/peer.py)
+        self.allreduce = allreduce
         # set by the train_* functions from the env (CPPO_main.py:99-101)
         self.state_dim = 18
         self.action_dim = 3

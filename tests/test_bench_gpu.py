@@ -15,14 +15,19 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_ranks_one_device():
+@pytest.mark.parametrize("allreduce", ["rccl", "peer"])
+def test_bench_two_ranks_one_device(allreduce):
+    """... and with --allreduce peer the whole update runs through the peer
+    all-reduce kernel (IPC within the device); either way the line carries
+    the peer kernel's all-reduce time beside the c10d path."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--one-device",
                         "--num-envs", "512", "--horizon", "32", "--epochs", "1", "--minibatch", "4096",
                         "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--kernel-iters", "10",
-                        "--global-slice", "8"], env=env, capture_output=True, text=True, timeout=240)
+                        "--global-slice", "8", "--allreduce", allreduce], env=env, capture_output=True, text=True,
+                       timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -33,6 +38,7 @@ def test_bench_two_ranks_one_device():
     assert dp["world"] == 2 and dp["backend"] == "gloo"
     sl = dp["configs3_semantics_slice"]
     assert sl["rows_per_rank"] == 2048 and sl["us_per_global_minibatch_step"] > 0
+    assert dp["allreduce"] == allreduce and dp["peer_allreduce_error"] is False and dp["peer_allreduce_us"] > 0
 
 
 def test_bench_one_gpu_line_keeps_the_contract():

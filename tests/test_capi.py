@@ -20,6 +20,7 @@ def test_headers_declare_expected_entry_points():
             "satenv_get_state", "satenv_set_state", "satenv_last_error"} <= env
     assert {"satrl_gae", "satrl_gaussian_sample", "satrl_moments"} <= _declared("satrl_rollout.h")
     assert {"satrl_ppo_rowpass", "satrl_ppo_reduce", "satrl_ppo_adam", "satrl_ppo_layout"} <= _declared("satrl_ppo.h")
+    assert {"satrl_peer_alloc", "satrl_peer_open", "satrl_ppo_allreduce_peer"} <= _declared("satrl_peer.h")
     # the host build exports every env entry point of satenv.h it restates, same signature, satenv_cpu_ prefix
     cpu = _declared("satenv_cpu.h")
     assert {n.replace("satenv_", "satenv_cpu_", 1) for n in ("satenv_create", "satenv_destroy", "satenv_num_envs",
@@ -33,7 +34,7 @@ def test_library_exports_every_declared_symbol():
         L.build()
     lib = L.lib()          # loads with torch's HIP runtime; no device needed
     declared = (_declared("satenv.h") | _declared("satenv_cpu.h") | _declared("satrl_rollout.h") |
-                _declared("satrl_ppo.h"))
+                _declared("satrl_ppo.h") | _declared("satrl_peer.h"))
     for name in sorted(declared):
         assert hasattr(lib, name), name
     assert set(L.exported_symbols()) == declared

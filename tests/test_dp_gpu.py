@@ -314,3 +314,111 @@ def test_comm_wait_deadline_and_async_error_raise():
     with pytest.raises(rccl.CommError, match="asynchronous error"):
         c.wait(60.0)
     torch.cuda.synchronize()
+
+
+def _peer_rank(rank, port, q):
+    """World 2 on one device: the peer all-reduce (satrl_ppo_allreduce_peer,
+    IPC-mapped buffers) against c10d's SUM / world + satrl_ppo_reduce_dp, on
+    a raw gradient and through whole DP updates (eager and graph-replayed)."""
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        sys.path.insert(0, PKG_DIR)
+        import satrl._lib as _L
+        from satrl.ppo import PPOLearner
+        from satrl.trainer import args_param
+        out = {}
+        # (1) one raw gradient bucket: peer kernel vs gloo SUM + reduce_dp
+        args = args_param(hidden_width=256, mini_batch_size=512, batch_size=B, chkpt_dir="/tmp", allreduce="peer")
+        Lp = PPOLearner(args, "pursuer", device="cuda:0", pg=dist.group.WORLD, use_graph=False)
+        assert Lp.peer is not None and Lp.comm is None
+        g = torch.Generator(device="cuda:0").manual_seed(100 + rank)
+        G0 = torch.randn(Lp.G.numel(), device="cuda:0", generator=g)
+        st = Lp.stepper(512)
+        nsq_p = torch.zeros_like(st.nsq[0])
+        steps_p = torch.zeros(2, dtype=torch.float64, device="cuda:0")
+        Gp = G0.clone()
+        for _ in range(3):                                  # three calls: tags advance, buffers reused
+            Gp.copy_(G0)
+            Lp.peer.all_reduce_dp_(256, 512, Gp, nsq_p, steps_p)
+        torch.cuda.synchronize()
+        Gg = G0.clone().cpu()
+        dist.all_reduce(Gg)
+        Gg = Gg.cuda()
+        nsq_g = torch.zeros_like(nsq_p)
+        steps_g = torch.full((2,), 2.0, dtype=torch.float64, device="cuda:0")
+        _L.check(_L.lib().satrl_ppo_reduce_dp(256, 512, -1, 2, _L.ptr(Gg), _L.ptr(nsq_g), _L.ptr(steps_g),
+                                              _L.stream_ptr()), "satrl_ppo_reduce_dp")
+        torch.cuda.synchronize()
+        out["raw"] = (torch.equal(Gp, Gg), torch.equal(nsq_p, nsq_g), torch.equal(steps_p, steps_g), Gp.cpu().numpy())
+        assert Lp.peer.error() == 0
+        # (2) DP updates, H 64: peer path (graph-replayed and eager) vs the gloo path
+        res = {}
+        for mode, graph in (("peer", True), ("peer", False), ("rccl", False)):
+            torch.manual_seed(11)
+            a2 = args_param(hidden_width=H, mini_batch_size=MB, batch_size=B, chkpt_dir="/tmp", allreduce=mode,
+                            K_epochs=2)
+            L = PPOLearner(a2, "pursuer", device="cuda:0", pg=dist.group.WORLD, graph_group=2, use_graph=graph)
+            gg = torch.Generator(device="cuda:0").manual_seed(7 + rank)
+            src = torch.randn((B, 32), device="cuda:0", generator=gg)
+            src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda:0", generator=gg)
+            L.sync_w2t()
+            pg = torch.Generator(device="cuda:0").manual_seed(3)
+            L.update_packed(src, 0.0, perms=[torch.randperm(B, device="cuda:0", generator=pg)[:5 * MB + 37]
+                                             for _ in range(2)])
+            torch.cuda.synchronize()
+            res[(mode, graph)] = (L.P.clone(), L.M.clone(), L.V.clone(), L.steps.clone())
+            if L.peer is not None:
+                assert L.peer.error() == 0
+                L.peer.close()
+        same = [all(torch.equal(a, b) for a, b in zip(res[("peer", True)], res[k]))
+                for k in (("peer", False), ("rccl", False))]
+        out["update"] = (same, res[("peer", True)][0].cpu().numpy())
+        Lp.peer.close()
+        q.put((rank, out))
+    except BaseException:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peer_allreduce_world2_one_device():
+    """satrl_ppo_allreduce_peer over two ranks on one GPU (IPC within the
+    device): bitwise c10d's SUM / world and reduce_dp's norms and step
+    counters on a raw gradient over three calls, bitwise identical on both
+    ranks; whole DP updates (2 epochs of 5 minibatches + a ragged tail,
+    graph-replayed and eager) bitwise equal to the gloo-all-reduce path."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ps = [ctx.Process(target=_peer_rank, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    import queue
+    import time
+    res, t_end = {}, time.monotonic() + 150
+    while len(res) < 2 and time.monotonic() < t_end:
+        try:
+            r, v = q.get(timeout=2)
+            assert not isinstance(v, str), f"rank {r}:\n{v}"
+            res[r] = v
+        except queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in ps):
+                break
+    for p in ps:
+        p.join(timeout=30)
+        if p.exitcode is None:
+            p.kill()
+    assert len(res) == 2 and all(p.exitcode == 0 for p in ps), ([p.exitcode for p in ps], sorted(res))
+    for r in (0, 1):
+        eqG, eqN, eqS, _ = res[r]["raw"]
+        assert eqG and eqN and eqS, (r, eqG, eqN, eqS)
+        assert all(res[r]["update"][0]), (r, res[r]["update"][0])
+    import numpy as np
+    assert np.array_equal(res[0]["raw"][3], res[1]["raw"][3])
+    assert np.array_equal(res[0]["update"][1], res[1]["update"][1])
