@@ -60,7 +60,7 @@ def parse():
                     help="N > 1: the update's per-minibatch gradient all-reduce: RCCL (ncclAllReduce + reduce_dp in "
                          "the graphs) or the peer kernel (satrl_ppo_allreduce_peer: two-shot over IPC-mapped "
                          "buffers, fused with reduce_dp); the line times the other one beside it")
-    ap.add_argument("--profile-tag", default="r3", help="profiles/<tag>_* files the rocprof cross-check fields read")
+    ap.add_argument("--profile-tag", default="r4", help="profiles/<tag>_* files the rocprof cross-check fields read")
     ap.add_argument("--global-slice", type=int, default=256,
                     help="N > 1: minibatches of the configs[3]-semantics slice timed after the run (global "
                          "minibatch --minibatch, i.e. --minibatch/N rows per rank per Adam step); 0 = off")
@@ -483,13 +483,17 @@ def run(a, world):
     b2b_us = e0.elapsed_time(e1) * 1e3 / a.kernel_iters
     # rocprof cross-checks from the committed profiles of this command / the PMC workloads
     # the committed kernel stats profile the default command (1 GPU, 16384 envs,
-    # H 256, mb 4096): other shapes time other launches, so they fall back to
-    # the live figures
+    # H 256, mb 4096; profiles/<tag>_bench_kernel_stats.csv) and configs[1] (4096
+    # envs, H 64, mb 4096; ..._bench_configs1_kernel_stats.csv): other shapes time
+    # other launches, so they fall back to the live figures
     profiled_shape = world == 1 and a.num_envs == 16384 and a.hidden == 256 and mb_local == 4096
+    ks_suffix = {(1, 16384, 256, 4096): "", (1, 4096, 64, 4096): "_configs1"}.get(
+        (world, a.num_envs, a.hidden, mb_local))
+    ks_file = (os.path.join(ROOT, "profiles", f"{a.profile_tag}_bench{ks_suffix}_kernel_stats.csv")
+               if ks_suffix is not None else None)
 
     def prof_avg_us(kname):
-        ks_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_bench_kernel_stats.csv")
-        if not profiled_shape or not os.path.exists(ks_file):
+        if ks_file is None or not os.path.exists(ks_file):
             return None
         import csv
         with open(ks_file) as f:
@@ -513,16 +517,17 @@ def run(a, world):
     # the rollout's policy kernel (both agents' forward, the (num_envs x hidden)
     # GEMMs): per row and agent fc1 2*18*H + H, fc2 2*H*H + H, mean layer 2*3*H + 3
     policy_roof = None
-    pol_us = prof_avg_us("policy_kernel<%d;16;0>" % a.hidden)
+    pol_us = prof_avg_us("policy_kernel<%d;%d;0>" % (a.hidden, a.hidden // 16))
     if pol_us:
         pol_flop = 2 * a.num_envs * (2 * 18 * a.hidden + a.hidden + 2 * a.hidden * a.hidden + a.hidden
                                      + 2 * 3 * a.hidden + 3)
         pol_tfs = pol_flop / (pol_us * 1e-6) / 1e12
-        policy_roof = {"kernel": f"policy_kernel<{a.hidden},16,0> (both agents' choose_action, f32 MFMA)",
+        policy_roof = {"kernel": f"policy_kernel<{a.hidden},{a.hidden // 16},0> (both agents' choose_action, "
+                                 "f32 MFMA)",
                        "bound": "mfma", "achieved": pol_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                        "frac": pol_tfs / FP32_MFMA_PEAK_TFS, "avg_launch_us": pol_us, "flop_per_launch": pol_flop,
                        "timing": f"rocprofv3 average over the rollout's launches "
-                                 f"(profiles/{a.profile_tag}_bench_kernel_stats.csv)"}
+                                 f"(profiles/{os.path.basename(ks_file)})"}
         pol_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_policy_mfma_pmc.json")
         if os.path.exists(pol_file):
             with open(pol_file) as f:
@@ -858,8 +863,9 @@ def run(a, world):
                          "minibatch_step_us": t_chain,
                          "event_bracketed_avg_launch_us": rowpass_ev_us, "event_bracketed_median_us": rowpass_med,
                          "rocprof_avg_launch_us": rowpass_prof_us,
-                         "rocprof_source": f"profiles/{a.profile_tag}_bench_kernel_stats.csv (rocprofv3 average over "
-                                           "all rowpass launches of this command, nearly all in the update's graphs)",
+                         "rocprof_source": (f"profiles/{os.path.basename(ks_file)} (rocprofv3 average over all rowpass "
+                                            "launches of this command, nearly all in the update's graphs)"
+                                            if ks_file else None),
                          "back_to_back_avg_launch_us": b2b_us,
                          "back_to_back_frac": rowpass_flop / (b2b_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS,
                          "traffic_source": f"profiles/{a.profile_tag}_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "

@@ -44,11 +44,16 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/env_swee
 python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$ROOT/profiles"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o run -- \
     python3 "$ROOT/bench.py" --profile-tag "$TAG" > "$OUT/bench.json" 2> "$OUT/bench.err"
-rm -f "$OUT/bench/run_kernel_trace.csv" "$OUT/env_rollout/run_kernel_trace.csv"
+# BASELINE configs[1] (4096 envs, H 64): its own kernel stats for its roofline line
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_configs1" -o run -- \
+    python3 "$ROOT/bench.py" --num-envs 4096 --hidden 64 --no-cpu-baseline --profile-tag "$TAG" \
+    > "$OUT/bench_configs1.json" 2> "$OUT/bench_configs1.err"
+rm -f "$OUT/bench/run_kernel_trace.csv" "$OUT/bench_configs1/run_kernel_trace.csv" "$OUT/env_rollout/run_kernel_trace.csv"
 # the committed summaries first, then this run's (the fresh bench stats must win)
 mkdir -p "$OUT/profiles"
 cp "$ROOT"/profiles/"${TAG}"_*.json "$OUT/profiles/" 2>/dev/null || true
 cp "$ROOT"/profiles/"${TAG}"_*.csv "$OUT/profiles/" 2>/dev/null || true
 python3 "$W/summarize_profiles.py" "$OUT" "$TAG" "$OUT/profiles"
 cp "$OUT/profiles/${TAG}_bench_kernel_stats.csv" "$ROOT/profiles/"
+cp "$OUT/profiles/${TAG}_bench_configs1_kernel_stats.csv" "$ROOT/profiles/" 2>/dev/null || true
 tail -1 "$OUT/bench.json"

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU box: the whole -m gpu suite, then the r4 profile round (counter passes, env
+# traces, bench under kernel stats) and an unprofiled bench reading the fresh profiles.
+set -euo pipefail
+ROOT=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$ROOT"
+mkdir -p gpurun_out
+( while true; do date >> gpurun_out/heartbeat.log; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null || true' EXIT
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      > gpurun_out/r4_gpu_tests.log 2>&1
+fi
+timeout -k 10 1500 bash tools/profile_round.sh r4 > gpurun_out/r4_profile.log 2>&1
+timeout -k 10 400 python3 bench.py --profile-tag r4 > gpurun_out/r4_bench.json 2> gpurun_out/r4_bench.err
+timeout -k 10 300 python3 bench.py --num-envs 4096 --hidden 64 --no-cpu-baseline --profile-tag r4 \
+    > gpurun_out/r4_bench_configs1.json 2> gpurun_out/r4_bench_configs1.err
+tail -c 400 gpurun_out/r4_bench.json

@@ -42,6 +42,9 @@ def main():
     ks = os.path.join(d, "bench", "run_kernel_stats.csv")
     if os.path.exists(ks):
         kernel_stats(ks, os.path.join(prof, f"{tag}_bench_kernel_stats.csv"))
+    ks = os.path.join(d, "bench_configs1", "run_kernel_stats.csv")      # BASELINE configs[1]'s bench command
+    if os.path.exists(ks):
+        kernel_stats(ks, os.path.join(prof, f"{tag}_bench_configs1_kernel_stats.csv"))
     fetch = os.path.join(d, "pmc_fetch", "run_counter_collection.csv")
     write = os.path.join(d, "pmc_write", "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
