@@ -35,4 +35,5 @@ for mb in [int(x) for x in sys.argv[1:]] or [4096]:
     e1.record()
     torch.cuda.synchronize()
     print(f"H {H} mb {mb:5d}: {e0.elapsed_time(e1) * 1e3 / (n * 16):7.2f} us per minibatch step "
-          f"(SATRL_RP_SHORT_MB={os.environ.get('SATRL_RP_SHORT_MB', 'default')})", flush=True)
+          f"(SATRL_RP_SHORT_MB={os.environ.get('SATRL_RP_SHORT_MB', 'default')}, "
+          f"SATRL_FUSED_ADAM={os.environ.get('SATRL_FUSED_ADAM', 'default')})", flush=True)

@@ -34,7 +34,10 @@ def run():
 
 
 def short(name):
-    for k in ("rowpass", "reduce_kernel", "adam_kernel", "dw2_kernel", "Cijk", "gather", "copy"):
+    if "rowpass" in name and "true, true>" in name.replace(";", ","):
+        return "rowpass_adam"
+    for k in ("rowpass", "reduce_kernel", "reduce_apply_kernel<true", "reduce_apply_kernel<false", "adam_kernel",
+              "steps_advance", "dw2_kernel", "Cijk", "gather", "copy"):
         if k in name:
             return k
     return name[:40]
