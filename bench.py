@@ -511,10 +511,7 @@ def run(a, world):
                 return d["hbm_bytes_per_launch"]
         return None
 
-    # the update's rowpass: at H 64 the deferred-Adam variant (all but each
-    # graph group's first launch)
-    rowpass_prof_us = prof_avg_us("rowpass_kernel<64;4;32;true;true>" if st.fused_adam else
-                                  "rowpass_kernel<%d" % a.hidden)
+    rowpass_prof_us = prof_avg_us("rowpass_kernel<%d" % a.hidden)
     head_us = rowpass_prof_us if rowpass_prof_us else rowpass_us
     traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
     # the rollout's policy kernel (both agents' forward, the (num_envs x hidden)
@@ -844,10 +841,7 @@ def run(a, world):
             "env_kernel_env_steps_per_s": a.num_envs / (env_us * 1e-6),
             "minibatch_steps_per_s": n_minibatches / (update_ms * 1e-3),
             "episodes_finished_total": float(stats[0]),
-            "roofline": {"kernel": (f"satrl_ppo_rowpass_dw2_adam<{a.hidden},{a.hidden // 16}> (hand-written HIP, "
-                                    "f32 MFMA 16x16x4; the dW2 product and the deferred Adam step fused in)"
-                                    if st.fused_adam else
-                                    f"satrl_ppo_rowpass_dw2<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA "
+            "roofline": {"kernel": (f"satrl_ppo_rowpass_dw2<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA "
                                     "16x16x4; the dW2 product fused in)" if st.fused_dw2 else
                                     f"satrl_ppo_rowpass<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA 16x16x4)"),
                          "bound": "mfma",

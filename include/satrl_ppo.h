@@ -9,8 +9,7 @@
  * minibatch rows.  Per minibatch: satrl_ppo_rowpass (everything that is
  * row-parallel, incl. the two H x H products on f32 MFMA), satrl_ppo_dw2
  * (the dW2 weight gradient, split-K over rows), satrl_ppo_reduce and
- * satrl_ppo_adam (at H = 64: satrl_ppo_rowpass_dw2_adam and
- * satrl_ppo_reduce_apply, two launches, with the Adam step deferred into them).
+ * satrl_ppo_adam.
  *
  * Flat parameter / gradient / Adam-moment layout (f32, see satrl_ppo_layout):
  *   W2   [2][H][H]     fc2.weight (actor, critic)
@@ -141,44 +140,6 @@ int satrl_ppo_row_blocks(int H, int mb);
 int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
                           const float* W2T, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
                           float* pw1, void* stream);
-
-/* H = 64, deferred Adam: the minibatch step in TWO launches.  Step k's
- * gradient G (and its norm partials) is not applied by a launch of its own:
- * the rowpass of step k+1 applies clip_grad_norm_ + Adam to its net's
- * parameters on the fly into LDS (every workgroup the same bits) and runs on
- * them, and the reduce of step k+1 applies the same step to P / M / V in
- * memory, element by element, just before it overwrites G with step k+1's
- * gradient.  The step count of the pending step is steps[net] + dk (the
- * steps counters are not advanced by these calls: satrl_ppo_steps_advance
- * once per group, then satrl_ppo_adam applies the group's last step).  Every
- * value is bitwise the one satrl_ppo_adam computes, so a group stepped this
- * way ends with the P / M / V / W2T of rowpass_dw2 | reduce | adam steps
- * (tested).  W2T is NOT kept current by these calls (only by satrl_ppo_adam).
- * nsq: the pending step's norm partials (satrl_ppo_reduce's), which the
- * reduce of the next step must not overwrite: alternate two buffers.       */
-typedef struct satrl_ppo_adam_pending {
-  const double* nsq;   /* [n_norm_blocks][2] of the pending step            */
-  const double* steps; /* [2] Adam step counters; the pending step is + dk  */
-  int dk;
-  const double* bct;   /* as satrl_ppo_adam                                 */
-  int bct_len;
-  const float* lr;     /* [2]                                               */
-  float beta1, beta2, eps, max_norm;
-  int use_clip;
-} satrl_ppo_adam_pending;
-/* pend NULL: satrl_ppo_rowpass_dw2.  G / M / V: the pending gradient and moments. */
-int satrl_ppo_rowpass_dw2_adam(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                               const float* W2T, float epsilon, float ent_coef, float max_action,
-                               const satrl_ppo_adam_pending* pend, const float* G, const float* M, const float* V,
-                               float* p2, float* ptail, float* pw1, void* stream);
-/* satrl_ppo_reduce mode 3 for both nets without advancing steps, writing the
- * norm partials to nsq_out; with pend (nullable) it first applies the pending
- * step held in G to P / M / V (pend->nsq must not be nsq_out).             */
-int satrl_ppo_reduce_apply(int H, int mb, int S, const float* p2, const float* p1, const float* pt,
-                           const satrl_ppo_adam_pending* pend, float* G, float* P, float* M, float* V, double* nsq_out,
-                           void* stream);
-/* steps[0] += n, steps[1] += n                                             */
-int satrl_ppo_steps_advance(double* steps, int n, void* stream);
 
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result
  * is independent of N and of the sharding, and the rollout's log-probs equal

@@ -29,7 +29,7 @@ thread_local std::string g_err;
 #ifdef SATRL_PHASE_PROBE
 // development-only phase stamps (tools/_probe/phase_probe.py), never in the
 // shipped build: [workgroup][stamp][wave][s_memrealtime, s_memtime]
-__device__ unsigned long long g_probe[512][24][16][2];
+__device__ unsigned long long g_probe[512][16][16][2];
 #define PHASE_PROBE(k)                                                        \
   do {                                                                        \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 512) {                        \
@@ -77,159 +77,6 @@ __device__ __forceinline__ int net_of(const Layout& L, int64_t e, int H) {
   if (e < L.W3a) return (e - L.b2) >= H;
   return e >= L.W3c;
 }
-
-// ---------------------------------------------------------------------------
-// float4 / f64 reduction helpers (reduce, adam, and the deferred Adam step)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-// IEEE division per component, as torch's G.div_(world) after the all-reduce
-__device__ __forceinline__ float4 f4div(float4 a, float d) {
-  return make_float4(a.x / d, a.y / d, a.z / d, a.w / d);
-}
-__device__ __forceinline__ double sq4(float4 v) {
-  return (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-}
-
-template <int CH>
-__device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, int64_t stride4, int nparts,
-                                             int64_t col, bool valid, float4* red) {
-  constexpr int EB = 256 / CH;
-  const int t = threadIdx.x, e = t % EB, c = t / EB;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid) {
-#pragma unroll 16
-    for (int w = c; w < nparts; w += CH) s = f4add(s, part[(int64_t)w * stride4 + col]);
-  }
-  red[t] = s;
-  __syncthreads();
-  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c == 0) {
-    // the CH partials in order; their LDS reads go out 8 at a time ahead of
-    // the adds (one read round trip per 8, not per 2)
-    constexpr int KB = CH < 8 ? CH : 8;
-#pragma unroll
-    for (int k0 = 0; k0 < CH; k0 += KB) {
-      float4 part[KB];
-#pragma unroll
-      for (int k = 0; k < KB; ++k) part[k] = red[(k0 + k) * EB + e];
-#pragma unroll
-      for (int k = 0; k < KB; ++k) tot = f4add(tot, part[k]);
-    }
-  }
-  return tot;
-}
-
-// block-level f64 pair sum in fixed order, result in every thread
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double lane_d(double v, int lane) {
-  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
-                          __builtin_amdgcn_readlane(__double2loint(v), lane));
-}
-// wave sum of (a, c) in a fixed order: DPP sums of each 16-lane row (the
-// row16_sum stages), then rows 0..3 by readlane -- no ds_bpermute round trips
-__device__ __forceinline__ void wave_sum2(double& a, double& c) {
-  a += dpp_d<0xB1>(a); c += dpp_d<0xB1>(c);
-  a += dpp_d<0x4E>(a); c += dpp_d<0x4E>(c);
-  a += dpp_d<0x141>(a); c += dpp_d<0x141>(c);
-  a += dpp_d<0x140>(a); c += dpp_d<0x140>(c);
-  a = ((lane_d(a, 0) + lane_d(a, 16)) + lane_d(a, 32)) + lane_d(a, 48);
-  c = ((lane_d(c, 0) + lane_d(c, 16)) + lane_d(c, 32)) + lane_d(c, 48);
-}
-__device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
-  wave_sum2(a, c);
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sh[2 * w] = a; sh[2 * w + 1] = c; }
-  __syncthreads();
-  a = 0.0; c = 0.0;
-  for (int k = 0; k < nw; ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
-}
-
-__device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float step_size,
-                                           float bc2s, float w1, float w2, float beta2, float eps, int use_clip) {
-  if (use_clip) g = g * coef;                                      // grads.mul_(clip_coef_clamped)
-  m = m + w1 * (g - m);                                            // exp_avg.lerp_(grad, 1 - beta1)
-  v = v * beta2 + w2 * (g * g);                                    // mul_(beta2).addcmul_(g, g, 1 - beta2)
-  const float denom = sqrtf(v) / bc2s + eps;
-  return p + (-step_size) * (m / denom);                           // addcdiv_(m, denom, -step_size)
-}
-
-// ---------------------------------------------------------------------------
-// Deferred Adam step (H = 64: satrl_ppo_rowpass_dw2_adam, satrl_ppo_reduce_apply):
-// adam_kernel's norm fold, per-net constants and per-element update as
-// functions, so every kernel that applies a pending step computes
-// adam_kernel's bits.  The fold is adam_kernel's: thread t of a 256-thread
-// block sums partials t, t + 256, t + 512, t + 768 (masked past nblk), then
-// block_sum2 -- the same order, hence the same (a, c), in every block.
-// ---------------------------------------------------------------------------
-struct AdamK {
-  float coef, ss, b2s, w1, w2;
-};
-__device__ __forceinline__ void adam_fold_load(const double* __restrict__ nsq, int nblk, double2 (&pn2)[4]) {
-  const double2* nsq2 = reinterpret_cast<const double2*>(nsq);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) pn2[i] = nsq2[min((int)threadIdx.x + 256 * i, nblk - 1)];
-}
-__device__ __forceinline__ void adam_fold(const double* __restrict__ nsq, int nblk, const double2 (&pn2)[4],
-                                          double& a, double& c, double* sh) {
-  const int t = threadIdx.x;
-  a = 0.0;
-  c = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const double in = t + 256 * i < nblk ? 1.0 : 0.0;
-    a += pn2[i].x * in;
-    c += pn2[i].y * in;
-  }
-  if (nblk > 1024) {
-    for (int k = t + 1024; k < nblk; k += 256) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
-  }
-  block_sum2(a, c, sh);
-}
-// clip coefficient and step constants of `net` for the pending step (count steps[net] + dk)
-__device__ __forceinline__ AdamK adam_consts(const satrl_ppo_adam_pending& A, int net, double a, double c) {
-  AdamK k;
-  const double nn = net == 0 ? a : c;
-  const float nrm = (float)sqrt(nn);
-  k.coef = A.use_clip ? fminf(A.max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
-  const int st = (int)A.steps[net] + A.dk;
-  const double bc1 = st < A.bct_len ? A.bct[2 * st] : 1.0;
-  const double bc2s = st < A.bct_len ? A.bct[2 * st + 1] : 1.0;
-  k.ss = (float)((double)A.lr[net] / bc1);
-  k.b2s = (float)bc2s;
-  k.w1 = (float)(1.0 - (double)A.beta1);
-  k.w2 = (float)(1.0 - (double)A.beta2);
-  return k;
-}
-__device__ __forceinline__ float4 adam4(const AdamK& k, const satrl_ppo_adam_pending& A, float4 g, float4& m,
-                                        float4& v, float4 p) {
-  float4 pn;
-  pn.x = adam_elem(g.x, m.x, v.x, p.x, k.coef, k.ss, k.b2s, k.w1, k.w2, A.beta2, A.eps, A.use_clip);
-  pn.y = adam_elem(g.y, m.y, v.y, p.y, k.coef, k.ss, k.b2s, k.w1, k.w2, A.beta2, A.eps, A.use_clip);
-  pn.z = adam_elem(g.z, m.z, v.z, p.z, k.coef, k.ss, k.b2s, k.w1, k.w2, A.beta2, A.eps, A.use_clip);
-  pn.w = adam_elem(g.w, m.w, v.w, p.w, k.coef, k.ss, k.b2s, k.w1, k.w2, A.beta2, A.eps, A.use_clip);
-  return pn;
-}
-
-// One net's parameters after the pending step, in LDS (the rowpass of the
-// deferred-Adam step): fc2.weight row-major and transposed (rows padded by
-// 16 B: the B operand reads of phases B and D are conflict-free), W1aug, b2,
-// the output layer(s) and the head scalars
-template <int H>
-struct AdamImg {
-  float W2s[H][H + 4];
-  float W2Ts[H][H + 4];
-  float W1s[H * 20];
-  float b2s[H];
-  float w3s[3][H];    // actor: mean_layer rows; critic: fc3 in row 0
-  float hs[8];        // b3a[0..2], b3c, log_std[0..2]
-};
 
 // ---------------------------------------------------------------------------
 // rowpass: the whole row-parallel part of a minibatch step in one launch.
@@ -510,14 +357,13 @@ struct MlpSmem {
 // acc = tanh(fc2) for this wave's columns, h1 = tanh(fc1) (for the fc1
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
-// tanh(fc1) goes to h1out[r * H + n].  IMG: the net's parameters come from
-// the LDS image img (the deferred-Adam rowpass) instead of P.
-template <int H, int NW, int R, bool APRE, class Gather, bool IMG = false>
+// tanh(fc1) goes to h1out[r * H + n].
+template <int H, int NW, int R, bool APRE, class Gather>
 __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P, int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
                                             f4 (&acc)[R / 16][H / 16 / NW],
                                             float (&h1)[R / 16][H / 16 / NW][4],
-                                            float (&w3)[H / 16 / NW][3], const AdamImg<H>* img = nullptr) {
+                                            float (&w3)[H / 16 / NW][3]) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
   static_assert(CT >= 1 && H % (16 * NW) == 0, "tile split");
   const Layout L = layout(H);
@@ -535,20 +381,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   // issued after the gather would hold up the barrier below
   float4 w1raw[CT][2];
   float b2v[CT], w3raw[CT][3];
-  if constexpr (IMG) {
-    const int o0 = lg < 2 ? 8 * lg : 16, o1 = lg < 2 ? 8 * lg + 4 : 16;
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int n = n0 + 16 * t + li;
-      const float* bp = img->W1s + n * 20;
-      w1raw[t][0] = *reinterpret_cast<const float4*>(bp + o0);
-      w1raw[t][1] = *reinterpret_cast<const float4*>(bp + o1);
-      b2v[t] = img->b2s[n];
-      w3raw[t][0] = img->w3s[0][n];
-      w3raw[t][1] = img->w3s[1][n];
-      w3raw[t][2] = img->w3s[2][n];
-    }
-  } else {
+  {
     const float* W1 = P + L.W1 + (int64_t)net * H * 20;
     const int o0 = lg < 2 ? 8 * lg : 16, o1 = lg < 2 ? 8 * lg + 4 : 16;
 #pragma unroll
@@ -607,8 +440,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  if constexpr (IMG) mfma_rows<H, LDA, H + 4, RT, CT, APRE>(&sm.h1s[0][0], &img->W2s[0][0], n0, acc);
-  else mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -672,23 +504,16 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
   return od;
 }
 
-// FADAM (H = 64, with FDW2): the deferred-Adam rowpass (satrl_ppo_rowpass_dw2_adam).
-// The workgroup first applies the pending step (A, G, M, V) to its net's
-// parameters into the LDS image (dynamic LDS) and runs on that image.
-template <int H, int NW, int R = kRows, bool FDW2 = false, bool FADAM = false>
+template <int H, int NW, int R = kRows, bool FDW2 = false>
 __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const float* __restrict__ W2T, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1, int net_sel, float* __restrict__ p2,
-                                                      int S2, float* __restrict__ ratio_out,
-                                                      satrl_ppo_adam_pending A, int nblk,
-                                                      const float* __restrict__ Gp, const float* __restrict__ Mp,
-                                                      const float* __restrict__ Vp) {
+                                                      int S2, float* __restrict__ ratio_out) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
-  static_assert(!FADAM || (FDW2 && NT == 256), "deferred Adam: 256-thread workgroups (adam_kernel's norm fold)");
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
   __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
@@ -719,37 +544,30 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   __shared__ float hb3s[4];                                        // b3a[0..2], b3c
   const int hd = tid - (NT - 64);                                  // head-scalar lane of the last wave
   float hls_d = 0.0f, hb3_d = 0.0f;
-  if constexpr (!FADAM) {
-    if (hd >= 0 && hd < 4) {
-      hb3_d = P[hd < 3 ? L.b3a + hd : L.b3c];
-      hls_d = P[L.ls + (hd < 3 ? hd : 0)];
-    }
+  if (hd >= 0 && hd < 4) {
+    hb3_d = P[hd < 3 ? L.b3a + hd : L.b3c];
+    hls_d = P[L.ls + (hd < 3 ? hd : 0)];
   }
 
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  // the head constants from (b3, log_std) held by the head-scalar lanes
-  auto head_consts_of = [&](float hb3, float hls) {
-    if (hd >= 0 && hd < 4) {
-      hb3s[hd] = hb3;
-      if (hd < 3) {
-        const float sd = expf(hls), var = sd * sd;
-        hcs[0][hd] = var;
-        hcs[1][hd] = logf(sd);
-        hcs[2][hd] = 1.0f / var;
+  auto gather = [&](int t0, int nt) {
+    auto head_consts = [&] {
+      // (opaque to the compiler and ordered after the row loads: otherwise it
+      // hoists this arithmetic next to its loads at the top of the kernel,
+      // and the whole wave waits for them before issuing any row load)
+      asm volatile("" : "+v"(hls_d), "+v"(hb3_d)::"memory");
+      if (hd >= 0 && hd < 4) {
+        hb3s[hd] = hb3_d;
+        if (hd < 3) {
+          const float sd = expf(hls_d), var = sd * sd;
+          hcs[0][hd] = var;
+          hcs[1][hd] = logf(sd);
+          hcs[2][hd] = 1.0f / var;
+        }
       }
-    }
-  };
-  auto head_consts = [&] {
-    // (opaque to the compiler and ordered after the row loads: otherwise it
-    // hoists this arithmetic next to its loads at the top of the kernel,
-    // and the whole wave waits for them before issuing any row load)
-    asm volatile("" : "+v"(hls_d), "+v"(hb3_d)::"memory");
-    head_consts_of(hb3_d, hls_d);
-  };
-  // the block's rows -> S / ax; hc() runs while the row loads are in flight
-  auto rows = [&](int t0, int nt, auto hc) {
+    };
     if (idx == nullptr) {
       // contiguous (staged) rows: one 16-B load per thread covers the block's
       // R x 32 floats, all in flight at once (a loop of dependent scalar
@@ -759,7 +577,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
       const int r = (t0 >> 3) & (R - 1), c4 = t0 & 7, row = r0 + r;
       const bool in = t0 < R * 8;
       float4 v = reinterpret_cast<const float4*>(src)[(int64_t)(row < mb ? row : mb - 1) * 8 + c4];
-      hc();
+      head_consts();
       if (row >= mb) v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (in) {
         const float e4[4] = {v.x, v.y, v.z, v.w};
@@ -776,105 +594,14 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         const float v = row < mb ? src[idx[row] * 32 + c] : 0.0f;
         if (c < 18) S[r][c] = v; else ax[r][c - 18] = v;
       }
-      hc();
+      head_consts();
     }
   };
-  AdamImg<H>* img = nullptr;
+  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, FDW2 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc,
+                              h1, w3);
+  // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
-  if constexpr (FADAM) {
-    extern __shared__ __attribute__((aligned(16))) float rp_dyn_lds[];
-    img = reinterpret_cast<AdamImg<H>*>(rp_dyn_lds);
-    __shared__ double shf[8];
-    // ---- the pending Adam step on this net's parameters, into img ------------
-    // Thread t owns float4s t, t + 256, ... of the net's W2, then of its
-    // W1aug, then one of its tail (b2, then mean_layer | b3a | log_std, or
-    // fc3 | b3c); every workgroup of the net computes the same bits, which
-    // are adam_kernel's (satrl_ppo_reduce_apply writes them to P / M / V).
-    // Its operand loads and the norm partials go out before the row loads,
-    // so one memory latency covers both.
-    constexpr int N2 = H * H / 4 / 256, N1 = (H * 5 + 255) / 256, NQ = N2 + N1 + 1;
-    static_assert(N2 * 256 == H * H / 4, "W2 float4s per thread");
-    const int ntail = net == 0 ? H + 2 : H / 2 + 1;
-    static_assert(H + 2 <= 256, "one tail float4 per thread");
-    int64_t e4[NQ];
-    bool lv[NQ];
-#pragma unroll
-    for (int j = 0; j < N2; ++j) {
-      e4[j] = (int64_t)net * (H * H / 4) + tid + 256 * j;
-      lv[j] = true;
-    }
-#pragma unroll
-    for (int j = 0; j < N1; ++j) {
-      const int i = tid + 256 * j;
-      lv[N2 + j] = i < H * 5;
-      e4[N2 + j] = L.W1 / 4 + (int64_t)net * H * 5 + min(i, H * 5 - 1);
-    }
-    {
-      const int i = min(tid, ntail - 1);
-      lv[NQ - 1] = tid < ntail;
-      e4[NQ - 1] = i < H / 4 ? L.b2 / 4 + net * (H / 4) + i : (net == 0 ? L.W3a / 4 : L.W3c / 4) + (i - H / 4);
-    }
-    double2 pn2[4];
-    adam_fold_load(A.nsq, nblk, pn2);
-    float4 qg[NQ], qm[NQ], qv[NQ], qp[NQ];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) {
-      qg[j] = reinterpret_cast<const float4*>(Gp)[e4[j]];
-      qm[j] = reinterpret_cast<const float4*>(Mp)[e4[j]];
-      qv[j] = reinterpret_cast<const float4*>(Vp)[e4[j]];
-      qp[j] = reinterpret_cast<const float4*>(P)[e4[j]];
-    }
-    rows(tid, NT, [] {});
-    PHASE_PROBE(16);
-    double fa, fc;
-    adam_fold(A.nsq, nblk, pn2, fa, fc, shf);
-    const AdamK k = adam_consts(A, net, fa, fc);
-    PHASE_PROBE(17);
-#pragma unroll
-    for (int j = 0; j < N2; ++j) {
-      const float4 pn = adam4(k, A, qg[j], qm[j], qv[j], qp[j]);
-      const int e = 4 * (tid + 256 * j), n = e / H, kk = e % H;
-      *reinterpret_cast<float4*>(&img->W2s[n][kk]) = pn;
-      img->W2Ts[kk][n] = pn.x;
-      img->W2Ts[kk + 1][n] = pn.y;
-      img->W2Ts[kk + 2][n] = pn.z;
-      img->W2Ts[kk + 3][n] = pn.w;
-    }
-#pragma unroll
-    for (int j = 0; j < N1; ++j) {
-      const float4 pn = adam4(k, A, qg[N2 + j], qm[N2 + j], qv[N2 + j], qp[N2 + j]);
-      if (lv[N2 + j]) *reinterpret_cast<float4*>(&img->W1s[4 * (tid + 256 * j)]) = pn;
-    }
-    {
-      const float4 pn = adam4(k, A, qg[NQ - 1], qm[NQ - 1], qv[NQ - 1], qp[NQ - 1]);
-      if (lv[NQ - 1]) {
-        const int i = tid, jj = 4 * (i - H / 4);
-        if (i < H / 4) {
-          *reinterpret_cast<float4*>(&img->b2s[4 * i]) = pn;
-        } else if (net == 0) {
-          if (jj < 3 * H) *reinterpret_cast<float4*>(&img->w3s[0][0] + jj) = pn;
-          else if (jj == 3 * H) { img->hs[0] = pn.x; img->hs[1] = pn.y; img->hs[2] = pn.z; }
-          else { img->hs[4] = pn.x; img->hs[5] = pn.y; img->hs[6] = pn.z; }
-        } else {
-          if (jj < H) *reinterpret_cast<float4*>(&img->w3s[0][jj]) = pn;
-          else img->hs[3] = pn.x;
-        }
-      }
-    }
-    PHASE_PROBE(18);
-    __syncthreads();
-    auto gather_img = [&](int, int) {
-      if (hd >= 0 && hd < 4) head_consts_of(img->hs[hd < 3 ? hd : 3], img->hs[4 + (hd < 3 ? hd : 0)]);
-    };
-    mlp_forward<H, NW, R, true, decltype(gather_img), true>(sm, P, net, mb - r0, gather_img, nullptr, acc, h1, w3,
-                                                            img);
-  } else {
-    auto gather = [&](int t0, int nt) { rows(t0, nt, head_consts); };
-    mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, FDW2 ? nullptr : H1g + ((int64_t)net * mb + r0) * H,
-                                acc, h1, w3);
-    // phase D's first W2T chunks go out now, under the loss head and the tail
-    mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
-  }
+  mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -1012,8 +739,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (FADAM) mfma_rows<H, LDA, H + 4, RT, CT, true>(&dzs[0][0], &img->W2Ts[0][0], n0, acc);
-  else mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
+  mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
@@ -1251,6 +977,76 @@ int dw2_splits(int H, int mb, int net) {
 struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
 constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;   // chunks per column: W1, tail, W2 regions
 
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+// IEEE division per component, as torch's G.div_(world) after the all-reduce
+__device__ __forceinline__ float4 f4div(float4 a, float d) {
+  return make_float4(a.x / d, a.y / d, a.z / d, a.w / d);
+}
+__device__ __forceinline__ double sq4(float4 v) {
+  return (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+}
+
+template <int CH>
+__device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, int64_t stride4, int nparts,
+                                             int64_t col, bool valid, float4* red) {
+  constexpr int EB = 256 / CH;
+  const int t = threadIdx.x, e = t % EB, c = t / EB;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+#pragma unroll 16
+    for (int w = c; w < nparts; w += CH) s = f4add(s, part[(int64_t)w * stride4 + col]);
+  }
+  red[t] = s;
+  __syncthreads();
+  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c == 0) {
+    // the CH partials in order; their LDS reads go out 8 at a time ahead of
+    // the adds (one read round trip per 8, not per 2)
+    constexpr int KB = CH < 8 ? CH : 8;
+#pragma unroll
+    for (int k0 = 0; k0 < CH; k0 += KB) {
+      float4 part[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) part[k] = red[(k0 + k) * EB + e];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) tot = f4add(tot, part[k]);
+    }
+  }
+  return tot;
+}
+
+// block-level f64 pair sum in fixed order, result in every thread
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_d(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+// wave sum of (a, c) in a fixed order: DPP sums of each 16-lane row (the
+// row16_sum stages), then rows 0..3 by readlane -- no ds_bpermute round trips
+__device__ __forceinline__ void wave_sum2(double& a, double& c) {
+  a += dpp_d<0xB1>(a); c += dpp_d<0xB1>(c);
+  a += dpp_d<0x4E>(a); c += dpp_d<0x4E>(c);
+  a += dpp_d<0x141>(a); c += dpp_d<0x141>(c);
+  a += dpp_d<0x140>(a); c += dpp_d<0x140>(c);
+  a = ((lane_d(a, 0) + lane_d(a, 16)) + lane_d(a, 32)) + lane_d(a, 48);
+  c = ((lane_d(c, 0) + lane_d(c, 16)) + lane_d(c, 32)) + lane_d(c, 48);
+}
+__device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
+  wave_sum2(a, c);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[2 * w] = a; sh[2 * w + 1] = c; }
+  __syncthreads();
+  a = 0.0; c = 0.0;
+  for (int k = 0; k < nw; ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
+}
+
 // what a reduce thread ends with: the float4 of G it wrote (lead threads
 // only: live), its float4 index in the flat layout, and its net
 struct RedOut {
@@ -1264,11 +1060,10 @@ struct RedOut {
 // after it: b counts from the first W1 block): sums the rowpass slabs into G
 // (mode & 1) or rescales G (world > 1), and adds this thread's squares to
 // (sa, sc).
-template <class Store>
 __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const RedGeom& g, int b, int mode,
                                                const float* __restrict__ p1, const float* __restrict__ pt,
                                                float4* __restrict__ G4, int world, float4* red, double& sa,
-                                               double& sc, RedOut& o, Store store) {
+                                               double& sc, RedOut& o) {
   const int t = threadIdx.x;
   if (b < g.nb1) {                                                // W1: [nw1] slabs of 2*H*20
     constexpr int EB = 256 / kRedCH1;
@@ -1278,7 +1073,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCH1>(reinterpret_cast<const float4*>(p1), n4, g.nw1, col, valid, red);
-      if (lead && valid) store(L.W1 / 4 + col, v);
+      if (lead && valid) G4[L.W1 / 4 + col] = v;
     } else if (lead && valid) {
       v = G4[L.W1 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.W1 / 4 + col] = v; }
@@ -1298,7 +1093,7 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
       v = chunk_sum4<kRedCHt>(reinterpret_cast<const float4*>(pt), n4, g.nwg, col, valid, red);
-      if (lead && valid) store(L.b2 / 4 + col, v);
+      if (lead && valid) G4[L.b2 / 4 + col] = v;
     } else if (lead && valid) {
       v = G4[L.b2 / 4 + col];
       if (world > 1) { v = f4div(v, (float)world); G4[L.b2 / 4 + col] = v; }
@@ -1313,13 +1108,11 @@ __device__ __forceinline__ void reduce_w1_tail(int H, const Layout& L, const Red
   }
 }
 
-// block b of reduce: the W2 region, else the W1 / tail regions.  store(i, v)
-// writes the summed float4 v of G at float4 index i (mode & 1)
-template <class Store>
+// block b of reduce: the W2 region, else the W1 / tail regions
 __device__ __forceinline__ void reduce_block(int H, const Layout& L, const RedGeom& g, int b, int mode,
                                              const float* __restrict__ p2, const float* __restrict__ p1,
                                              const float* __restrict__ pt, float4* __restrict__ G4, int world,
-                                             float4* red, double& sa, double& sc, RedOut& o, Store store) {
+                                             float4* red, double& sa, double& sc, RedOut& o) {
   const int t = threadIdx.x;
   const int64_t HH4 = (int64_t)H * H / 4;
   if (b < g.nb2) {                                                // W2: [2][S] split-K slabs of H*H
@@ -1331,7 +1124,7 @@ __device__ __forceinline__ void reduce_block(int H, const Layout& L, const RedGe
     if (mode & 1) {
       v = chunk_sum4<kRedCH2>(reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4, HH4, g.S,
                               col - net * HH4, valid, red);
-      if (lead && valid) store(col, v);
+      if (lead && valid) G4[col] = v;
     } else if (lead && valid) {
       v = G4[col];
       if (world > 1) { v = f4div(v, (float)world); G4[col] = v; }
@@ -1341,35 +1134,8 @@ __device__ __forceinline__ void reduce_block(int H, const Layout& L, const RedGe
     }
     o = RedOut{v, col, net, lead && valid};
   } else {
-    reduce_w1_tail(H, L, g, b - g.nb2, mode, p1, pt, G4, world, red, sa, sc, o, store);
+    reduce_w1_tail(H, L, g, b - g.nb2, mode, p1, pt, G4, world, red, sa, sc, o);
   }
-}
-
-// the float4 of G that thread t of reduce block b leads (reduce_block's
-// mapping: the RedOut it ends with, without v), known before any load
-__device__ __forceinline__ RedOut red_lead(int H, const Layout& L, const RedGeom& g, int b, int t) {
-  const int64_t HH4 = (int64_t)H * H / 4;
-  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (b < g.nb2) {
-    constexpr int EB = 256 / kRedCH2;
-    const int64_t col = (g.net > 0 ? HH4 : 0) + (int64_t)b * EB + (t % EB);
-    const bool valid = col < (g.net < 0 ? 2 : g.net + 1) * HH4, lead = t < EB;
-    return RedOut{z, col, (int)(col >= HH4), lead && valid};
-  }
-  b -= g.nb2;
-  if (b < g.nb1) {
-    constexpr int EB = 256 / kRedCH1;
-    const int64_t n4 = 2LL * H * 20 / 4, h4 = (int64_t)H * 20 / 4;
-    const int64_t col = (g.net > 0 ? h4 : 0) + (int64_t)b * EB + (t % EB);
-    const bool valid = col < (g.net == 0 ? h4 : n4), lead = t < EB;
-    return RedOut{z, L.W1 / 4 + col, col * 4 >= (int64_t)H * 20 ? 1 : 0, lead && valid};
-  }
-  b -= g.nb1;
-  constexpr int EB = 256 / kRedCHt;
-  const int64_t n4 = L.tail / 4, col = (int64_t)b * EB + (t % EB);
-  const bool valid = col < n4 && (g.net < 0 || net_of(L, L.b2 + col * 4, H) == g.net), lead = t < EB;
-  const bool crit = valid && net_of(L, L.b2 + col * 4, H);
-  return RedOut{z, L.b2 / 4 + col, crit ? 1 : 0, lead && valid};
 }
 
 __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode, const float* __restrict__ p2,
@@ -1383,8 +1149,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
   const int t = threadIdx.x;
   float4* G4 = reinterpret_cast<float4*>(G);
   RedOut o;
-  reduce_block(H, L, g, blockIdx.x, mode, p2, p1, pt, G4, world, red, sa, sc, o,
-               [&](int64_t i, float4 v) { G4[i] = v; });
+  reduce_block(H, L, g, blockIdx.x, mode, p2, p1, pt, G4, world, red, sa, sc, o);
   if (mode & 2) {
     block_sum2(sa, sc, sh);
     if (t == 0) {
@@ -1398,65 +1163,6 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
   }
 }
 
-// reduce_apply (satrl_ppo_reduce_apply): reduce mode 3 for both nets without
-// the step-counter advance, norm partials to nsq_out; PEND: each lead thread
-// first applies the pending step held in G to its float4 of P / M / V
-// (adam_kernel's bits: the same fold, constants and update), then stores the
-// new gradient over it.  Its operands and the pending norm partials are
-// loaded before the slab sums, so their latency hides under them.
-template <bool PEND>
-__global__ void __launch_bounds__(256) reduce_apply_kernel(int H, RedGeom g, const float* __restrict__ p2,
-                                                           const float* __restrict__ p1,
-                                                           const float* __restrict__ pt, satrl_ppo_adam_pending A,
-                                                           float* __restrict__ G, float* __restrict__ P,
-                                                           float* __restrict__ M, float* __restrict__ V,
-                                                           double* __restrict__ nsq_out) {
-  const Layout L = layout(H);
-  __shared__ double sh[8], shf[8];
-  __shared__ float4 red[256];
-  const int t = threadIdx.x, b = blockIdx.x;
-  float4* G4 = reinterpret_cast<float4*>(G);
-  float4* P4 = reinterpret_cast<float4*>(P);
-  float4* M4 = reinterpret_cast<float4*>(M);
-  float4* V4 = reinterpret_cast<float4*>(V);
-  const RedOut ld = red_lead(H, L, g, b, t);
-  float4 og, om, ov, op;
-  AdamK k;
-  if constexpr (PEND) {
-    double2 pn2[4];
-    adam_fold_load(A.nsq, (int)gridDim.x, pn2);
-    const int64_t el = ld.live ? ld.e4 : 0;
-    og = G4[el];
-    om = M4[el];
-    ov = V4[el];
-    op = P4[el];
-    double fa, fc;
-    adam_fold(A.nsq, (int)gridDim.x, pn2, fa, fc, shf);
-    k = adam_consts(A, ld.net, fa, fc);
-  }
-  double sa = 0.0, sc = 0.0;
-  RedOut o;
-  reduce_block(H, L, g, b, 1, p2, p1, pt, G4, 1, red, sa, sc, o, [&](int64_t i, float4 v) {
-    if constexpr (PEND) {                                          // (i == ld.e4: the same mapping)
-      const float4 pn = adam4(k, A, og, om, ov, op);
-      P4[i] = pn;
-      M4[i] = om;
-      V4[i] = ov;
-    }
-    G4[i] = v;
-  });
-  block_sum2(sa, sc, sh);
-  if (t == 0) {
-    nsq_out[2 * b] = sa;
-    nsq_out[2 * b + 1] = sc;
-  }
-}
-
-__global__ void steps_advance_kernel(double* steps, int n) {
-  steps[0] += (double)n;
-  steps[1] += (double)n;
-}
-
 // ---------------------------------------------------------------------------
 // adam: torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (_single_tensor_adam)
 // Every block first folds the per-block norms (fixed order, identical in
@@ -1464,6 +1170,15 @@ __global__ void steps_advance_kernel(double* steps, int n) {
 // float4 per thread, and the updated tile goes out transposed through LDS
 // into W2T (coalesced).  Blocks [nbw, ...): the rest of the layout, float4.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float step_size,
+                                           float bc2s, float w1, float w2, float beta2, float eps, int use_clip) {
+  if (use_clip) g = g * coef;                                      // grads.mul_(clip_coef_clamped)
+  m = m + w1 * (g - m);                                            // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * beta2 + w2 * (g * g);                                    // mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + eps;
+  return p + (-step_size) * (m / denom);                           // addcdiv_(m, denom, -step_size)
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double* __restrict__ nsq,
                                                    const double* __restrict__ steps, const double* __restrict__ bct,
                                                    int bct_len, const float* __restrict__ lr, float beta1,
@@ -1790,21 +1505,13 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
 // instead of H1 / dZ2; ratio (nullable) receives the actor's per-row ratio
 static int launch_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
                           const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
-                          float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream,
-                          const satrl_ppo_adam_pending* pend = nullptr, const float* Gp = nullptr,
-                          const float* Mp = nullptr, const float* Vp = nullptr) {
+                          float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream) {
   const int R = rows_per_wg(H, mb), nrb = n_head_wg(H, mb);
   dim3 g((net < 0 ? 2 : 1) * nrb);   // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
-  satrl_ppo_adam_pending A{};
-  if (pend) A = *pend;
-  const int nblk = n_blocks(geom(H, mb, 1, -1));
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
-#define RP_ARGS mb, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio, A, \
-                nblk, Gp, Mp, Vp
-  if (H == 64 && fdw2 && pend)
-    hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true, true>), g, dim3(256), sizeof(AdamImg<64>), s, RP_ARGS);
-  else if (H == 64 && fdw2)
+#define RP_ARGS mb, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio
+  if (H == 64 && fdw2)
     hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true>), g, dim3(256), 0, s, RP_ARGS);
   else if (H == 64)
     hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, RP_ARGS);
@@ -1852,44 +1559,6 @@ int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_
     return -1;
   return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
                         nullptr, true, stream);
-}
-
-int satrl_ppo_rowpass_dw2_adam(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                               const float* W2T, float epsilon, float ent_coef, float max_action,
-                               const satrl_ppo_adam_pending* pend, const float* G, const float* M, const float* V,
-                               float* p2, float* ptail, float* pw1, void* stream) {
-  if (H != 64 || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !p2 || !ptail || !pw1) return -1;
-  if (pend && (!G || !M || !V || !pend->nsq || !pend->steps || !pend->bct || pend->bct_len < 1 || !pend->lr))
-    return -1;
-  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
-                        nullptr, true, stream, pend, G, M, V);
-}
-
-int satrl_ppo_reduce_apply(int H, int mb, int S, const float* p2, const float* p1, const float* pt,
-                           const satrl_ppo_adam_pending* pend, float* G, float* P, float* M, float* V, double* nsq_out,
-                           void* stream) {
-  if (!valid_h(H) || mb <= 0 || S < 1 || !p2 || !p1 || !pt || !G || !nsq_out) return -1;
-  if (pend && (!P || !M || !V || !pend->nsq || pend->nsq == nsq_out || !pend->steps || !pend->bct ||
-               pend->bct_len < 1 || !pend->lr))
-    return -1;
-  const RedGeom g = geom(H, mb, S, -1);
-  satrl_ppo_adam_pending A{};
-  if (pend) A = *pend;
-  if (pend)
-    hipLaunchKernelGGL(reduce_apply_kernel<true>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, p2, p1,
-                       pt, A, G, P, M, V, nsq_out);
-  else
-    hipLaunchKernelGGL(reduce_apply_kernel<false>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, p2, p1,
-                       pt, A, G, P, M, V, nsq_out);
-  LAUNCH_CHECK();
-  return 0;
-}
-
-int satrl_ppo_steps_advance(double* steps, int n, void* stream) {
-  if (!steps) return -1;
-  hipLaunchKernelGGL(steps_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, steps, n);
-  LAUNCH_CHECK();
-  return 0;
 }
 
 int satrl_ppo_dw2_splits(int H, int mb) {

@@ -39,14 +39,6 @@ class SatenvParams(C.Structure):
                 ("cw_omega", C.c_double), ("propagator", C.c_int32), ("rk4_substeps", C.c_int32)]
 
 
-class AdamPending(C.Structure):
-    """Mirror of ``satrl_ppo_adam_pending`` (include/satrl_ppo.h): a deferred
-    Adam step (satrl_ppo_rowpass_dw2_adam / satrl_ppo_reduce_apply)."""
-    _fields_ = [("nsq", C.c_void_p), ("steps", C.c_void_p), ("dk", C.c_int), ("bct", C.c_void_p),
-                ("bct_len", C.c_int), ("lr", C.c_void_p), ("beta1", C.c_float), ("beta2", C.c_float),
-                ("eps", C.c_float), ("max_norm", C.c_float), ("use_clip", C.c_int)]
-
-
 class NativeError(RuntimeError):
     pass
 
@@ -131,11 +123,6 @@ _SIGS = {
     "satrl_ppo_row_blocks": ([C.c_int, C.c_int], C.c_int),
     "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                                _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_rowpass_dw2_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
-                                    C.POINTER(AdamPending), _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_reduce_apply": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.POINTER(AdamPending), _vp, _vp, _vp, _vp,
-                                _vp, _vp], C.c_int),
-    "satrl_ppo_steps_advance": ([_vp, C.c_int, _vp], C.c_int),
     "satrl_peer_buffer_bytes": ([_i64, C.c_int, _vp], C.c_int),
     "satrl_peer_alloc": ([_i64, _vp, _vp], C.c_int),
     "satrl_peer_open": ([_vp, _vp], C.c_int),

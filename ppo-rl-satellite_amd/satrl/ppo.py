@@ -292,17 +292,6 @@ class FusedMinibatch:
             for net in ((0, 1) if self.split else (-1,)):
                 self._ws_for[(self.mb, self.S, net)] = (self._dw2_plan(self.mb, self.S, net),)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
-        # H = 64, one process, graph-replayed groups: each step's Adam is
-        # deferred into the next step's two launches (satrl_ppo_rowpass_dw2_adam
-        # applies it on the fly in LDS, satrl_ppo_reduce_apply to P / M / V before
-        # it overwrites G), the group's last one by satrl_ppo_adam: two launches
-        # per minibatch instead of three, bitwise the same parameters.  The
-        # pending step's norm partials alternate between two buffers.
-        self.fused_adam = self.fused_dw2 and learner.pg is None and not self.split
-        if os.environ.get("SATRL_FUSED_ADAM") is not None:               # dev A/B knob
-            self.fused_adam = self.fused_adam and os.environ["SATRL_FUSED_ADAM"] == "1"
-        self.nsq_par = (torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev) if self.fused_adam
-                        else None)
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
         # group (one index_select) so rowpass reads them without an index hop
@@ -498,38 +487,6 @@ class FusedMinibatch:
                                  float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
                                  ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
 
-    def pending(self, k, nsq):
-        """The deferred Adam step of step k-1 of a group (count steps + k; its
-        norm partials in nsq), as the C struct satrl_ppo_adam_pending."""
-        L = self.L
-        return _lib.AdamPending(nsq=ptr(nsq), steps=ptr(L.steps), dk=int(k), bct=ptr(L.bct), bct_len=L.bct.shape[0],
-                                lr=ptr(L.lr), beta1=float(L.beta1), beta2=float(L.beta2), eps=float(L.adam_eps),
-                                max_norm=0.5, use_clip=int(bool(L.use_grad_clip)))
-
-    def _deferred_steps(self, ng):
-        """ng minibatch steps on self.stage's rows, two launches each, with the
-        Adam step deferred (see __init__): step k's rowpass and reduce apply
-        step k-1's update; then the steps counters advance by ng and
-        satrl_ppo_adam applies the last step (and refreshes W2T)."""
-        L = self.L
-        H, mb, S = L.H, self.mb, self.S
-        lib, sp = _lib.lib(), stream_ptr()
-        for k in range(ng):
-            rows = self.stage[k * mb:(k + 1) * mb]
-            pend = C.byref(self.pending(k, self.nsq_par[(k - 1) & 1])) if k > 0 else None
-            check(lib.satrl_ppo_rowpass_dw2_adam(H, mb, -1, ptr(rows), None, ptr(L.P), ptr(L.W2T), float(L.epsilon),
-                                                 float(L.entropy_coef), float(L.max_action), pend, ptr(L.G),
-                                                 ptr(L.M), ptr(L.V), ptr(self.p2), ptr(self.ptail), ptr(self.pw1),
-                                                 sp), "satrl_ppo_rowpass_dw2_adam")
-            check(lib.satrl_ppo_reduce_apply(H, mb, S, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), pend, ptr(L.G),
-                                             ptr(L.P), ptr(L.M), ptr(L.V), ptr(self.nsq_par[k & 1]), sp),
-                  "satrl_ppo_reduce_apply")
-        check(lib.satrl_ppo_steps_advance(ptr(L.steps), int(ng), sp), "satrl_ppo_steps_advance")
-        check(lib.satrl_ppo_adam(H, mb, -1, ptr(self.nsq_par[(ng - 1) & 1]), ptr(L.steps), ptr(L.bct),
-                                 L.bct.shape[0], ptr(L.lr), float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5,
-                                 int(bool(L.use_grad_clip)), ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp),
-              "satrl_ppo_adam")
-
     def _chains(self, fn):
         """fn(net) for the actor on the current stream and the critic on the
         side stream (fork/join), or fn(-1) once when not split."""
@@ -572,13 +529,11 @@ class FusedMinibatch:
         mb, G = self.mb, self.group
         check(_lib.lib().satrl_ppo_stage(G * mb, ptr(src), ptr(self.perm_buf), ptr(self.grp), ptr(self.stage),
                                          stream_ptr()), "satrl_ppo_stage")
-        if self.fused_adam:
-            self._deferred_steps(G)
-        else:
-            def chain(net):
-                for k in range(G):
-                    self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
-            self._chains(chain)
+
+        def chain(net):
+            for k in range(G):
+                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
+        self._chains(chain)
         check(_lib.lib().satrl_ppo_group_advance(ptr(self.grp), stream_ptr()), "satrl_ppo_group_advance")
 
     def _capture(self, src):

@@ -8,8 +8,6 @@ Tolerances (DESIGN.md "Parity"):
     24 Adam steps within 1e-3 rel + 2*lr*steps*1% abs (Adam's m/sqrt(v) turns
     ulp-level gradient noise into up-to-lr-sized steps on near-zero grads)
 """
-import ctypes as C
-
 import numpy as np
 import pytest
 import torch
@@ -637,112 +635,6 @@ def test_fused_dw2_rowpass_bitwise_equals_separate(mb, contig):
                      st.pw1[:S * 2 * 64 * 20].clone(), G, nsq])
     for a, b in zip(*outs):
         assert bool(torch.isfinite(a).all()) and torch.equal(a, b)
-
-
-@pytest.mark.parametrize("mb,contig", [(4096, True), (777, False)])
-def test_deferred_adam_kernels_equal_adam_then_rowpass(mb, contig):
-    """H 64, deferred Adam: with step t's gradient pending (G, its norm
-    partials, steps advanced by the reduce), satrl_ppo_rowpass_dw2_adam
-    writes bitwise the slabs satrl_ppo_adam + satrl_ppo_rowpass_dw2 write
-    (the step applied on the fly in LDS), and satrl_ppo_reduce_apply leaves
-    bitwise satrl_ppo_adam's P / M / V and satrl_ppo_reduce's G and norm
-    partials for the next step (ppo_continuous.py:227-239: clip_grad_norm_,
-    Adam.step, then the next minibatch's loss)."""
-    import satrl._lib as _L
-    from satrl.ppo import PPOLearner
-    torch.manual_seed(5)
-    B = 8192
-    args = _args(hidden_width=64, mini_batch_size=mb, batch_size=B)
-    L = PPOLearner(args, "pursuer", use_graph=False)
-    L.sync_w2t()
-    g = torch.Generator(device="cuda").manual_seed(6)
-    src = torch.randn((B, 32), device="cuda", generator=g)
-    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
-    idx = None if contig else torch.randperm(B, device="cuda", generator=g)[:mb]
-    st = L.stepper(mb)
-    for _ in range(3):                                   # non-trivial moments and step counts
-        st.step(src, idx)
-    lib, sp, S, p = _L.lib(), _L.stream_ptr(), st.S, _L.ptr
-    nsq = torch.zeros_like(st.nsq[0])
-
-    def reduce(G, nsq_out, steps):
-        _L.check(lib.satrl_ppo_reduce(64, mb, -1, S, 3, p(st.p2), p(st.pw1), p(st.ptail), p(G), p(nsq_out), p(steps),
-                                      sp), "satrl_ppo_reduce")
-
-    def slabs():
-        return [st.p2[:2 * S * 64 * 64].clone(), st.ptail[:S * (6 * 64 + 12)].clone(), st.pw1[:S * 2 * 64 * 20].clone()]
-
-    st.rowpass_dw2(src, idx)
-    reduce(L.G, nsq, L.steps)                            # step t pending: G, nsq, steps = t
-    snap = [t.clone() for t in (L.P, L.M, L.V, L.G, L.W2T, L.steps)]
-    # reference: Adam, then the next step's rowpass and reduce
-    _L.check(lib.satrl_ppo_adam(64, mb, -1, p(nsq), p(L.steps), p(L.bct), L.bct.shape[0], p(L.lr), float(L.beta1),
-                                float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)), p(L.G), p(L.P),
-                                p(L.M), p(L.V), p(L.W2T), sp), "satrl_ppo_adam")
-    ref_pmv = [t.clone() for t in (L.P, L.M, L.V)]
-    for b in (st.p2, st.ptail, st.pw1):
-        b.fill_(float("nan"))
-    st.rowpass_dw2(src, idx)
-    ref_slabs = slabs()
-    G_ref, nsq_ref, steps_scratch = torch.empty_like(L.G), torch.zeros_like(nsq), L.steps.clone()
-    reduce(G_ref, nsq_ref, steps_scratch)
-    # deferred: the same state, step t applied inside the next step's two launches
-    for t, s in zip((L.P, L.M, L.V, L.G, L.W2T, L.steps), snap):
-        t.copy_(s)
-    pend = C.byref(st.pending(0, nsq))
-    for b in (st.p2, st.ptail, st.pw1):
-        b.fill_(float("nan"))
-    _L.check(lib.satrl_ppo_rowpass_dw2_adam(64, mb, -1, p(src), None if idx is None else p(idx), p(L.P), p(L.W2T),
-                                            float(L.epsilon), float(L.entropy_coef), float(L.max_action), pend,
-                                            p(L.G), p(L.M), p(L.V), p(st.p2), p(st.ptail), p(st.pw1), sp),
-             "satrl_ppo_rowpass_dw2_adam")
-    torch.cuda.synchronize()
-    assert torch.equal(L.P, snap[0]) and torch.equal(L.M, snap[1])      # the rowpass writes no parameter
-    for a, b in zip(ref_slabs, slabs()):
-        assert bool(torch.isfinite(a).all()) and torch.equal(a, b)
-    nsq_out = torch.zeros_like(nsq)
-    _L.check(lib.satrl_ppo_reduce_apply(64, mb, S, p(st.p2), p(st.pw1), p(st.ptail), pend, p(L.G), p(L.P), p(L.M),
-                                        p(L.V), p(nsq_out), sp), "satrl_ppo_reduce_apply")
-    torch.cuda.synchronize()
-    for a, b in zip(ref_pmv, (L.P, L.M, L.V)):
-        assert torch.equal(a, b)
-    assert torch.equal(L.G, G_ref) and torch.equal(nsq_out, nsq_ref)
-    assert torch.equal(L.steps, snap[5])                 # counters untouched (satrl_ppo_steps_advance)
-    # the C ABI refuses a pending step whose partials are the output buffer
-    assert lib.satrl_ppo_reduce_apply(64, mb, S, p(st.p2), p(st.pw1), p(st.ptail), C.byref(st.pending(0, nsq_out)),
-                                      p(L.G), p(L.P), p(L.M), p(L.V), p(nsq_out), sp) == -1
-
-
-@pytest.mark.parametrize("mb,G", [(256, 4), (4096, 16)])
-def test_deferred_adam_graph_epochs_equal_three_launch_steps(mb, G):
-    """FusedMinibatch.run at H 64 with the deferred-Adam graph groups (two
-    launches per minibatch; the group's last step by satrl_ppo_adam after
-    satrl_ppo_steps_advance) == the same two epochs with rowpass_dw2 | reduce
-    | adam per minibatch, bitwise: parameters, Adam moments, W2T and step
-    counters, through graph groups, eager remainder groups and a ragged tail."""
-    from satrl.ppo import PPOLearner
-    B = (2 * G + 3) * mb + 17
-    res = []
-    for deferred in (True, False):
-        torch.manual_seed(12)
-        args = _args(hidden_width=64, mini_batch_size=mb, batch_size=B)
-        L = PPOLearner(args, "pursuer", graph_group=G, use_graph=True)
-        g = torch.Generator(device="cuda").manual_seed(3)
-        src = torch.randn((B, 32), device="cuda", generator=g)
-        src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
-        perms = [torch.randperm(B, device="cuda", generator=g) for _ in range(2)]
-        L.sync_w2t()
-        st = L.stepper(mb)
-        assert st.fused_adam
-        st.fused_adam = deferred
-        for q in perms:
-            st.run(src, q)
-        torch.cuda.synchronize()
-        assert st.graph is not None and int(st.grp.item()) == 2
-        res.append((L.P.clone(), L.M.clone(), L.V.clone(), L.W2T.clone(), L.steps.clone()))
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
-    assert float(res[0][4][0]) == 2 * (2 * G + 4)
 
 
 @pytest.mark.parametrize("H,mb", [(64, 4096), (256, 4096), (256, 512)])

@@ -9,9 +9,7 @@ Stamps (ppo_kernels.hip PHASE_PROBE): 0 start, 8 gather issued, 9 S ready,
 10 fc1 MFMA, 11 tanh(fc1) stored, 1 barrier, 2 fc2 MFMA (B), 3 output-layer
 sums (C fwd), 12 head: out_sum/tanh/logp, 13 head: ratio..dz/dls, 14 head:
 dz3s + row sums (12-14 wave 0 only), 4 loss head, 5 dZ2 + tail partials,
-6 dH1 MFMA (D), 7 end (E).  The deferred-Adam rowpass (H 64, PROBE_CHAIN):
-16 operands + rows loaded, 17 norm fold + constants, 18 the step into the
-LDS image (then 8 after its barrier).
+6 dH1 MFMA (D), 7 end (E).
 """
 import ctypes as C
 import os
@@ -61,13 +59,11 @@ torch.cuda.synchronize()
 
 if probe:
     lib = _L.lib()
-    buf = np.zeros((512, 24, 16, 2), dtype=np.uint64)
+    buf = np.zeros((512, 16, 16, 2), dtype=np.uint64)
     lib.satrl_probe_read.argtypes = [C.c_void_p]
     assert lib.satrl_probe_read(buf.ctypes.data) == 0
     b = buf.astype(np.int64)                     # [wg][stamp][wave][realtime, shader clock]
     order = [0, 8, 9, 10, 11, 1, 2, 3, 12, 13, 14, 4, 5, 6, 7]   # 12-14: inside the loss head (wave 0)
-    if os.environ.get("PROBE_CHAIN") and st.fused_adam:
-        order = [0, 16, 17, 18] + order[1:]      # the deferred-Adam prologue: loads + rows, fold, update
     b = b[:2 * (mb // 32), :, :NWV]               # the launched workgroups and waves only
     t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
     print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
