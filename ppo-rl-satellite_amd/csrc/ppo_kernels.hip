@@ -306,6 +306,142 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
   }
 }
 
+// ---------------------------------------------------------------------------
+// fc2 products at H = 256 as three-way bf16 splits (kBf3): gfx950 has no
+// reduced-precision f32 MFMA, and v_mfma_f32_16x16x4_f32 issues 2048 FLOP per
+// 32 cycles where v_mfma_f32_16x16x32_bf16 issues 16384 per 16.  Every f32
+// operand x is split x = hi + mid + lo exactly (round-to-nearest bf16 splits:
+// each residual is exact in f32 and the last one fits bf16's 8 bits), and a
+// product is the six partial products whose magnitude reaches f32's
+// rounding (lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi, smallest first;
+// the dropped mid*lo, lo*mid, lo*lo are below 2^-24 of it), each exact in the
+// MFMA's f32 accumulator.  Measured (tools/bf16x3_probe.hip, K = 256): error
+// / sum|a*b| max 2.2e-7, mean 1.3e-8 against 2.9e-7 / 1.7e-8 for the f32
+// MFMA chain.  The A operand (activations, written once per row block) goes
+// to LDS as three bf16 planes; the B operand (fc2.weight / its transpose,
+// read once per workgroup from L2) stays f32 and is split in registers, 44
+// VALU per 32-wide k chunk beside its 12 MFMAs.  The 16x16x32 operand layout
+// (lane l: row / column l & 15, k = 8 (l >> 4) + j) is the f32 path's k
+// mapping, and its accumulator layout the 16x16x4's, so nothing else changes.
+// ---------------------------------------------------------------------------
+template <int H>
+inline constexpr bool kBf3 = H == 256;
+typedef short s8v __attribute__((ext_vector_type(8)));   // 8 bf16: a 16x16x32 operand (4 VGPRs)
+
+__device__ __forceinline__ unsigned short bf16_rne(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+__device__ __forceinline__ float bf16_up(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+// x = hi + mid + lo exactly
+__device__ __forceinline__ void split3(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
+  h = bf16_rne(x);
+  const float r = x - bf16_up(h);
+  m = bf16_rne(r);
+  const float q = r - bf16_up(m);
+  l = bf16_rne(q);
+}
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+// two f32 -> one dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even), and back
+__device__ __forceinline__ unsigned pk_bf16(f2v x) { return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2v)); }
+__device__ __forceinline__ f2v unpk_bf16(unsigned p) {
+  return f2v{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+// split3 on a pair, packed: 9 VALU per pair (the residuals as packed f32 subtractions)
+__device__ __forceinline__ void split3x2(f2v x, unsigned& h, unsigned& m, unsigned& l) {
+  h = pk_bf16(x);
+  const f2v r = x - unpk_bf16(h);
+  m = pk_bf16(r);
+  const f2v q = r - unpk_bf16(m);
+  l = pk_bf16(q);
+}
+__device__ __forceinline__ void split3x8(const float4 (&x)[2], s8v (&o)[3]) {
+  unsigned h[4], m[4], l[4];
+  split3x2(f2v{x[0].x, x[0].y}, h[0], m[0], l[0]);
+  split3x2(f2v{x[0].z, x[0].w}, h[1], m[1], l[1]);
+  split3x2(f2v{x[1].x, x[1].y}, h[2], m[2], l[2]);
+  split3x2(f2v{x[1].z, x[1].w}, h[3], m[3], l[3]);
+  o[0] = __builtin_bit_cast(s8v, u4v{h[0], h[1], h[2], h[3]});
+  o[1] = __builtin_bit_cast(s8v, u4v{m[0], m[1], m[2], m[3]});
+  o[2] = __builtin_bit_cast(s8v, u4v{l[0], l[1], l[2], l[3]});
+}
+__device__ __forceinline__ f4 mfma_bf16(s8v a, s8v b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// one 32-wide k chunk: A planes (registers) x B (f32, split here)
+template <int RT, int CT>
+__device__ __forceinline__ void mfma3_regs(const s8v (&a)[RT][3], const float4 (&b)[CT][2], f4 (&acc)[RT][CT]) {
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    s8v bs[3];
+    split3x8(b[t], bs);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      acc[rt][t] = mfma_bf16(a[rt][2], bs[0], acc[rt][t]);
+      acc[rt][t] = mfma_bf16(a[rt][0], bs[2], acc[rt][t]);
+      acc[rt][t] = mfma_bf16(a[rt][1], bs[1], acc[rt][t]);
+      acc[rt][t] = mfma_bf16(a[rt][1], bs[0], acc[rt][t]);
+      acc[rt][t] = mfma_bf16(a[rt][0], bs[1], acc[rt][t]);
+      acc[rt][t] = mfma_bf16(a[rt][0], bs[0], acc[rt][t]);
+    }
+  }
+}
+template <int LDP, int PS, int RT>
+__device__ __forceinline__ void a3_chunk(const unsigned short* __restrict__ ap, s8v (&a)[RT][3]) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[rt][p] = *reinterpret_cast<const s8v*>(ap + p * PS + 16 * rt * LDP);
+  __builtin_amdgcn_sched_barrier(0);
+}
+// mfma_rows (APRE path) on the split operands: A = three bf16 planes in LDS
+// (row stride LDP, plane stride PS elements), B f32 row-major (ld LDB) as
+// there, kBPD chunks ahead, its first chunks optionally issued early (pre)
+constexpr int kBPD3 = 2;          // B chunks in flight ahead of the MFMAs
+constexpr int kADB3 = 1;          // A chunk buffers (2: the next chunk's LDS reads before this one's MFMAs: no faster)
+template <int K, int LDP, int PS, int LDB, int RT, int CT, bool PRE = false>
+__device__ __forceinline__ void mfma_rows3(const unsigned short* __restrict__ A, const float* __restrict__ B, int n0,
+                                           f4 (&acc)[RT][CT], const WPre<CT>* pre = nullptr) {
+  constexpr int NC = K / 32;
+  constexpr int BPD = kBPD3 < NC ? kBPD3 : NC, NB = BPD + 1;
+  static_assert(!PRE || BPD >= kBPD, "early-issued chunks fit the ring");
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const unsigned short* ap = A + i * LDP + 8 * g;
+  const float* bp = B + (int64_t)(n0 + i) * LDB + kGOff * g;
+  float4 bb[NB][CT][2];
+  s8v aa[kADB3][RT][3];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int c = 0; c < kBPD; ++c)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) { bb[c][t][0] = pre->bb[c][t][0]; bb[c][t][1] = pre->bb[c][t][1]; }
+#pragma unroll
+    for (int c = kBPD; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < BPD; ++c) b_chunk<CT>(bp + 32 * c, LDB, bb[c]);
+  }
+  if constexpr (kADB3 == 2) a3_chunk<LDP, PS, RT>(ap, aa[0]);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c + BPD < NC) b_chunk<CT>(bp + 32 * (c + BPD), LDB, bb[(c + BPD) % NB]);
+    if constexpr (kADB3 == 2) {
+      if (c + 1 < NC) a3_chunk<LDP, PS, RT>(ap + 32 * (c + 1), aa[(c + 1) % 2]);
+    } else {
+      a3_chunk<LDP, PS, RT>(ap + 32 * c, aa[0]);
+    }
+    mfma3_regs<RT, CT>(aa[kADB3 == 2 ? c % 2 : 0], bb[c % NB], acc);
+  }
+}
+// the three planes of x at element e of an LDS plane image (plane stride PS)
+template <int PS>
+__device__ __forceinline__ void put3(unsigned short* img, int e, float x) {
+  unsigned short h, m, l;
+  split3(x, h, m, l);
+  img[e] = h;
+  img[PS + e] = m;
+  img[2 * PS + e] = l;
+}
+
 // rows r < nvalid of a 32-/16-row block's accumulator-layout values v[rt][t][j]
 // (row 16rt + 4lg + j, column n0 + 16t + li) to out[r * ld + column]: a
 // uniform branch keeps a full block's stores straight-line (a per-lane test
@@ -346,10 +482,13 @@ __device__ __forceinline__ void rp_barrier() { __syncthreads(); }
 // recomputation bit for bit, and every row's result is independent of N.
 template <int H, int NW, int RR = kRows>
 struct MlpSmem {
+  static constexpr bool BF3 = kBf3<H>;
   static constexpr int R = RR, LDA = H + 4, LDS_S = 36;
-  float h1s[R][LDA] __attribute__((aligned(16)));     // tanh(fc1)
+  static constexpr int LDP = H + 8, PS = R * LDP;     // bf16 planes: rows padded by 16 B
+  float h1s[BF3 ? 0 : R][LDA] __attribute__((aligned(16)));                // tanh(fc1)
+  unsigned short h1p[BF3 ? 3 * PS : 0] __attribute__((aligned(16)));      // (BF3) its three bf16 planes
   float S[R][LDS_S] __attribute__((aligned(16)));     // [s(18) | 1 | 0...] per row
-  float osum[NW][R][3];                               // per-wave output-layer partial sums
+  float osum[H / 16][R][3];                           // per-column-tile output-layer partial sums
 };
 
 // Rows r < nvalid of the block must be in S[r][0..17] when gather() returns;
@@ -430,7 +569,8 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         const int r = 16 * rt + 4 * lg + j;
         const float h = tanh_f32(acc[rt][t][j]);                   // fc1 + tanh
         h1[rt][t][j] = h;
-        sm.h1s[r][n] = h;
+        if constexpr (kBf3<H>) put3<MlpSmem<H, NW, R>::PS>(sm.h1p, r * MlpSmem<H, NW, R>::LDP + n, h);
+        else sm.h1s[r][n] = h;
       }
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -440,18 +580,18 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  if constexpr (kBf3<H>)
+    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT>(sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc);
+  else
+    mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
   const int NQ = net == 0 ? 3 : 1;                                  // output columns of this net
-  float p[3][RT][4];
-#pragma unroll
-  for (int q = 0; q < 3; ++q)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) p[q][rt][j] = 0.0f;
+  // one partial per 16-column tile (DPP row sums), so the output layer sums
+  // the same H/16 partials in the same order whatever the wave count: the
+  // 8-wave policy kernel's log-probs are the 16-wave rowpass's bit for bit
+  float p[3][CT][RT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -461,46 +601,53 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         const float h = tanh_f32(acc[rt][t][j] + b2v[t]);           // fc2 + tanh
         acc[rt][t][j] = h;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) p[q][rt][j] = fmaf(h, w3[t][q], p[q][rt][j]);
+        for (int q = 0; q < 3; ++q) p[q][t][rt][j] = fmaf(h, w3[t][q], 0.0f);
       }
   // the DPP row sums; NQ is uniform per workgroup (3 actor, 1 critic)
-  float ps[3 * RT * 4];
+  constexpr int NP = CT * RT * 4;                                   // partials per output column
+  float ps[3 * NP];
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int t = 0; t < CT; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ps[(q * RT + rt) * 4 + j] = p[q][rt][j];
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ps[((q * CT + t) * RT + rt) * 4 + j] = p[q][t][rt][j];
   if (NQ == 3) {
-    row16_sum_n<3 * RT * 4>(ps);
+    row16_sum_n<3 * NP>(ps);
   } else {
-    float p0[RT * 4];
+    float p0[NP];
 #pragma unroll
-    for (int k = 0; k < RT * 4; ++k) p0[k] = ps[k];
-    row16_sum_n<RT * 4>(p0);
+    for (int k = 0; k < NP; ++k) p0[k] = ps[k];
+    row16_sum_n<NP>(p0);
 #pragma unroll
-    for (int k = 0; k < RT * 4; ++k) ps[k] = p0[k];
+    for (int k = 0; k < NP; ++k) ps[k] = p0[k];
   }
   if (li == 0) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       if (q >= NQ) break;
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
+      for (int t = 0; t < CT; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sm.osum[w][16 * rt + 4 * lg + j][q] = ps[(q * RT + rt) * 4 + j];
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            sm.osum[w * CT + t][16 * rt + 4 * lg + j][q] = ps[((q * CT + t) * RT + rt) * 4 + j];
     }
   }
   rp_barrier();
   PHASE_PROBE(3);
 }
 
-// output-layer pre-activation of row r, column d: wave partials in fixed order
-template <int NW, int R>
+// output-layer pre-activation of row r, column d: the NTL column-tile
+// partials in fixed order
+template <int NTL, int R>
 __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d) {
   float od = 0.0f;
 #pragma unroll
-  for (int k = 0; k < NW; ++k) od += osum[k][r][d];
+  for (int k = 0; k < NTL; ++k) od += osum[k][r][d];
   return od;
 }
 
@@ -516,7 +663,10 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
-  __shared__ __attribute__((aligned(16))) float dzs[R][LDA];     // dZ2
+  constexpr bool BF3 = kBf3<H>;
+  constexpr int LDP = H + 8, PS = R * LDP;
+  __shared__ __attribute__((aligned(16))) float dzs[BF3 ? 1 : R][BF3 ? 4 : LDA];   // dZ2
+  __shared__ __attribute__((aligned(16))) unsigned short dzp[BF3 ? 3 * PS : 8];    // (BF3) its bf16 planes
   __shared__ float ax[R][8];
   __shared__ float dz3s[R][4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
@@ -613,7 +763,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanh_f32(out_sum<NW, R>(sm.osum, r, d) + hb3s[d]);
+          th[d] = tanh_f32(out_sum<H / 16, R>(sm.osum, r, d) + hb3s[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           var[d] = hcs[0][d];
           dv[d] = ax[r][d] - mu[d];
@@ -643,7 +793,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
           dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        const float vc = out_sum<NW, R>(sm.osum, r, 0) + hb3s[3];
+        const float vc = out_sum<H / 16, R>(sm.osum, r, 0) + hb3s[3];
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
@@ -706,7 +856,8 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
           if constexpr (ACT) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
           else dh = dz3s[r][3] * w3[t][0];
           const float d2 = dh * (1.0f - h * h);                     // tanh backward
-          dzs[r][n] = d2;
+          if constexpr (BF3) put3<PS>(dzp, r * LDP + n, d2);
+          else dzs[r][n] = d2;
           d2v[rt][t][j] = d2;
           cb2 += d2;
           if constexpr (ACT) {
@@ -739,7 +890,10 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
+  if constexpr (BF3)
+    mfma_rows3<H, LDP, PS, H, RT, CT, true>(dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
+  else
+    mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
@@ -814,7 +968,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 // rollout step at 16k envs: fewer, larger workgroups lose more to the tail
 // than the halved weight ingest saves)
 constexpr int kPolRows = 32;   // rows per policy workgroup
-constexpr int kPolNW = 16;     // waves per policy workgroup at H = 256
+constexpr int kPolNW = 8;      // waves per policy workgroup at H = 256 (16: 61.6 vs 52.3 us per rollout step)
 
 template <int H, int NW, int MODE>
 __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float* __restrict__ obs,
@@ -862,7 +1016,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
   if (MODE == 1) {
-    value[i] = out_sum<NW, R>(sm.osum, r, 0) + P[L.b3c];
+    value[i] = out_sum<H / 16, R>(sm.osum, r, 0) + P[L.b3c];
     return;
   }
   float z[4];
@@ -872,7 +1026,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   float* logp = agent == 0 ? logp0 : logp1;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const float mu = max_action * tanh_f32(out_sum<NW, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
+    const float mu = max_action * tanh_f32(out_sum<H / 16, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
     gaussian_act(mu, P[L.ls + d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
   }
 }

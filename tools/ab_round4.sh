@@ -28,7 +28,12 @@ case "${1:-}" in
       else L=tools/_probe/libsatrl_$v.so; fi
       echo "== $v" >> "$LOG"
       env "${E[@]}" SATRL_LIB_PATH=$L PROBE_H=256 timeout -k 10 120 python3 tools/minibatch_time.py 4096 512 >> "$LOG" 2>&1
-      env "${E[@]}" SATRL_LIB_PATH=$L PROBE_H=64 timeout -k 10 120 python3 tools/minibatch_time.py 4096 >> "$LOG" 2>&1
+      if [ "${AB_H64:-1}" = "1" ]; then
+        env "${E[@]}" SATRL_LIB_PATH=$L PROBE_H=64 timeout -k 10 120 python3 tools/minibatch_time.py 4096 >> "$LOG" 2>&1
+      fi
+      if [ "${AB_POLICY:-0}" = "1" ]; then
+        env "${E[@]}" SATRL_LIB_PATH=$L timeout -k 10 120 python3 tools/policy_time.py >> "$LOG" 2>&1
+      fi
     done
     grep -v amdgpu.ids "$LOG"
     ;;
