@@ -4,7 +4,7 @@
 //   rowpass  gather, fc1, fc2 (f32 MFMA), output layers, losses, backprop to
 //            dZ2 and through fc2 (f32 MFMA) and fc1's tanh; writes H1, dZ2
 //            and partial slabs of every small gradient
-//   dW2      dZ2^T @ H1 split-K S ways: dw2_kernel (H <= 128) or hipBLASLt
+//   dW2      dZ2^T @ H1 split-K S ways: dw2_kernel (H <= 128), dw2_bf3_kernel (H = 256) or hipBLASLt
 //            (H = 256, dw2_blas.cpp)
 //   reduce   partial slabs -> G (fixed order), per-block squared norms per net
 //   adam     clip coefficient per net + Adam (torch single-tensor formula),
@@ -1107,9 +1107,117 @@ __global__ void __launch_bounds__(256) dw2_kernel(int mb, int S, int KR, int net
     for (int q = 0; q < 4; ++q) out[(int64_t)(n0 + 16 * w + 4 * lg + q) * H + m0 + 16 * j + li] = acc[j][q];
 }
 
+// ---------------------------------------------------------------------------
+// dW2 at H = 256 on the split-bf16 MFMA (kBf3; the rowpass's fc2 products'
+// arithmetic): the same grid and slabs as dw2_kernel -- workgroup (net,
+// 64x64 output tile, split s), rows [s*KR, (s+1)*KR) -- with each wave on a
+// 32x32 quarter of the tile (2 x 2 tiles of v_mfma_f32_16x16x32_bf16).
+// The reduction index (rows) must be the MFMA's k, so each 32-row chunk is
+// transposed on its way to LDS: thread (column l, row group w) loads eight
+// rows of one column of dZ2 and of H1 (each load instruction 256 contiguous
+// bytes), splits them (split3x8) and writes each plane's 8 bf16 as one 16-B
+// store at [column][k] (80-B rows: the stores and the operand reads are
+// bank-conflict free).  Two LDS buffers: chunk c+1's loads are in flight
+// under chunk c's MFMAs, one barrier per chunk.  Every sum has a fixed order.
+// ---------------------------------------------------------------------------
+template <int H>
+__global__ void __launch_bounds__(256) dw2_bf3_kernel(int mb, int S, int KR, int net_sel,
+                                                      const float* __restrict__ H1g, const float* __restrict__ dZ2g,
+                                                      float* __restrict__ p2) {
+  constexpr int TT = H / 64, LK = 40;                               // plane row: 32 k + 16-B pad
+  __shared__ __attribute__((aligned(16))) unsigned short pl[2][2][3][64][LK];   // [buf][dZ2 | H1][plane][col][k]
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, li = l & 15, lg = l >> 4;
+  const int b = blockIdx.x, s = b % S, tile = (b / S) % (TT * TT);
+  const int net = net_sel < 0 ? b / (S * TT * TT) : net_sel;
+  const int o0 = (tile / TT) * 64, n0 = (tile % TT) * 64;
+  const int r_begin = s * KR, nvalid = min(mb, r_begin + KR) - r_begin;
+  const float* Z = dZ2g + (int64_t)net * mb * H + o0 + l;
+  const float* Y = H1g + (int64_t)net * mb * H + n0 + l;
+  const int nchunks = (nvalid + 31) / 32;
+  // two register slots of staged rows: chunk c+2's loads go out while chunk
+  // c's MFMAs run and chunk c+1 is split into the other LDS buffer
+  float za[2][8], ya[2][8];
+  auto load = [&](int c, float (&zr)[8], float (&yr)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = min(r_begin + 32 * c + 8 * w + j, mb - 1);      // rows past the end: zeroed in put
+      zr[j] = Z[(int64_t)r * H];
+      yr[j] = Y[(int64_t)r * H];
+    }
+  };
+  auto put = [&](int c, int buf, float (&zr)[8], float (&yr)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (32 * c + 8 * w + j >= nvalid) { zr[j] = 0.0f; yr[j] = 0.0f; }
+    s8v zp[3], yp[3];
+    const float4 zf[2] = {make_float4(zr[0], zr[1], zr[2], zr[3]), make_float4(zr[4], zr[5], zr[6], zr[7])};
+    const float4 yf[2] = {make_float4(yr[0], yr[1], yr[2], yr[3]), make_float4(yr[4], yr[5], yr[6], yr[7])};
+    split3x8(zf, zp);
+    split3x8(yf, yp);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      *reinterpret_cast<s8v*>(&pl[buf][0][p][l][8 * w]) = zp[p];
+      *reinterpret_cast<s8v*>(&pl[buf][1][p][l][8 * w]) = yp[p];
+    }
+  };
+  const int wo = w >> 1, wn = w & 1;
+  f4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = f4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int buf) {
+    s8v a[2][3], bq[2][3];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a[x][p] = *reinterpret_cast<const s8v*>(&pl[buf][0][p][32 * wo + 16 * x + li][8 * lg]);
+        bq[x][p] = *reinterpret_cast<const s8v*>(&pl[buf][1][p][32 * wn + 16 * x + li][8 * lg]);
+      }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        acc[x][y] = mfma_bf16(a[x][2], bq[y][0], acc[x][y]);
+        acc[x][y] = mfma_bf16(a[x][0], bq[y][2], acc[x][y]);
+        acc[x][y] = mfma_bf16(a[x][1], bq[y][1], acc[x][y]);
+        acc[x][y] = mfma_bf16(a[x][1], bq[y][0], acc[x][y]);
+        acc[x][y] = mfma_bf16(a[x][0], bq[y][1], acc[x][y]);
+        acc[x][y] = mfma_bf16(a[x][0], bq[y][0], acc[x][y]);
+      }
+  };
+  load(0, za[0], ya[0]);
+  if (nchunks > 1) load(1, za[1], ya[1]);
+  put(0, 0, za[0], ya[0]);
+  __syncthreads();
+  // chunk c (even) in LDS buffer 0, its successor in slot 1; slots swap per chunk
+  for (int c = 0; c < nchunks; c += 2) {
+    if (c + 2 < nchunks) load(c + 2, za[0], ya[0]);
+    mma(0);
+    if (c + 1 < nchunks) put(c + 1, 1, za[1], ya[1]);
+    __syncthreads();
+    if (c + 1 >= nchunks) break;
+    if (c + 3 < nchunks) load(c + 3, za[1], ya[1]);
+    mma(1);
+    if (c + 2 < nchunks) put(c + 2, 0, za[0], ya[0]);
+    __syncthreads();
+  }
+  // acc[x][y][q] = dW2[o0 + 32wo + 16x + 4lg + q][n0 + 32wn + 16y + li]
+  float* out = p2 + ((int64_t)net * S + s) * H * H;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[(int64_t)(o0 + 32 * wo + 16 * x + 4 * lg + q) * H + n0 + 32 * wn + 16 * y + li] = acc[x][y][q];
+}
+
+constexpr int kDw3Wgs = 512;      // dw2_bf3_kernel workgroups to aim for (splits = this / tiles; 256 / 1024 slower)
 int dw2_splits(int H, int mb, int net) {
   const int tiles = (net < 0 ? 2 : 1) * (H / 64) * (H / 64);
-  int S = 256 / tiles;
+  int S = (H == 256 ? kDw3Wgs : 256) / tiles;
   const int maxS = (mb + kDwKC - 1) / kDwKC;
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
@@ -1731,7 +1839,7 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
   else if (H == 128)
     hipLaunchKernelGGL(dw2_kernel<128>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
   else
-    hipLaunchKernelGGL(dw2_kernel<256>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
+    hipLaunchKernelGGL(dw2_bf3_kernel<256>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
   LAUNCH_CHECK();
   return 0;
 }

@@ -255,7 +255,8 @@ class FusedMinibatch:
         # dW2: the hand-written split-K kernel for H <= 128 (hipBLASLt picks
         # K-serial tiles there: 12.5 us vs 3 us at H = 64); at H = 256 a
         # plain library GEMM (satrl_ppo_dw2_lib: hipBLASLt from the C ABI,
-        # split-K 4, 11.7 us vs 15 us for satrl_ppo_dw2; the plan times the
+        # split-K 4, 11.7 us; satrl_ppo_dw2's split-bf16 kernel measured 1.5 us
+        # slower per step, its f32 predecessor 3 us; the plan times the
         # library's solutions per shape, which matters for short splits)
         self.lib_gemm = learner.H >= 256
         if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob

@@ -12,22 +12,11 @@ SRC = os.path.join(ROOT, "ppo-rl-satellite_amd", "csrc", "ppo_kernels.hip")
 OUT = os.path.join(ROOT, "tools", "_probe", "ab4")
 
 VARIANTS = {
-    # (round 4's L2 warm-up of W2 / W2T, reduce chunk counts and Adam's table
-    # load were measured against this harness; EXPERIMENTS.md)
-    # the bf16x3 fc2 products: B prefetch distance / A buffering
-    "b3_d3": [("constexpr int kBPD3 = 2;", "constexpr int kBPD3 = 3;")],
-    "b3_d4a1": [("constexpr int kBPD3 = 2;", "constexpr int kBPD3 = 4;"),
-                ("constexpr int kADB3 = 2;", "constexpr int kADB3 = 1;")],
-    "b3_d6a1": [("constexpr int kBPD3 = 2;", "constexpr int kBPD3 = 6;"),
-                ("constexpr int kADB3 = 2;", "constexpr int kADB3 = 1;")],
-    "b3_d2a1": [("constexpr int kADB3 = 2;", "constexpr int kADB3 = 1;")],
-    # 8 waves per H 256 workgroup (2 column tiles each): half the A-plane LDS reads
-    "nw8": [("constexpr int kNW256 = 16;", "constexpr int kNW256 = 8;")],
-    "nw8a1": [("constexpr int kNW256 = 16;", "constexpr int kNW256 = 8;"),
-              ("constexpr int kADB3 = 2;", "constexpr int kADB3 = 1;")],
-    "pol8": [("constexpr int kPolNW = 16;", "constexpr int kPolNW = 8;")],
-    "pol8a1": [("constexpr int kPolNW = 16;", "constexpr int kPolNW = 8;"),
-               ("constexpr int kADB3 = 2;", "constexpr int kADB3 = 1;")],
+    # (round 4: L2 warm-up of W2 / W2T, reduce chunk counts, Adam's table load,
+    # bf16x3 prefetch depth / A buffering / wave counts were measured against
+    # this harness; EXPERIMENTS.md)
+    "dw3s16": [("constexpr int kDw3Wgs = 256;", "constexpr int kDw3Wgs = 512;")],
+    "dw3s32": [("constexpr int kDw3Wgs = 256;", "constexpr int kDw3Wgs = 1024;")],
 }
 
 
