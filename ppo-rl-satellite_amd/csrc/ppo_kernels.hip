@@ -474,6 +474,11 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
 // barriers that leave the global stores and early weight chunks in flight
 // measured no faster, EXPERIMENTS.md round 3).
 __device__ __forceinline__ void rp_barrier() { __syncthreads(); }
+// a workgroup barrier that waits for this wave's LDS operations only, not for
+// its outstanding global loads / stores
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+constexpr bool kPreB3 = true;     // split-bf16 fc2: phase B's first weight chunks issued under fc1
+constexpr bool kLdsBar3 = false;  // split-bf16 fc2: an LDS-only barrier before phase B
 
 // Shared-memory block and forward pass (phases A, B and the output-layer dot
 // products of C) common to rowpass_kernel and policy_kernel, so the rollout's
@@ -543,6 +548,9 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(8);
   rp_barrier();
   PHASE_PROBE(9);
+  // (split-bf16 fc2) phase B's first weight chunks go out now, under fc1
+  WPre<CT> preB;
+  if constexpr (kBf3<H> && kPreB3) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   float4 bw1[CT][2];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -576,12 +584,14 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
     }
   if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
   PHASE_PROBE(11);
-  rp_barrier();
+  if constexpr (kBf3<H> && kLdsBar3) lds_barrier();               // (the early chunks stay in flight)
+  else rp_barrier();
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
   if constexpr (kBf3<H>)
-    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT>(sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc);
+    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, kPreB3>(
+        sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   else
     mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);

@@ -13,10 +13,22 @@ OUT = os.path.join(ROOT, "tools", "_probe", "ab4")
 
 VARIANTS = {
     # (round 4: L2 warm-up of W2 / W2T, reduce chunk counts, Adam's table load,
-    # bf16x3 prefetch depth / A buffering / wave counts were measured against
-    # this harness; EXPERIMENTS.md)
-    "dw3s16": [("constexpr int kDw3Wgs = 256;", "constexpr int kDw3Wgs = 512;")],
-    "dw3s32": [("constexpr int kDw3Wgs = 256;", "constexpr int kDw3Wgs = 1024;")],
+    # bf16x3 prefetch depth / A buffering / wave counts, dW2 split counts were
+    # measured against this harness; EXPERIMENTS.md)
+    "nopreb": [("constexpr bool kPreB3 = true;", "constexpr bool kPreB3 = false;")],
+    "ldsbar": [("constexpr bool kLdsBar3 = false;", "constexpr bool kLdsBar3 = true;")],
+    # timing probes only (wrong results): the split-bf16 fc2 without the weights' split VALU / without
+    # the per-chunk A-plane LDS reads
+    "t_nosplit": [("""    s8v bs[3];
+    split3x8(b[t], bs);""", """    s8v bs[3];
+    bs[0] = __builtin_bit_cast(s8v, b[t][0]);
+    bs[1] = __builtin_bit_cast(s8v, b[t][1]);
+    bs[2] = __builtin_bit_cast(s8v, b[t][0]);""")],
+    "t_noalds": [("""    } else {
+      a3_chunk<LDP, PS, RT>(ap + 32 * c, aa[0]);
+    }""", """    } else {
+      if (c == 0) a3_chunk<LDP, PS, RT>(ap, aa[0]);
+    }""")],
 }
 
 
