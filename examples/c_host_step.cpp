@@ -129,12 +129,8 @@ int main(int argc, char** argv) {
   int64_t off[SATRL_PPO_NOFF];
   PPO_OK(satrl_ppo_layout(H, off));
   const int64_t total = off[SATRL_PPO_TOTAL];
-  std::vector<float> P(total), W2T(2 * (size_t)H * H), src((size_t)mb * 32, 0.0f);
+  std::vector<float> P(total), src((size_t)mb * 32, 0.0f);
   for (auto& v : P) v = unif(-0.06f, 0.06f);
-  for (int net = 0; net < 2; ++net)               // fc2.weight^T per net: W2T[net][k][n] = W2[net][n][k]
-    for (int n = 0; n < H; ++n)
-      for (int k = 0; k < H; ++k)
-        W2T[((size_t)net * H + k) * H + n] = P[off[SATRL_PPO_OFF_W2] + ((size_t)net * H + n) * H + k];
   for (int r = 0; r < mb; ++r) {                  // packed rows: s | a | logp | adv | v_target
     float* row = &src[(size_t)r * 32];
     for (int c = 0; c < 18; ++c) row[c] = unif(-1.0f, 1.0f);
@@ -157,7 +153,10 @@ int main(int argc, char** argv) {
   PPO_OK(satrl_ppo_sizes(H, mb, &nwg, &nblk));
 
   float* d_P = dev(P);
-  float* d_W2T = dev(W2T);
+  // the fc2 operand image (pre-split bf16 planes at H = 256), built on the device from P
+  const int64_t w2x = satrl_ppo_w2x_floats(H);
+  float* d_W2X = dev<float>((size_t)w2x);
+  PPO_OK(satrl_ppo_w2x_sync(H, -1, d_P, d_W2X, st));
   float* d_M = dev<float>(total);
   float* d_V = dev<float>(total);
   float* d_G = dev<float>(total);
@@ -183,14 +182,14 @@ int main(int argc, char** argv) {
   PPO_OK(satrl_ppo_dw2_lib_workspace(H, mb, -1, S, &wsb, &algo));
   uint8_t* d_ws = wsb > 0 ? dev<uint8_t>((size_t)wsb) : nullptr;
 
-  PPO_OK(satrl_ppo_rowpass(H, mb, -1, d_src, nullptr, d_P, d_W2T, 0.1f, 0.01f, 1.6f, d_H1, d_dZ2, d_pt, d_pw, st));
+  PPO_OK(satrl_ppo_rowpass(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1, d_dZ2, d_pt, d_pw, st));
   HIP_OK(hipStreamSynchronize(st));
   save(out, "ppo_H1.f32", host(d_H1, 2 * (size_t)mb * H));
   save(out, "ppo_dZ2.f32", host(d_dZ2, 2 * (size_t)mb * H));
   PPO_OK(satrl_ppo_dw2_lib(H, mb, -1, S, d_H1, d_dZ2, d_p2, d_ws, wsb, st));
   PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, d_pw, d_pt, d_G, d_nsq, d_steps, st));
   PPO_OK(satrl_ppo_adam(H, mb, -1, d_nsq, d_steps, d_bct, (int)(bct.size() / 2), d_lr, 0.9f, 0.999f, 1e-5f, 0.5f, 1,
-                        d_G, d_P, d_M, d_V, d_W2T, st));
+                        d_G, d_P, d_M, d_V, d_W2X, st));
   HIP_OK(hipStreamSynchronize(st));
   save(out, "ppo_P0.f32", P);
   save(out, "ppo_src.f32", src);
@@ -199,7 +198,7 @@ int main(int argc, char** argv) {
   save(out, "ppo_P.f32", host(d_P, (size_t)total));
   save(out, "ppo_M.f32", host(d_M, (size_t)total));
   save(out, "ppo_V.f32", host(d_V, (size_t)total));
-  save(out, "ppo_W2T.f32", host(d_W2T, 2 * (size_t)H * H));
+  save(out, "ppo_W2T.f32", host(d_W2X, (size_t)w2x));
   save(out, "ppo_steps.f64", host(d_steps, 2));
   char kname[256] = {0};
   int used = -1;

@@ -104,18 +104,29 @@ int satrl_ppo_reduce_dp(int H, int mb, int net, int world, float* G, double* nsq
  * torch.optim.Adam does), 1.0 past the table.                             */
 int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
-                   float* P, float* M, float* V, float* W2T /* nullable: also write fc2.weight^T */,
+                   float* P, float* M, float* V, void* W2X /* nullable: also refresh the fc2 operand image */,
                    void* stream);
 
+/* The fc2 operand image W2X the rowpass reads for its two H x H products
+ * (and satrl_ppo_adam keeps current), satrl_ppo_w2x_floats(H) floats:
+ *   H <= 128  f32 fc2.weight^T per net, [2][H][H];
+ *   H = 256   fc2.weight and its transpose split once into three bf16 planes
+ *             (hi + mid + lo == the f32 weight exactly), the split-bf16 MFMA's
+ *             B operands: u16 [net][W2, W2^T][hi, mid, lo][H][H].
+ * satrl_ppo_w2x_sync builds it from P (net -1: both) -- after a load or any
+ * write to fc2.weight outside satrl_ppo_adam.                               */
+int64_t satrl_ppo_w2x_floats(int H);
+int satrl_ppo_w2x_sync(int H, int net, const float* P, void* W2X, void* stream);
+
 /* The row-parallel part of one minibatch step in ONE launch (a workgroup
- * per net and 32-row block): gather + fc1 + tanh, fc2 (f32 MFMA), output
- * layer, the net's loss and gradients, backprop through fc2 (f32 MFMA on
- * W2T = fc2.weight^T per net, [2][H][H]) and tanh(fc1).  Rows are
+ * per net and 32-row block): gather + fc1 + tanh, fc2 (f32 MFMA; split-bf16
+ * at H = 256), output layer, the net's loss and gradients, backprop through
+ * fc2 (the fc2 operand image W2X, above) and tanh(fc1).  Rows are
  * src[idx[r]] (idx nullable: rows 0..mb-1 of src, contiguous).  Writes H1
  * and dZ2 [2][mb][H] (inputs of the dW2 GEMM), the tail partial slabs
  * [n_head_wg][6H+12] and the [dW1 | db1] partial slabs [n_head_wg][2][H][20]
  * (n_head_wg from satrl_ppo_sizes).                                      */
-int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const float* W2T,
+int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream);
 
@@ -126,7 +137,7 @@ int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* i
  * first epoch's first minibatch recomputes the rollout's log-probs bit for
  * bit", i.e. every ratio == 1.0f exactly.  net must include the actor.    */
 int satrl_ppo_rowpass_ratio(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                            const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
+                            const void* W2X, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
                             float* ptail, float* pw1, float* ratio, void* stream);
 
 /* H = 64 / 128 (BASELINE configs[1]): the rowpass with the dW2 product fused
@@ -138,7 +149,7 @@ int satrl_ppo_rowpass_ratio(int H, int mb, int net, const float* src, const int6
  * minibatch step is three launches (rowpass_dw2, reduce, adam).            */
 int satrl_ppo_row_blocks(int H, int mb);
 int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                          const float* W2T, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
+                          const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
                           float* pw1, void* stream);
 
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result

@@ -367,6 +367,15 @@ __device__ __forceinline__ void split3x8(const float4 (&x)[2], s8v (&o)[3]) {
 __device__ __forceinline__ f4 mfma_bf16(s8v a, s8v b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// the six partial products of one 16x16 tile and 32-wide k chunk, smallest first
+__device__ __forceinline__ f4 mfma6(const s8v (&a)[3], const s8v (&bs)[3], f4 c) {
+  c = mfma_bf16(a[2], bs[0], c);
+  c = mfma_bf16(a[0], bs[2], c);
+  c = mfma_bf16(a[1], bs[1], c);
+  c = mfma_bf16(a[1], bs[0], c);
+  c = mfma_bf16(a[0], bs[1], c);
+  return mfma_bf16(a[0], bs[0], c);
+}
 // one 32-wide k chunk: A planes (registers) x B (f32, split here)
 template <int RT, int CT>
 __device__ __forceinline__ void mfma3_regs(const s8v (&a)[RT][3], const float4 (&b)[CT][2], f4 (&acc)[RT][CT]) {
@@ -375,15 +384,16 @@ __device__ __forceinline__ void mfma3_regs(const s8v (&a)[RT][3], const float4 (
     s8v bs[3];
     split3x8(b[t], bs);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      acc[rt][t] = mfma_bf16(a[rt][2], bs[0], acc[rt][t]);
-      acc[rt][t] = mfma_bf16(a[rt][0], bs[2], acc[rt][t]);
-      acc[rt][t] = mfma_bf16(a[rt][1], bs[1], acc[rt][t]);
-      acc[rt][t] = mfma_bf16(a[rt][1], bs[0], acc[rt][t]);
-      acc[rt][t] = mfma_bf16(a[rt][0], bs[1], acc[rt][t]);
-      acc[rt][t] = mfma_bf16(a[rt][0], bs[0], acc[rt][t]);
-    }
+    for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma6(a[rt], bs, acc[rt][t]);
   }
+}
+// the same on B planes split beforehand (the fc2 operand image, below)
+template <int RT, int CT>
+__device__ __forceinline__ void mfma3s_regs(const s8v (&a)[RT][3], const s8v (&b)[CT][3], f4 (&acc)[RT][CT]) {
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma6(a[rt], b[t], acc[rt][t]);
 }
 template <int LDP, int PS, int RT>
 __device__ __forceinline__ void a3_chunk(const unsigned short* __restrict__ ap, s8v (&a)[RT][3]) {
@@ -431,6 +441,87 @@ __device__ __forceinline__ void mfma_rows3(const unsigned short* __restrict__ A,
     }
     mfma3_regs<RT, CT>(aa[kADB3 == 2 ? c % 2 : 0], bb[c % NB], acc);
   }
+}
+
+// ---------------------------------------------------------------------------
+// The fc2 operand image (W2X) at H = 256: fc2.weight and its transpose split
+// into their three bf16 planes ONCE per parameter change -- by adam_kernel
+// beside the f32 update, or by satrl_ppo_w2x_sync from P -- instead of in the
+// registers of every rowpass workgroup (256 workgroups x two phases, each
+// splitting the whole net: 36 VALU per chunk and wave, ≈3.4 us of the step
+// measured, EXPERIMENTS.md round 4).  The splits are the same RNE conversions
+// and exact subtractions, so every plane -- hence every MFMA input and result
+// bit -- is the in-register split's.  Layout (bf16 elements):
+//   [net][0: W2 [n][k] (phase B), 1: W2^T [k][n] (phase D)][plane hi, mid, lo][H][H]
+// At H <= 128 W2X is the f32 W2^T [2][H][H] the f32 path reads.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int64_t w2x_plane(int H, int net, int which) { return (int64_t)(net * 2 + which) * 3 * H * H; }
+// elements of the W2X buffer, in floats
+__host__ __device__ constexpr int64_t w2x_floats(int H) { return H == 256 ? 6LL * H * H : 2LL * H * H; }
+template <int CT>
+struct B3Pre {                    // early-issued pre-split B chunks (kBPD of them)
+  s8v bb[kBPD][CT][3];
+};
+// one 32-wide k chunk of pre-split B: the three planes (plane stride PSB) of
+// the lane's 8 k, as the f32 path's b_chunk holds them before its split
+template <int CT, int LDB, int PSB>
+__device__ __forceinline__ void b3_chunk(const unsigned short* __restrict__ bp, s8v (&b)[CT][3]) {
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) b[t][p] = *reinterpret_cast<const s8v*>(bp + (int64_t)p * PSB + 16 * t * LDB);
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int LDB, int CT>
+__device__ __forceinline__ void mfma_rows3s_pre(const unsigned short* __restrict__ B, int n0, B3Pre<CT>& pre) {
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const unsigned short* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
+#pragma unroll
+  for (int c = 0; c < kBPD; ++c) b3_chunk<CT, LDB, LDB * LDB>(bp + 32 * c, pre.bb[c]);
+}
+// mfma_rows3 on B planes split beforehand: B = three bf16 planes [K rows of
+// LDB] (plane stride K * LDB), kBPD3 chunks ahead, the first kBPD optionally
+// issued early (pre); the MFMA sequence is mfma_rows3's
+template <int K, int LDP, int PS, int LDB, int RT, int CT, bool PRE = false>
+__device__ __forceinline__ void mfma_rows3s(const unsigned short* __restrict__ A, const unsigned short* __restrict__ B,
+                                            int n0, f4 (&acc)[RT][CT], const B3Pre<CT>* pre = nullptr) {
+  constexpr int NC = K / 32, PSB = K * LDB;
+  constexpr int BPD = kBPD3 < NC ? kBPD3 : NC, NB = BPD + 1;
+  static_assert(!PRE || BPD >= kBPD, "early-issued chunks fit the ring");
+  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+  const unsigned short* ap = A + i * LDP + 8 * g;
+  const unsigned short* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
+  s8v bb[NB][CT][3];
+  s8v aa[RT][3];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int c = 0; c < kBPD; ++c)
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bb[c][t][p] = pre->bb[c][t][p];
+#pragma unroll
+    for (int c = kBPD; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (c + BPD < NC) b3_chunk<CT, LDB, PSB>(bp + 32 * (c + BPD), bb[(c + BPD) % NB]);
+    a3_chunk<LDP, PS, RT>(ap + 32 * c, aa);
+    mfma3s_regs<RT, CT>(aa, bb[c % NB], acc);
+  }
+}
+// the three planes of 4 consecutive elements v (at e, plane stride PS) as
+// three 8-B stores
+__device__ __forceinline__ void put3x4(unsigned short* __restrict__ img, int64_t e, int64_t PS, float4 v) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3x2(f2v{v.x, v.y}, h0, m0, l0);
+  split3x2(f2v{v.z, v.w}, h1, m1, l1);
+  *reinterpret_cast<uint2*>(img + e) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(img + PS + e) = make_uint2(m0, m1);
+  *reinterpret_cast<uint2*>(img + 2 * PS + e) = make_uint2(l0, l1);
 }
 // the three planes of x at element e of an LDS plane image (plane stride PS)
 template <int PS>
@@ -502,8 +593,9 @@ struct MlpSmem {
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
 // tanh(fc1) goes to h1out[r * H + n].
-template <int H, int NW, int R, bool APRE, class Gather>
-__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P, int net, int nvalid,
+template <int H, int NW, int R, bool APRE, bool W2S, class Gather>
+__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P,
+                                            const unsigned short* __restrict__ w2s, int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
                                             f4 (&acc)[R / 16][H / 16 / NW],
                                             float (&h1)[R / 16][H / 16 / NW][4],
@@ -549,8 +641,12 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   rp_barrier();
   PHASE_PROBE(9);
   // (split-bf16 fc2) phase B's first weight chunks go out now, under fc1
+  // (W2S: from the pre-split planes of this net's fc2.weight, w2s)
+  static_assert(!W2S || kBf3<H>, "pre-split weights feed the split-bf16 path");
   WPre<CT> preB;
-  if constexpr (kBf3<H> && kPreB3) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
+  B3Pre<CT> preBs;
+  if constexpr (W2S) mfma_rows3s_pre<H, CT>(w2s, n0, preBs);
+  else if constexpr (kBf3<H> && kPreB3) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   float4 bw1[CT][2];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -589,7 +685,9 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  if constexpr (kBf3<H>)
+  if constexpr (W2S)
+    mfma_rows3s<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, true>(sm.h1p, w2s, n0, acc, &preBs);
+  else if constexpr (kBf3<H>)
     mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, kPreB3>(
         sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   else
@@ -664,7 +762,7 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
 template <int H, int NW, int R = kRows, bool FDW2 = false>
 __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
-                                                      const float* __restrict__ W2T, float epsilon, float ent_coef,
+                                                      const void* __restrict__ W2X, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1, int net_sel, float* __restrict__ p2,
@@ -757,11 +855,16 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
       head_consts();
     }
   };
-  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather, FDW2 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc,
-                              h1, w3);
+  // the fc2 operand image: pre-split bf16 planes at H = 256, else f32 W2^T
+  const float* W2T = static_cast<const float*>(W2X);
+  const unsigned short* W2p = static_cast<const unsigned short*>(W2X);
+  mlp_forward<H, NW, R, true, BF3>(sm, P, BF3 ? W2p + w2x_plane(H, net, 0) : nullptr, net, mb - r0, gather,
+                                   FDW2 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
-  mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
+  B3Pre<CT> preDs;
+  if constexpr (BF3) mfma_rows3s_pre<H, CT>(W2p + w2x_plane(H, net, 1), n0, preDs);
+  else mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -901,7 +1004,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
   if constexpr (BF3)
-    mfma_rows3<H, LDP, PS, H, RT, CT, true>(dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
+    mfma_rows3s<H, LDP, PS, H, RT, CT, true>(dzp, W2p + w2x_plane(H, net, 1), n0, acc, &preDs);
   else
     mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
@@ -1021,7 +1124,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW, R, false>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  mlp_forward<H, NW, R, false, false>(sm, P, nullptr, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
@@ -1442,6 +1545,38 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
 // float4 per thread, and the updated tile goes out transposed through LDS
 // into W2T (coalesced).  Blocks [nbw, ...): the rest of the layout, float4.
 // ---------------------------------------------------------------------------
+// The updated 32x32 tile tb of net's fc2.weight (thread t holds row n0 + t/8,
+// columns k0 + (t%8)*4 .. +3 in v) into the fc2 operand image: at H = 256
+// its bf16 planes and those of its transpose, else the f32 transpose (through
+// LDS, so every store is coalesced).  Every thread of the block calls it.
+__device__ __forceinline__ void w2x_tile(int H, int net, int tb, float4 v, void* __restrict__ W2X,
+                                         float (&tile)[32][33]) {
+  const int t = threadIdx.x, nl = t >> 3, kl = (t & 7) * 4, ntc = H / 32;
+  const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
+  const bool bf3 = H == 256;
+  unsigned short* X = static_cast<unsigned short*>(W2X);
+  const int64_t HH = (int64_t)H * H;
+  if (bf3) put3x4(X + w2x_plane(H, net, 0), (int64_t)(n0 + nl) * H + k0 + kl, HH, v);   // W2 [n][k]
+  tile[nl][kl] = v.x; tile[nl][kl + 1] = v.y; tile[nl][kl + 2] = v.z; tile[nl][kl + 3] = v.w;
+  __syncthreads();
+  // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
+  const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
+  if (bf3) put3x4(X + w2x_plane(H, net, 1), (int64_t)(k0 + nl) * H + n0 + kl, HH, o);
+  else reinterpret_cast<float4*>(W2X)[((int64_t)net * HH + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
+}
+
+// the fc2 operand image of P (satrl_ppo_w2x_sync): adam_kernel's W2 blocks
+// without the step
+__global__ void __launch_bounds__(256) w2x_sync_kernel(int H, int net_sel, const float* __restrict__ P,
+                                                       void* __restrict__ W2X) {
+  __shared__ float tile[32][33];
+  const int t = threadIdx.x, ntc = H / 32, tb = blockIdx.x % (ntc * ntc);
+  const int net = net_sel < 0 ? (int)(blockIdx.x / (ntc * ntc)) : net_sel;
+  const int n = (tb / ntc) * 32 + (t >> 3), k = (tb % ntc) * 32 + (t & 7) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(P + (int64_t)net * H * H + (int64_t)n * H + k);
+  w2x_tile(H, net, tb, v, W2X, tile);
+}
+
 __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p, float coef, float step_size,
                                            float bc2s, float w1, float w2, float beta2, float eps, int use_clip) {
   if (use_clip) g = g * coef;                                      // grads.mul_(clip_coef_clamped)
@@ -1457,7 +1592,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
                                                    float beta2, float eps, float max_norm, int use_clip,
                                                    const float* __restrict__ G, float* __restrict__ P,
                                                    float* __restrict__ M, float* __restrict__ V,
-                                                   float* __restrict__ W2T, int net_sel) {
+                                                   void* __restrict__ W2X, int net_sel) {
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float tile[32][33];
@@ -1533,16 +1668,8 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   P4[e4] = pn;
   M4[e4] = m;
   V4[e4] = v;
-  if ((int)blockIdx.x < nbw && W2T != nullptr) {                   // keep fc2.weight^T for the dH1 MFMA
-    const int nl = t >> 3, kl = (t & 7) * 4;
-    tile[nl][kl] = pn.x; tile[nl][kl + 1] = pn.y; tile[nl][kl + 2] = pn.z; tile[nl][kl + 3] = pn.w;
-    __syncthreads();
-    const int tb = blockIdx.x % (ntc * ntc);                       // (net as above)
-    const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
-    // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
-    const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
-    reinterpret_cast<float4*>(W2T)[((int64_t)net * H * H + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
-  }
+  if ((int)blockIdx.x < nbw && W2X != nullptr)                     // keep the fc2 operand image current
+    w2x_tile(H, net, blockIdx.x % (ntc * ntc), pn, W2X, tile);
 }
 
 // ---------------------------------------------------------------------------
@@ -1776,13 +1903,13 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
 // every rowpass launch: fdw2 (H <= 128) writes the block's dW2 partial to p2
 // instead of H1 / dZ2; ratio (nullable) receives the actor's per-row ratio
 static int launch_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                          const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
+                          const void* W2X, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
                           float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream) {
   const int R = rows_per_wg(H, mb), nrb = n_head_wg(H, mb);
   dim3 g((net < 0 ? 2 : 1) * nrb);   // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
-#define RP_ARGS mb, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio
+#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio
   if (H == 64 && fdw2)
     hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true>), g, dim3(256), 0, s, RP_ARGS);
   else if (H == 64)
@@ -1800,22 +1927,22 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
   return 0;
 }
 
-int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const float* W2T,
+int satrl_ppo_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
                       float epsilon, float ent_coef, float max_action, float* H1, float* dZ2, float* ptail,
                       float* pw1, void* stream) {
-  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1)
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !H1 || !dZ2 || !ptail || !pw1)
     return -1;
-  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, nullptr,
+  return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, nullptr,
                         nullptr, false, stream);
 }
 
 int satrl_ppo_rowpass_ratio(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                            const float* W2T, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
+                            const void* W2X, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
                             float* ptail, float* pw1, float* ratio, void* stream) {
-  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !H1 || !dZ2 || !ptail || !pw1 ||
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !H1 || !dZ2 || !ptail || !pw1 ||
       !ratio)
     return -1;
-  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, nullptr,
+  return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, nullptr,
                         ratio, false, stream);
 }
 
@@ -1825,11 +1952,11 @@ int satrl_ppo_row_blocks(int H, int mb) {
 }
 
 int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                          const float* W2T, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
+                          const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
                           float* pw1, void* stream) {
-  if ((H != 64 && H != 128) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2T || !p2 || !ptail || !pw1)
+  if ((H != 64 && H != 128) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !p2 || !ptail || !pw1)
     return -1;
-  return launch_rowpass(H, mb, net, src, idx, P, W2T, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
+  return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
                         nullptr, true, stream);
 }
 
@@ -1942,13 +2069,24 @@ int satrl_ppo_allreduce_peer(int H, int mb, int world, int rank, void* const* bu
 
 int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
-                   float* P, float* M, float* V, float* W2T, void* stream) {
+                   float* P, float* M, float* V, void* W2X, void* stream) {
   if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P ||
       !M || !V)
     return -1;
   const int nblk = n_blocks(geom(H, mb, 1, net));
   hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq,
-                     steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2T, net);
+                     steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2X, net);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int64_t satrl_ppo_w2x_floats(int H) { return valid_h(H) ? w2x_floats(H) : -1; }
+
+int satrl_ppo_w2x_sync(int H, int net, const float* P, void* W2X, void* stream) {
+  if (!valid_h(H) || net < -1 || net > 1 || !P || !W2X) return -1;
+  const int ntc = H / 32;
+  hipLaunchKernelGGL(w2x_sync_kernel, dim3((net < 0 ? 2 : 1) * ntc * ntc), dim3(256), 0, (hipStream_t)stream, H, net,
+                     P, W2X);
   LAUNCH_CHECK();
   return 0;
 }

@@ -121,6 +121,8 @@ _SIGS = {
     "satrl_ppo_rowpass_ratio": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                                  _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_row_blocks": ([C.c_int, C.c_int], C.c_int),
+    "satrl_ppo_w2x_floats": ([C.c_int], _i64),
+    "satrl_ppo_w2x_sync": ([C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                                _vp, _vp, _vp], C.c_int),
     "satrl_peer_buffer_bytes": ([_i64, C.c_int, _vp], C.c_int),

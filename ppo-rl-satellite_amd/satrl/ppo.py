@@ -177,6 +177,41 @@ def ppo_layout(H):
     return dict(zip(OFF_NAMES, [int(v) for v in off]))
 
 
+def w2x_floats(H):
+    """f32 elements of the fc2 operand image (satrl_ppo_w2x_floats)."""
+    n = int(_lib.lib().satrl_ppo_w2x_floats(int(H)))
+    if n <= 0:
+        raise ValueError(f"hidden width {H} not supported")
+    return n
+
+
+def _split3(x):
+    """x (f32) = hi + mid + lo exactly, each round-to-nearest bf16 (as int16 bits)."""
+    hi = x.to(torch.bfloat16)
+    r = x - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return [t.view(torch.int16) for t in (hi, mid, lo)]
+
+
+def w2x_image(W2, H):
+    """Host statement of satrl_ppo_w2x_sync: the fc2 operand image of the two
+    nets' fc2.weight W2 (flat [2*H*H] f32), as the f32 tensor the kernels read."""
+    W2 = W2.reshape(2, H, H)
+    if H != 256:
+        return W2.transpose(1, 2).contiguous().reshape(-1)
+    planes = [torch.stack(_split3(w.contiguous())) for n in range(2) for w in (W2[n], W2[n].t())]
+    return torch.stack(planes).reshape(-1).view(torch.float32).clone()
+
+
+def w2x_decode(img, H):
+    """fc2.weight^T per net [2, H, H] f32 from an operand image."""
+    if H != 256:
+        return img.view(2, H, H)
+    p = img.view(torch.int16).view(2, 2, 3, H, H).view(torch.bfloat16).float()
+    return (p[:, 1, 0] + p[:, 1, 1]) + p[:, 1, 2]
+
+
 DW2_PLANS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dw2_plans.json")
 _dw2_table = None
 
@@ -676,7 +711,9 @@ class PPOLearner:
         self.critic = critic.to(self.device)
         P = self.P
         self.W2v = P[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
-        self.W2T = torch.zeros(2 * H * H, **f32)                 # fc2.weight^T per net (rowpass backprop)
+        # the fc2 operand image the rowpass reads (f32 fc2.weight^T, or at H = 256 the
+        # pre-split bf16 planes of fc2.weight and its transpose; satrl_ppo.h)
+        self.W2T = torch.zeros(w2x_floats(H), **f32)
         self.GW2v = self.G[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
         W1 = P[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
         self.GW1v = self.G[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
@@ -738,10 +775,18 @@ class PPOLearner:
 
     # -- update -----------------------------------------------------------------
     def sync_w2t(self):
-        """Refresh fc2.weight^T from P (Adam keeps it current during an update;
-        this covers loads / external writes between updates)."""
-        H = self.H
-        self.W2T.view(2, H, H).copy_(self.W2v.transpose(1, 2))
+        """Refresh the fc2 operand image from P (Adam keeps it current during an
+        update; this covers loads / external writes between updates)."""
+        if self.device.type == "cuda":
+            check(_lib.lib().satrl_ppo_w2x_sync(self.H, -1, ptr(self.P), ptr(self.W2T), stream_ptr()),
+                  "satrl_ppo_w2x_sync")
+        else:
+            self.W2T.copy_(w2x_image(self.P[:2 * self.H * self.H], self.H))
+
+    def w2t_f32(self):
+        """fc2.weight^T per net [2, H, H] f32 decoded from the operand image
+        (planes summed: hi + mid + lo is the weight exactly)."""
+        return w2x_decode(self.W2T, self.H)
 
     def stepper(self, mb):
         if mb not in self._steppers:

@@ -237,8 +237,11 @@ def test_fused_step_vs_torch_autograd(H, split, mb):
         got = P[k].reshape(ref.shape)
         assert torch.allclose(got, ref, rtol=1e-5, atol=2e-7), (k, (got - ref).abs().max().item())
     assert L.steps.cpu().tolist() == [1.0, 1.0]
-    # Adam also refreshed fc2.weight^T (the dH1 operand of the next rowpass)
-    assert torch.equal(L.W2T.view(2, H, H), L.P[:2 * H * H].view(2, H, H).transpose(1, 2))
+    # Adam also refreshed the fc2 operand image (fc2.weight^T, or at H = 256 the
+    # pre-split planes of fc2.weight and its transpose): bitwise the image of P
+    from satrl.ppo import w2x_image
+    assert torch.equal(L.W2T.view(torch.int32), w2x_image(L.P[:2 * H * H], H).view(torch.int32))
+    assert torch.equal(L.w2t_f32(), L.P[:2 * H * H].view(2, H, H).transpose(1, 2))
 
 
 def _packed_rows(B, seed=0):

@@ -24,6 +24,11 @@ VARIANTS = {
     bs[0] = __builtin_bit_cast(s8v, b[t][0]);
     bs[1] = __builtin_bit_cast(s8v, b[t][1]);
     bs[2] = __builtin_bit_cast(s8v, b[t][0]);""")],
+    # timing probe (wrong results): Adam's bias corrections as constants, no
+    # dependent table load behind the step-count load
+    "t_nobct": [("""    const double bc1 = st < bct_len ? bct[2 * st] : 1.0;
+    const double bc2s = st < bct_len ? bct[2 * st + 1] : 1.0;""", """    const double bc1 = st < 0 ? bct[0] : 0.5;
+    const double bc2s = st < 0 ? bct[1] : 0.25;""")],
     "t_noalds": [("""    } else {
       a3_chunk<LDP, PS, RT>(ap + 32 * c, aa[0]);
     }""", """    } else {
