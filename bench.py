@@ -472,7 +472,7 @@ def run(a, world):
     rowpass_flop = st.step_kernel_flops(mb_local)        # + the fused dW2 product at H = 64
     rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
     # warm-L2 figure: back-to-back rowpass launches alone (W2/W2T stay in L2)
-    rp_launch = st.rowpass_dw2 if st.fused_dw2 else st.rowpass
+    rp_launch = st.rowpass_dw2 if st.fused_dw2 else (st.rowpass_kx if st.kx(mb_local) else st.rowpass)
     for _ in range(10):
         rp_launch(stage, None)
     e0.record()
@@ -731,7 +731,8 @@ def run(a, world):
         dp = {"world": n_gpus, "backend": dist.get_backend(pg), "dp_minibatch": tr.dp_minibatch,
               "allreduce": a.allreduce,
               "gradient_bucket_bytes": L.G.numel() * 4, "minibatch_step_us": t_chain,
-              "dw2_plan": {"solution": st.dw2_algo if st.lib_gemm else None,
+              "dw2_plan": {"kernel": "dw2_kx (split-bf16)" if st.kx(st.mb) else "library",
+                           "solution": getattr(st, "dw2_algo", None) if st.lib_gemm else None,
                            "source": getattr(st, "dw2_source", None) if st.lib_gemm else None}}
         if L.comm is not None:
             scratch = torch.zeros_like(L.G)
@@ -798,7 +799,8 @@ def run(a, world):
             dp["configs3_semantics_slice"] = {
                 "global_minibatch": a.minibatch, "rows_per_rank": mbg, "minibatches": a.global_slice,
                 "us_per_global_minibatch_step": us_g,
-                "dw2_plan": {"solution": stg.dw2_algo if stg.lib_gemm else None,
+                "dw2_plan": {"kernel": "dw2_kx (split-bf16)" if stg.kx(stg.mb) else "library",
+                           "solution": getattr(stg, "dw2_algo", None) if stg.lib_gemm else None,
                              "source": getattr(stg, "dw2_source", None) if stg.lib_gemm else None},
                 "note": ("global-minibatch mode (the reference's BatchSampler(..., 4096) semantics, "
                          "ppo_continuous.py:215) timed on a bounded slice after the run: wall time of "
@@ -843,6 +845,10 @@ def run(a, world):
             "episodes_finished_total": float(stats[0]),
             "roofline": {"kernel": (f"satrl_ppo_rowpass_dw2<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA "
                                     "16x16x4; the dW2 product fused in)" if st.fused_dw2 else
+                                    f"satrl_ppo_rowpass{'_kx' if st.kx(mb_local) else ''}<{a.hidden},{a.hidden // 16}> "
+                                    "(hand-written HIP; fc1 / [dW1|db1] on f32 MFMA 16x16x4, the two HxH products on "
+                                    "split-bf16 v_mfma_f32_16x16x32_bf16, FLOPs counted as f32)"
+                                    if a.hidden == 256 else
                                     f"satrl_ppo_rowpass<{a.hidden},{a.hidden // 16}> (hand-written HIP, f32 MFMA 16x16x4)"),
                          "bound": "mfma",
                          "achieved": rowpass_flop / (head_us * 1e-6) / 1e12, "peak": FP32_MFMA_PEAK_TFS,

@@ -186,8 +186,19 @@ int main(int argc, char** argv) {
   HIP_OK(hipStreamSynchronize(st));
   save(out, "ppo_H1.f32", host(d_H1, 2 * (size_t)mb * H));
   save(out, "ppo_dZ2.f32", host(d_dZ2, 2 * (size_t)mb * H));
+  // the product step at this shape: the rowpass with k-packed bf16 H1 / dZ2
+  // planes and the split-bf16 dW2 on them (the library GEMM above serves the
+  // short minibatches; kept here as the plan-pinning example)
   PPO_OK(satrl_ppo_dw2_lib(H, mb, -1, S, d_H1, d_dZ2, d_p2, d_ws, wsb, st));
-  PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, d_pw, d_pt, d_G, d_nsq, d_steps, st));
+  const int64_t kxe = satrl_ppo_kx_elems(H, mb);
+  uint16_t* d_H1x = dev<uint16_t>((size_t)kxe);
+  uint16_t* d_dZ2x = dev<uint16_t>((size_t)kxe);
+  const int Sx = satrl_ppo_dw2_kx_splits(H, mb, -1);
+  float* d_p2x = dev<float>(2 * (size_t)Sx * H * H);
+  PPO_OK(satrl_ppo_rowpass_kx(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1x, d_dZ2x, d_pt, d_pw,
+                              st));
+  PPO_OK(satrl_ppo_dw2_kx(H, mb, -1, Sx, d_H1x, d_dZ2x, d_p2x, st));
+  PPO_OK(satrl_ppo_reduce(H, mb, -1, Sx, 3, d_p2x, d_pw, d_pt, d_G, d_nsq, d_steps, st));
   PPO_OK(satrl_ppo_adam(H, mb, -1, d_nsq, d_steps, d_bct, (int)(bct.size() / 2), d_lr, 0.9f, 0.999f, 1e-5f, 0.5f, 1,
                         d_G, d_P, d_M, d_V, d_W2X, st));
   HIP_OK(hipStreamSynchronize(st));

@@ -152,6 +152,22 @@ int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_
                           const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
                           float* pw1, void* stream);
 
+/* H = 256, mb above the short-minibatch threshold (1024): the rowpass with
+ * H1 and dZ2 written as k-packed bf16 planes (each element split hi + mid +
+ * lo exactly; element (r, n) of a net's plane at ((r/8)*H + n)*8 + r%8,
+ * rows padded with zeros to whole 32-row chunks): u16 H1x / dZ2x
+ * [2][3][ceil(mb/32)*32][H], satrl_ppo_kx_elems(H, mb) elements each.
+ * satrl_ppo_dw2_kx multiplies them into the dW2 split-K slabs p2
+ * [2][S][H][H] on the split-bf16 MFMA (the fc2 products' arithmetic: error
+ * below an f32 MFMA chain's), S = satrl_ppo_dw2_kx_splits(H, mb, net); the
+ * minibatch step is then rowpass_kx, dw2_kx, reduce(S), adam.              */
+int64_t satrl_ppo_kx_elems(int H, int mb);
+int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
+                         float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, float* ptail,
+                         float* pw1, void* stream);
+int satrl_ppo_dw2_kx_splits(int H, int mb, int net);
+int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, float* p2, void* stream);
+
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result
  * is independent of N and of the sharding, and the rollout's log-probs equal
  * the update's first recomputation bit for bit.

@@ -523,6 +523,29 @@ __device__ __forceinline__ void put3x4(unsigned short* __restrict__ img, int64_t
   *reinterpret_cast<uint2*>(img + PS + e) = make_uint2(m0, m1);
   *reinterpret_cast<uint2*>(img + 2 * PS + e) = make_uint2(l0, l1);
 }
+
+// Row-parallel activations for the split-bf16 dW2 (satrl_ppo_rowpass_kx /
+// satrl_ppo_dw2_kx): a [rows][H] f32 tensor of one net as three bf16 planes
+// (plane stride PL elements), "k-packed": element (r, n) at ((r / 8) * H + n)
+// * 8 + r % 8, so the 8 consecutive rows an MFMA operand lane holds (the
+// reduction index of dW2 = dZ2^T H1 is the row) are one 16-B run, and the 16
+// columns of a lane group one 256-B run.  A rowpass lane holds rows 4lg..4lg+3
+// of a 16-row tile: one 8-B store per plane.
+template <int H, int R, int CT>
+__device__ __forceinline__ void store_kx(unsigned short* __restrict__ img, int64_t PL, int r0, int n0,
+                                         const float (&v)[R / 16][CT][4]) {
+  const int l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+#pragma unroll
+  for (int rt = 0; rt < R / 16; ++rt)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int r = r0 + 16 * rt + 4 * lg, n = n0 + 16 * t + li;
+      put3x4(img, ((int64_t)(r >> 3) * H + n) * 8 + (r & 7), PL,
+             make_float4(v[rt][t][0], v[rt][t][1], v[rt][t][2], v[rt][t][3]));
+    }
+}
+// rows of a k-packed tensor: the minibatch padded to whole 32-row chunks
+__host__ __device__ constexpr int64_t kx_rows(int mb) { return (mb + 31) / 32 * 32LL; }
 // the three planes of x at element e of an LDS plane image (plane stride PS)
 template <int PS>
 __device__ __forceinline__ void put3(unsigned short* img, int e, float x) {
@@ -759,7 +782,7 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
   return od;
 }
 
-template <int H, int NW, int R = kRows, bool FDW2 = false>
+template <int H, int NW, int R = kRows, bool FDW2 = false, bool KX = false>
 __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const void* __restrict__ W2X, float epsilon, float ent_coef,
@@ -769,6 +792,10 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
                                                       int S2, float* __restrict__ ratio_out) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
+  // KX: H1 / dZ2 go out as k-packed bf16 planes (store_kx; H1g / dZ2g point at
+  // u16 [2][3][kx_rows(mb)][H]) for satrl_ppo_dw2_kx, whole 32-row chunks
+  static_assert(!KX || (R == 32 && kBf3<H> && !FDW2), "k-packed outputs: 32-row blocks, split-bf16 width");
+  const int64_t PLX = kx_rows(mb) * H;                             // (KX) plane elements per net
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
   constexpr bool BF3 = kBf3<H>;
@@ -859,7 +886,9 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   const float* W2T = static_cast<const float*>(W2X);
   const unsigned short* W2p = static_cast<const unsigned short*>(W2X);
   mlp_forward<H, NW, R, true, BF3>(sm, P, BF3 ? W2p + w2x_plane(H, net, 0) : nullptr, net, mb - r0, gather,
-                                   FDW2 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+                                   FDW2 || KX ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
+  if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
   B3Pre<CT> preDs;
@@ -994,7 +1023,8 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   };
   if (net == 0) tail(std::true_type{});
   else tail(std::false_type{});
-  if constexpr (!FDW2) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
+  if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(dZ2g) + net * 3 * PLX, PLX, r0, n0, d2v);
+  else if constexpr (!FDW2) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   rp_barrier();
   PHASE_PROBE(5);
 
@@ -1325,6 +1355,93 @@ __global__ void __launch_bounds__(256) dw2_bf3_kernel(int mb, int S, int KR, int
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         out[(int64_t)(o0 + 32 * wo + 16 * x + 4 * lg + q) * H + n0 + 32 * wn + 16 * y + li] = acc[x][y][q];
+}
+
+// ---------------------------------------------------------------------------
+// dW2 at H = 256 from k-packed bf16 planes (satrl_ppo_dw2_kx): the rowpass
+// wrote H1 and dZ2 already split and laid out so that the reduction index
+// (rows) runs along each 16-B run (store_kx), so no transpose, no split and
+// no VGPR staging is left here.  Workgroup (net, 64x64 output tile, split s)
+// sums rows [s*KR, (s+1)*KR) into slab p2[net][s]; its 4 waves own 32x32
+// quarters (2 x 2 v_mfma_f32_16x16x32_bf16 tiles, six partial products
+// each, smallest first, as the rowpass).  Each 32-row chunk of the tile's
+// operands -- 2 tensors x 3 planes x 4 row groups x 64 columns x 16 B = 24 KB
+// -- streams global -> LDS by LDS-DMA (global_load_lds_dwordx4, one 1-KB run
+// per instruction, six per wave) through a kKxD-slot ring with counted vmcnt
+// and raw s_barrier; the MFMA operands are ds_read_b128 of consecutive 16-B
+// (row groups 16 B apart in bank space).  Every sum has a fixed order.
+// ---------------------------------------------------------------------------
+constexpr int kKxD = 3;                         // ring slots (chunks kKxD - 1 ahead)
+constexpr int kKxG = 1024 + 16;                 // bytes per (tensor, plane, row group) run in LDS
+__global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int net_sel,
+                                                     const unsigned short* __restrict__ H1x,
+                                                     const unsigned short* __restrict__ dZ2x, float* __restrict__ p2) {
+  constexpr int H = 256, TT = H / 64, RUNS = 2 * 3 * 4;         // runs per chunk: tensor x plane x row group
+  __shared__ __attribute__((aligned(16))) unsigned char ring[kKxD][RUNS][kKxG];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, li = l & 15, lg = l >> 4;
+  const int b = blockIdx.x, s = b % S, tile = (b / S) % (TT * TT);
+  const int net = net_sel < 0 ? b / (S * TT * TT) : net_sel;
+  const int o0 = (tile / TT) * 64, n0 = (tile % TT) * 64;
+  const int64_t PL = kx_rows(mb) * H;
+  const int c_begin = s * (KR / 32), nch = (int)((min((int64_t)(s + 1) * KR, kx_rows(mb)) - (int64_t)s * KR) / 32);
+  // run u = (tensor, plane, group) of chunk c: 64 columns x 8 rows, 1 KB contiguous in the plane
+  auto stage = [&](int c) {
+    const int slot = c % kKxD, cg = 4 * (c_begin + c);             // first row group of the chunk
+#pragma unroll
+    for (int k = 0; k < RUNS / 4; ++k) {
+      const int u = 4 * k + w, tz = u / 12, p = (u / 4) % 3, q = u % 4;   // wave w: runs w, w+4, ...
+      const unsigned short* src = (tz == 0 ? dZ2x : H1x) + (int64_t)net * 3 * PL + p * PL +
+                                  ((int64_t)(cg + q) * H + (tz == 0 ? o0 : n0) + l) * 8;
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)&ring[slot][u][0], 16, 0, 0);
+    }
+  };
+  const int wo = w >> 1, wn = w & 1;
+  f4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < kKxD - 1; ++c) stage(c < nch ? c : nch - 1);
+  for (int c = 0; c < nch; ++c) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kKxD - 2) * (RUNS / 4)) : "memory");   // this wave's runs of chunk c
+    __builtin_amdgcn_s_barrier();                                                   // every wave's; slot c-1 free
+    stage(c + kKxD - 1 < nch ? c + kKxD - 1 : nch - 1);                             // (tail: a harmless reload)
+    const int slot = c % kKxD;
+    s8v a[2][3], bq[2][3];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        // A[o][k] = dZ2[row 8lg + k'][o], B[k][n] = H1[row][n]: group lg of plane p
+        a[x][p] = *reinterpret_cast<const s8v*>(&ring[slot][0 * 12 + p * 4 + lg][(32 * wo + 16 * x + li) * 16]);
+        bq[x][p] = *reinterpret_cast<const s8v*>(&ring[slot][1 * 12 + p * 4 + lg][(32 * wn + 16 * x + li) * 16]);
+      }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = mfma6(a[x], bq[y], acc[x][y]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // acc[x][y][q] = dW2[o0 + 32wo + 16x + 4lg + q][n0 + 32wn + 16y + li]
+  float* out = p2 + ((int64_t)net * S + s) * H * H;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        out[(int64_t)(o0 + 32 * wo + 16 * x + 4 * lg + q) * H + n0 + 32 * wn + 16 * y + li] = acc[x][y][q];
+}
+// split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split
+constexpr int kKxWgs = 256;
+int kx_splits(int mb, int net, int target = kKxWgs) {
+  const int tiles = (net < 0 ? 2 : 1) * 16, nch = (int)(kx_rows(mb) / 32);
+  int S = target / tiles;
+  if (S > nch) S = nch;
+  if (S < 1) S = 1;
+  const int cps = (nch + S - 1) / S;                               // chunks per split
+  return (nch + cps - 1) / cps;
 }
 
 constexpr int kDw3Wgs = 512;      // dw2_bf3_kernel workgroups to aim for (splits = this / tiles; 256 / 1024 slower)
@@ -1904,7 +2021,8 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
 // instead of H1 / dZ2; ratio (nullable) receives the actor's per-row ratio
 static int launch_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
                           const void* W2X, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
-                          float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream) {
+                          float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream,
+                          bool kx = false) {
   const int R = rows_per_wg(H, mb), nrb = n_head_wg(H, mb);
   dim3 g((net < 0 ? 2 : 1) * nrb);   // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
@@ -1918,6 +2036,8 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
     hipLaunchKernelGGL((rowpass_kernel<128, 8, kRows, true>), g, dim3(512), 0, s, RP_ARGS);
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, RP_ARGS);
+  else if (kx)
+    hipLaunchKernelGGL((rowpass_kernel<256, kNW256, kRows, false, true>), g, dim3(kNW256 * 64), 0, s, RP_ARGS);
   else if (R == kRowsShort)
     hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, RP_ARGS);
   else
@@ -1958,6 +2078,37 @@ int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_
     return -1;
   return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
                         nullptr, true, stream);
+}
+
+int64_t satrl_ppo_kx_elems(int H, int mb) {
+  if (H != 256 || mb <= 0) return -1;
+  return 2LL * 3 * kx_rows(mb) * H;
+}
+
+int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
+                         float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, float* ptail,
+                         float* pw1, void* stream) {
+  if (H != 256 || mb <= short_mb() || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !H1x || !dZ2x ||
+      !ptail || !pw1)
+    return -1;
+  return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, static_cast<float*>(H1x),
+                        static_cast<float*>(dZ2x), ptail, pw1, nullptr, nullptr, false, stream, true);
+}
+
+int satrl_ppo_dw2_kx_splits(int H, int mb, int net) {
+  if (H != 256 || mb <= 0 || net < -1 || net > 1) return -1;
+  return kx_splits(mb, net);
+}
+
+int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, float* p2, void* stream) {
+  if (H != 256 || mb <= 0 || net < -1 || net > 1 || S < 1 || !H1x || !dZ2x || !p2) return -1;
+  const int nch = (int)(kx_rows(mb) / 32), cps = (nch + S - 1) / S;
+  if ((int64_t)cps * (S - 1) >= nch) return -1;                  // an empty split: use satrl_ppo_dw2_kx_splits
+  const dim3 g((unsigned)((net < 0 ? 2 : 1) * 16 * S));
+  hipLaunchKernelGGL(dw2_kx_kernel, g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net,
+                     static_cast<const unsigned short*>(H1x), static_cast<const unsigned short*>(dZ2x), p2);
+  LAUNCH_CHECK();
+  return 0;
 }
 
 int satrl_ppo_dw2_splits(int H, int mb) {

@@ -122,6 +122,11 @@ _SIGS = {
                                  _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_row_blocks": ([C.c_int, C.c_int], C.c_int),
     "satrl_ppo_w2x_floats": ([C.c_int], _i64),
+    "satrl_ppo_kx_elems": ([C.c_int, C.c_int], _i64),
+    "satrl_ppo_rowpass_kx": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
+                              _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_dw2_kx_splits": ([C.c_int, C.c_int, C.c_int], C.c_int),
+    "satrl_ppo_dw2_kx": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_w2x_sync": ([C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                                _vp, _vp, _vp], C.c_int),

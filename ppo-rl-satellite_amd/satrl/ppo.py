@@ -177,6 +177,13 @@ def ppo_layout(H):
     return dict(zip(OFF_NAMES, [int(v) for v in off]))
 
 
+def _short_mb():
+    """Minibatch rows up to which H = 256 runs the 16-row rowpass (the
+    library's SATRL_RP_SHORT_MB threshold, default 1024)."""
+    v = os.environ.get("SATRL_RP_SHORT_MB")
+    return int(v) if v is not None else 1024
+
+
 def w2x_floats(H):
     """f32 elements of the fc2 operand image (satrl_ppo_w2x_floats)."""
     n = int(_lib.lib().satrl_ppo_w2x_floats(int(H)))
@@ -282,7 +289,7 @@ class FusedMinibatch:
     all-reduce.  Groups of ``group`` minibatches are captured into a hipGraph
     and replayed over [group, mb] blocks of a device permutation."""
 
-    def __init__(self, learner, mb, group, use_graph=True, split_chains=False):
+    def __init__(self, learner, mb, group, use_graph=True, split_chains=False, kx=None):
         self.L = learner
         self.mb = int(mb)
         self.group = int(group)
@@ -300,6 +307,14 @@ class FusedMinibatch:
         # out of LDS itself (satrl_ppo_rowpass_dw2), bitwise the dw2_kernel's
         # one-chunk splits, so a minibatch step is three launches instead of four
         self.fused_dw2 = learner.H == 64 and not self.lib_gemm
+        # H = 256, mb above the short threshold: the rowpass writes H1 / dZ2 as
+        # k-packed bf16 planes and dW2 runs on the split-bf16 MFMA from them
+        # (satrl_ppo_rowpass_kx / satrl_ppo_dw2_kx); shorter minibatches (the
+        # 16-row rowpass) keep the library GEMM
+        if kx is None:
+            kx = os.environ.get("SATRL_DW2_KX", "1") != "0"              # dev A/B knob
+        self.kx_on = bool(kx) and learner.H == 256 and not split_chains
+        self.kx_elems = 0
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
         self.split = bool(split_chains) and learner.pg is None
@@ -312,6 +327,10 @@ class FusedMinibatch:
         f32 = dict(dtype=torch.float32, device=dev)
         self.H1 = torch.empty(2 * self.mb * H, **f32)
         self.dZ2 = torch.empty(2 * self.mb * H, **f32)
+        if self.kx(self.mb):
+            self.kx_elems = int(_lib.lib().satrl_ppo_kx_elems(H, self.mb))
+            self.H1x = torch.empty(self.kx_elems, dtype=torch.int16, device=dev)
+            self.dZ2x = torch.empty(self.kx_elems, dtype=torch.int16, device=dev)
         self.ptail = torch.empty(self.nwg * (6 * H + 12), **f32)
         self.pw1 = torch.empty(self.nwg * 2 * H * 20, **f32)
         # sized for the largest split count any minibatch size can produce
@@ -324,7 +343,7 @@ class FusedMinibatch:
         self.ws = {}
         self._ws_retired = []
         self._ws_for = {}                  # (mb, S, net) -> the workspace its plan was checked against
-        if self.lib_gemm and torch.cuda.is_available():
+        if self.lib_gemm and torch.cuda.is_available() and not self.kx(self.mb):
             for net in ((0, 1) if self.split else (-1,)):
                 self._ws_for[(self.mb, self.S, net)] = (self._dw2_plan(self.mb, self.S, net),)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
@@ -355,6 +374,26 @@ class FusedMinibatch:
                                            ptr(H1), ptr(dZ2), ptr(self.ptail), ptr(self.pw1), stream_ptr()),
                   "satrl_ppo_rowpass")
         return H1, dZ2
+
+    def kx(self, mb):
+        """True when a minibatch of mb rows takes the k-packed split-bf16 dW2
+        path (H = 256, 32-row rowpass blocks)."""
+        return self.kx_on and int(mb) > _short_mb()
+
+    def rowpass_kx(self, src, idx, mb=None, net=-1):
+        """satrl_ppo_rowpass_kx: the rowpass with H1 / dZ2 written as k-packed
+        bf16 planes into self.H1x / self.dZ2x (the dW2 operands)."""
+        L = self.L
+        mb = self.mb if mb is None else int(mb)
+        check(_lib.lib().satrl_ppo_rowpass_kx(L.H, mb, int(net), ptr(src), None if idx is None else ptr(idx),
+                                              ptr(L.P), ptr(L.W2T), float(L.epsilon), float(L.entropy_coef),
+                                              float(L.max_action), ptr(self.H1x), ptr(self.dZ2x), ptr(self.ptail),
+                                              ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass_kx")
+
+    def dw2_kx(self, mb, S, net=-1):
+        """satrl_ppo_dw2_kx: the dW2 split-K slabs from the k-packed planes."""
+        check(_lib.lib().satrl_ppo_dw2_kx(self.L.H, int(mb), int(net), int(S), ptr(self.H1x), ptr(self.dZ2x),
+                                          ptr(self.p2), stream_ptr()), "satrl_ppo_dw2_kx")
 
     def rowpass_dw2(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass_dw2 (H = 64): the rowpass with each block's dW2
@@ -400,7 +439,7 @@ class FusedMinibatch:
     def max_splits(self, H):
         """Upper bound of splits(H, mb) over every mb (the p2 capacity)."""
         if self.lib_gemm:
-            return max(self.S, 4)
+            return max(self.S, 4, 8 if self.kx_on else 0)        # (dw2_kx: <= 256 / 32 tiles splits)
         if self.fused_dw2:
             return self.nwg                  # row blocks of the longest minibatch at or below mb
         return max(self.S, 256 // (2 * (H // 64) ** 2))
@@ -411,6 +450,11 @@ class FusedMinibatch:
             S = _lib.lib().satrl_ppo_row_blocks(int(H), int(mb))      # one slab per rowpass row block
             if S < 1:
                 raise _lib.NativeError(f"satrl_ppo_row_blocks({H}, {mb}) failed")
+            return S
+        if self.kx(mb):
+            S = _lib.lib().satrl_ppo_dw2_kx_splits(int(H), int(mb), -1)
+            if S < 1:
+                raise _lib.NativeError(f"satrl_ppo_dw2_kx_splits({H}, {mb}) failed")
             return S
         if self.lib_gemm:
             S = int(os.environ.get("SATRL_DW2_SPLITS", "4"))          # dev A/B knob; 4 measured best
@@ -448,7 +492,7 @@ class FusedMinibatch:
         ragged tail) before the update loop, so no plan is tuned between
         minibatch steps and none inside a capture."""
         mb = int(mb)
-        if not self.lib_gemm or not torch.cuda.is_available():
+        if not self.lib_gemm or not torch.cuda.is_available() or self.kx(mb):
             return
         S = self.S if mb == self.mb else self.splits(self.L.H, mb)
         for net in ((0, 1) if self.split else (-1,)):
@@ -489,9 +533,13 @@ class FusedMinibatch:
         nsq = self.nsq[max(net, 0)]
         if events is not None:
             events[0].record()
+        kx = self.kx(mb)
         if skip_rowpass:
             n = 2 * mb * H
             H1, dZ2 = self.H1[:n], self.dZ2[:n]
+        elif kx:
+            self.rowpass_kx(src, idx, mb, net)
+            H1 = dZ2 = None
         elif self.fused_dw2:
             self.rowpass_dw2(src, idx, mb, net)
             H1 = dZ2 = None
@@ -500,12 +548,16 @@ class FusedMinibatch:
         if events is not None:
             events[1].record()
         if L.pg is None:
-            if not self.fused_dw2:
+            if kx:
+                self.dw2_kx(mb, S, net)
+            elif not self.fused_dw2:
                 self._dw2(H1, dZ2, mb, S, net)
             check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
-            if not self.fused_dw2:
+            if kx:
+                self.dw2_kx(mb, S, net)
+            elif not self.fused_dw2:
                 self._dw2(H1, dZ2, mb, S, net)
             check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
                                        None, None, sp), "satrl_ppo_reduce")

@@ -86,21 +86,10 @@ def test_c_host_matches_the_python_path(tmp_path):
     assert np.array_equal(dZ2.cpu().numpy(), _load(d, "ppo_dZ2.f32", np.float32, (2 * mb * H,)))
     st.step(src, None)
     torch.cuda.synchronize()
-    if st.dw2_source == "table":                 # the Python host pinned the table's solution
-        assert st.dw2_algo == plan["index"]
     out = {k: getattr(L, k).cpu().numpy() for k in ("G", "P", "M", "V", "W2T")}
     ref = {k: _load(d, f"ppo_{k}.f32", np.float32, out[k].shape) for k in out}
     assert np.array_equal(L.steps.cpu().numpy(), _load(d, "ppo_steps.f64", np.float64, (2,)))
-    if pinned:                                   # the same dW2 tile on both hosts
-        for k in out:
-            assert np.array_equal(out[k], ref[k]), k
-        return
-    # another hipBLASLt build: dW2 summed by another tile; every other gradient
-    # element is the same kernels' fixed-order sum, the dW2 part agrees to f32
-    # rounding, and Adam's first step (+-lr for every nonzero gradient) agrees
-    # except where a gradient is ~0 and its sign flips
-    w2 = 2 * H * H
-    assert np.array_equal(out["G"][w2:], ref["G"][w2:])
-    assert np.allclose(out["G"][:w2], ref["G"][:w2], rtol=1e-4, atol=1e-9)
-    dp = np.abs(out["P"] - ref["P"])
-    assert dp.max() <= 2.1 * 2e-4 and (dp > 1e-8).mean() < 1e-3
+    assert st.kx(mb)                             # both hosts: the k-packed split-bf16 dW2, no library tiles
+    for k in out:
+        assert np.array_equal(out[k], ref[k]), k
+    print("library dW2 plan pinned from the table:" if pinned else "library dW2 plan tuned:", plan["index"])

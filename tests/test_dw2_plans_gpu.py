@@ -30,7 +30,7 @@ def _dw2_once(mb, q, plans=None):
     args = args_param(hidden_width=H, mini_batch_size=mb, batch_size=8192, chkpt_dir="/tmp")
     args.state_dim, args.action_dim, args.max_action = 18, 3, 1.6
     L = PPOLearner(args, "pursuer", device="cuda:0", use_graph=False)
-    st = FusedMinibatch(L, mb, 1, use_graph=False)
+    st = FusedMinibatch(L, mb, 1, use_graph=False, kx=False)     # the library GEMM path itself
     g = torch.Generator(device="cuda:0").manual_seed(9)
     n = 2 * mb * H
     H1 = torch.rand(n, device="cuda:0", generator=g) * 2 - 1
@@ -108,7 +108,7 @@ def _split_update(split):
                       chkpt_dir="/tmp")
     args.state_dim, args.action_dim, args.max_action = 18, 3, 1.6
     L = PPOLearner(args, "pursuer", device="cuda:0", graph_group=4, use_graph=True)
-    L._steppers[mb] = FusedMinibatch(L, mb, 4, use_graph=True, split_chains=split)
+    L._steppers[mb] = FusedMinibatch(L, mb, 4, use_graph=True, split_chains=split, kx=False)
     g = torch.Generator(device="cuda:0").manual_seed(2)
     src = torch.zeros((B, 32), device="cuda:0")
     src[:, 0:18] = torch.randn((B, 18), device="cuda:0", generator=g)

@@ -669,3 +669,56 @@ def test_rollout_logp_equals_update_recomputation(H, mb):
         assert bad.numel() == 0, (bad[:8].tolist(), ratio[bad[:8]].tolist())
 
 
+
+
+@pytest.mark.parametrize("mb,contig", [(4096, True), (1500, False)])
+def test_kx_rowpass_planes_and_dw2(mb, contig):
+    """H 256: satrl_ppo_rowpass_kx writes H1 / dZ2 as k-packed bf16 planes
+    whose sum hi + mid + lo is bitwise the f32 rowpass's H1 / dZ2 (rows past
+    the minibatch zero), with the same [dW1|db1] / tail slabs; satrl_ppo_dw2_kx
+    sums dZ2^T H1 from them on the split-bf16 MFMA within the f32 bound of an
+    f64 reference (ppo_continuous.py:227-233: fc2.weight.grad).  1500: a ragged
+    last chunk on the index-gather path."""
+    import satrl._lib as _L
+    from satrl.ppo import PPOLearner
+    torch.manual_seed(5)
+    H, B = 256, 8192
+    args = _args(hidden_width=H, mini_batch_size=mb, batch_size=B)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    with torch.no_grad():
+        for p in list(L.actor.parameters()) + list(L.critic.parameters()):
+            p.add_(torch.randn_like(p) * 0.05)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    src = torch.randn((B, 32), device="cuda", generator=g)
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+    idx = None if contig else torch.randperm(B, device="cuda", generator=g)[:mb]
+    st = L.stepper(mb)
+    assert st.kx(mb)
+    H1, dZ2 = st.rowpass(src, idx)
+    torch.cuda.synchronize()
+    H1, dZ2 = H1.clone().view(2, mb, H), dZ2.clone().view(2, mb, H)
+    tail, w1 = st.ptail.clone(), st.pw1.clone()
+    st.H1x.fill_(-1)
+    st.dZ2x.fill_(-1)
+    st.rowpass_kx(src, idx)
+    torch.cuda.synchronize()
+    assert torch.equal(st.ptail, tail) and torch.equal(st.pw1, w1)
+    rows = (mb + 31) // 32 * 32
+
+    def decode(x):
+        p = x.view(2, 3, rows // 8, H, 8).view(torch.bfloat16).float()
+        v = (p[:, 0] + p[:, 1]) + p[:, 2]                           # [2][rows/8][H][8]
+        return v.permute(0, 1, 3, 2).reshape(2, rows, H)
+    h1x, dz2x = decode(st.H1x), decode(st.dZ2x)
+    assert torch.equal(h1x[:, :mb], H1) and torch.equal(dz2x[:, :mb], dZ2)
+    assert not h1x[:, mb:].any() and not dz2x[:, mb:].any()
+    S = st.S
+    st.p2.fill_(float("nan"))
+    st.dw2_kx(mb, S)
+    torch.cuda.synchronize()
+    got = st.p2[:2 * S * H * H].view(2, S, H, H).double().sum(1)
+    ref = torch.einsum("brn,brm->bnm", dZ2.double(), H1.double())
+    mag = torch.einsum("brn,brm->bnm", dZ2.double().abs(), H1.double().abs())
+    err = ((got - ref).abs() / mag.clamp_min(1e-30)).max().item()
+    assert err < 2e-6, err                 # per-slab split-bf16 sums (<= 2.2e-7 each) + f32 slab rounding
