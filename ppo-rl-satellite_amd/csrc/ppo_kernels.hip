@@ -458,9 +458,14 @@ __device__ __forceinline__ void mfma_rows3(const unsigned short* __restrict__ A,
 __host__ __device__ constexpr int64_t w2x_plane(int H, int net, int which) { return (int64_t)(net * 2 + which) * 3 * H * H; }
 // elements of the W2X buffer, in floats
 __host__ __device__ constexpr int64_t w2x_floats(int H) { return H == 256 ? 6LL * H * H : 2LL * H * H; }
+// early-issued pre-split B chunks: one (two measured no faster, and their
+// registers live through phase C push the rowpass past 104 VGPRs: then a
+// 16-wave workgroup no longer fits beside two waves of another kernel per
+// SIMD -- the peer all-reduce of a second rank on the same device)
+constexpr int kPre3 = 1;
 template <int CT>
-struct B3Pre {                    // early-issued pre-split B chunks (kBPD of them)
-  s8v bb[kBPD][CT][3];
+struct B3Pre {
+  s8v bb[kPre3][CT][3];
 };
 // one 32-wide k chunk of pre-split B: the three planes (plane stride PSB) of
 // the lane's 8 k, as the f32 path's b_chunk holds them before its split
@@ -477,7 +482,7 @@ __device__ __forceinline__ void mfma_rows3s_pre(const unsigned short* __restrict
   const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
   const unsigned short* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
 #pragma unroll
-  for (int c = 0; c < kBPD; ++c) b3_chunk<CT, LDB, LDB * LDB>(bp + 32 * c, pre.bb[c]);
+  for (int c = 0; c < kPre3; ++c) b3_chunk<CT, LDB, LDB * LDB>(bp + 32 * c, pre.bb[c]);
 }
 // mfma_rows3 on B planes split beforehand: B = three bf16 planes [K rows of
 // LDB] (plane stride K * LDB), kBPD3 chunks ahead, the first kBPD optionally
@@ -487,7 +492,7 @@ __device__ __forceinline__ void mfma_rows3s(const unsigned short* __restrict__ A
                                             int n0, f4 (&acc)[RT][CT], const B3Pre<CT>* pre = nullptr) {
   constexpr int NC = K / 32, PSB = K * LDB;
   constexpr int BPD = kBPD3 < NC ? kBPD3 : NC, NB = BPD + 1;
-  static_assert(!PRE || BPD >= kBPD, "early-issued chunks fit the ring");
+  static_assert(!PRE || BPD >= kPre3, "early-issued chunks fit the ring");
   const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
   const unsigned short* ap = A + i * LDP + 8 * g;
   const unsigned short* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
@@ -495,13 +500,13 @@ __device__ __forceinline__ void mfma_rows3s(const unsigned short* __restrict__ A
   s8v aa[RT][3];
   if constexpr (PRE) {
 #pragma unroll
-    for (int c = 0; c < kBPD; ++c)
+    for (int c = 0; c < kPre3; ++c)
 #pragma unroll
       for (int t = 0; t < CT; ++t)
 #pragma unroll
         for (int p = 0; p < 3; ++p) bb[c][t][p] = pre->bb[c][t][p];
 #pragma unroll
-    for (int c = kBPD; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);
+    for (int c = kPre3; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);
   } else {
 #pragma unroll
     for (int c = 0; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);

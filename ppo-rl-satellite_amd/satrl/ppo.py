@@ -359,6 +359,14 @@ class FusedMinibatch:
         # or host round trip between groups
         self.perm_buf = None
         self.grp = torch.zeros(1, dtype=torch.int64, device=dev)
+        if learner.pg is not None and _dist.world_size(learner.pg) > 1 and torch.cuda.is_available():
+            # every rank's first step of this shape starts together: the peer
+            # all-reduce waits a bounded 0.5 s for its peers, so a rank still
+            # setting up must not hold the others past that (the library dW2
+            # plan's broadcast used to be this sync point)
+            import torch.distributed as dist
+            torch.cuda.synchronize()
+            dist.barrier(group=learner.pg)
 
     def rowpass(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass alone (a pure function of src, idx and the
