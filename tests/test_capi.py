@@ -95,6 +95,18 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_policy_act(256, 8, fake, fake, fake, 1.6, 0, 0, 0, None, fake, fake, None, None,
                                 None) == -1                                   # second agent without outputs
     assert lib.satrl_ppo_tanh(0, fake, fake, None) == -1
+    # the fc2 operand image and the k-packed dW2 path (H = 256, mb above the 16-row threshold)
+    assert lib.satrl_ppo_w2x_floats(256) == 6 * 256 * 256 and lib.satrl_ppo_w2x_floats(64) == 2 * 64 * 64
+    assert lib.satrl_ppo_w2x_floats(100) == -1
+    assert lib.satrl_ppo_w2x_sync(100, -1, fake, fake, None) == -1 and lib.satrl_ppo_w2x_sync(256, -1, None, fake, None) == -1
+    assert lib.satrl_ppo_kx_elems(256, 4096) == 2 * 3 * 4096 * 256 and lib.satrl_ppo_kx_elems(256, 1500) == 6 * 1504 * 256
+    assert lib.satrl_ppo_kx_elems(64, 4096) == -1
+    assert lib.satrl_ppo_rowpass_kx(256, 1024, -1, *args) == -1                 # the 16-row kernel's minibatch
+    assert lib.satrl_ppo_rowpass_kx(64, 4096, -1, *args) == -1                  # H 256 only
+    assert lib.satrl_ppo_dw2_kx_splits(256, 4096, -1) == 8 and lib.satrl_ppo_dw2_kx_splits(256, 4096, 0) == 16
+    assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, fake, None) == -1     # S < 1
+    assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, fake, None) == -1       # an empty split (2 chunks)
+    assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, fake, None) == -1     # null H1x
 
 
 def test_product_has_no_cpu_fallback():
@@ -145,3 +157,24 @@ def test_improvednn_matches_reference_state_dict():
     net.load_state_dict(sd)
     out = net(torch.zeros(1, 5))
     assert out.shape == (1, 10) and torch.isfinite(out).all()
+
+
+def test_w2x_image_host_statement():
+    """The fc2 operand image's host statement (satrl.ppo.w2x_image, what
+    satrl_ppo_w2x_sync writes): at H = 256 every plane is a round-to-nearest
+    bf16 and hi + mid + lo is the f32 weight exactly, for fc2.weight and its
+    transpose; w2x_decode recovers fc2.weight^T bit for bit (H 64: the f32
+    transpose itself)."""
+    import torch
+    from satrl.ppo import w2x_decode, w2x_image
+    g = torch.Generator().manual_seed(0)
+    for H in (64, 256):
+        W2 = torch.randn(2 * H * H, generator=g) * torch.exp(torch.randn(2 * H * H, generator=g) * 4)
+        img = w2x_image(W2, H)
+        assert img.dtype == torch.float32 and img.numel() == (6 if H == 256 else 2) * H * H
+        assert torch.equal(w2x_decode(img, H), W2.view(2, H, H).transpose(1, 2))
+        if H == 256:
+            p = img.view(torch.int16).view(2, 2, 3, H, H).view(torch.bfloat16).float()
+            assert torch.equal((p[:, 0, 0] + p[:, 0, 1]) + p[:, 0, 2], W2.view(2, H, H))
+            assert torch.equal(p[:, 0, 0], W2.view(2, H, H).to(torch.bfloat16).float())      # hi: RNE of w
+            assert torch.equal(p[:, 1], p[:, 0].transpose(2, 3))                            # W2^T planes
