@@ -890,10 +890,13 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   // the fc2 operand image: pre-split bf16 planes at H = 256, else f32 W2^T
   const float* W2T = static_cast<const float*>(W2X);
   const unsigned short* W2p = static_cast<const unsigned short*>(W2X);
+  // (H = 256: the H1 store after phase B, not between fc1 and B: 8 fewer VGPRs
+  // live through B, so the 32-row kernel stays at <= 104)
   mlp_forward<H, NW, R, true, BF3>(sm, P, BF3 ? W2p + w2x_plane(H, net, 0) : nullptr, net, mb - r0, gather,
-                                   FDW2 || KX ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+                                   FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
+  else if constexpr (BF3 && !FDW2) store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, h1);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
   B3Pre<CT> preDs;
