@@ -1754,6 +1754,14 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   const float4 g = G4[el];
   float4 m = M4[el], v = V4[el];
   const float4 p = P4[el];
+  // both nets' step counts, learning rates and bias-correction rows, issued
+  // here too: after the fold (a barrier the compiler does not hoist loads
+  // over) they were two dependent load round trips on the kernel's path
+  const double st_a = steps[0], st_c = steps[1];
+  const float lr_a = lr[0], lr_c = lr[1];
+  const int ka = (int)st_a, kc = (int)st_c;
+  const double2* bct2 = reinterpret_cast<const double2*>(bct);
+  const double2 bca = bct2[ka < bct_len ? ka : bct_len - 1], bcc = bct2[kc < bct_len ? kc : bct_len - 1];
   double a = 0.0, c = 0.0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {                                    // k = t, t+256, ... in order, as the loop
@@ -1776,10 +1784,11 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
     coef = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
     // bct[2*step] = 1 - beta1**step, bct[2*step+1] = sqrt(1 - beta2**step) (python float
     // math, as torch.optim.Adam computes them); constant 1.0 past the table
-    const int st = (int)steps[net];
-    const double bc1 = st < bct_len ? bct[2 * st] : 1.0;
-    const double bc2s = st < bct_len ? bct[2 * st + 1] : 1.0;
-    ss = (float)((double)lr[net] / bc1);
+    const int st = net == 0 ? ka : kc;
+    const double2 bc = net == 0 ? bca : bcc;
+    const double bc1 = st < bct_len ? bc.x : 1.0;
+    const double bc2s = st < bct_len ? bc.y : 1.0;
+    ss = (float)((double)(net == 0 ? lr_a : lr_c) / bc1);
     b2s = (float)bc2s;
   }
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
