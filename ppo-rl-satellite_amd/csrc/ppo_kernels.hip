@@ -1648,6 +1648,10 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
   double sa = 0.0, sc = 0.0;
   const int t = threadIdx.x;
   float4* G4 = reinterpret_cast<float4*>(G);
+  // the step counters, read before the slab loads (read at the end they were
+  // one more load round trip on block 0's path), advanced at the end
+  double st0 = 0.0, st1 = 0.0;
+  if ((mode & 2) && blockIdx.x == 0 && t == 0) { st0 = steps[0]; st1 = steps[1]; }
   RedOut o;
   reduce_block(H, L, g, blockIdx.x, mode, p2, p1, pt, G4, world, red, sa, sc, o);
   if (mode & 2) {
@@ -1656,8 +1660,8 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
       nsq[2 * blockIdx.x] = sa;
       nsq[2 * blockIdx.x + 1] = sc;
       if (blockIdx.x == 0) {
-        if (g.net != 1) steps[0] += 1.0;
-        if (g.net != 0) steps[1] += 1.0;
+        if (g.net != 1) steps[0] = st0 + 1.0;
+        if (g.net != 0) steps[1] = st1 + 1.0;
       }
     }
   }
@@ -1949,6 +1953,8 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
   }
   __syncthreads();
   const unsigned tag = tag_s;
+  double st0 = 0.0, st1 = 0.0;                                     // (advanced at the end, as reduce_kernel)
+  if (b == 0 && t == 0) { st0 = steps[0]; st1 = steps[1]; }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   bool ok = true;
   // this thread's float4 of G, as reduce_kernel hands them out (lead threads)
@@ -2004,7 +2010,7 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
   if (t == 0) {
     nsq[2 * b] = sa;
     nsq[2 * b + 1] = sc;
-    if (b == 0) { steps[0] += 1.0; steps[1] += 1.0; }
+    if (b == 0) { steps[0] = st0 + 1.0; steps[1] = st1 + 1.0; }
   }
 }
 
