@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Workload for the PMC passes of tools/profile_round.sh: satrl_ppo_rowpass
-launched back to back at the bench configuration (hidden 256, minibatch
+"""Workload for the PMC passes of tools/profile_round.sh: satrl_ppo_rowpass_kx
+(the product's rowpass at H 256, mb 4096) launched back to back at the bench configuration (hidden 256, minibatch
 4096 rows drawn by a random permutation from a packed buffer of
 16384 x 2048 transitions and staged contiguously first, as the update's
 graphs do with satrl_ppo_stage; the staging copy is not a rowpass launch).
@@ -30,7 +30,7 @@ def main():
     st = L.stepper(mb)
     for k in range(iters):
         rows_k = src.index_select(0, perm[k * mb:(k + 1) * mb])
-        st.rowpass(rows_k, None)
+        (st.rowpass_kx if st.kx(mb) else st.rowpass)(rows_k, None)       # the product's launch at this shape
     torch.cuda.synchronize()
     print("ok")
 

@@ -50,7 +50,7 @@ def main():
     if os.path.exists(fetch) and os.path.exists(write):
         f_kb, nf = pmc_per_dispatch(fetch, "rowpass_kernel", "FETCH_SIZE")
         w_kb, nw = pmc_per_dispatch(write, "rowpass_kernel", "WRITE_SIZE")
-        res = {"kernel": "rowpass_kernel<256, 16>", "hidden": 256, "minibatch": 4096,
+        res = {"kernel": "rowpass_kernel<256, 16, 32, kx>", "hidden": 256, "minibatch": 4096,
                "dispatches": [nf, nw], "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
                "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
                "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
@@ -67,22 +67,29 @@ def main():
         grbm, ng = pmc_per_dispatch(mfma, "rowpass_kernel", "GRBM_GUI_ACTIVE")
         sqb, ns = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_BUSY_CYCLES")
         n_simd = 256 * 4
-        # v_mfma_f32_16x16x4f32 per launch: per row and net fc2 fwd + dH1 (2 x 2 H^2 FLOP) and
-        # fc1 fwd + [dW1|db1] (2 x 2 H 32 FLOP, K padded to 32): 288 per wave, 1 179 648 per launch
-        n_mfma = 2 * 4096 * (2 * 2 * 256 * 256 + 2 * 2 * 256 * 32) / (16 * 16 * 4 * 2)
-        res = {"kernel": "rowpass_kernel<256, 16>", "hidden": 256, "minibatch": 4096, "dispatches": [nb, ng, ns],
+        # per launch (256 workgroups x 16 waves): fc1 fwd + [dW1|db1] on v_mfma_f32_16x16x4f32
+        # (K padded to 32: 32 per wave, 131 072, 32 busy cycles each); fc2 fwd + dH1 as
+        # split-bf16 v_mfma_f32_16x16x32_bf16 (8 chunks x 2 row tiles x 6 products x 2
+        # phases = 192 per wave, 786 432, 16 busy cycles each)
+        n_f32, n_bf16 = 256 * 16 * 32, 256 * 16 * 192
+        n_mfma = n_f32 + n_bf16
+        busy_expected = 32 * n_f32 + 16 * n_bf16
+        res = {"kernel": "rowpass_kernel<256, 16, 32, kx>", "hidden": 256, "minibatch": 4096, "dispatches": [nb, ng, ns],
                "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
                "SQ_BUSY_CYCLES_median": sqb,
                "xcd_cycles": grbm / 8.0 if grbm else None,
                "mfma_busy_frac": busy / (grbm / 8.0 * n_simd) if busy and grbm else None,
                "mfma_instructions_per_launch": n_mfma,
-               "busy_cycles_per_mfma": busy / n_mfma if busy else None,
+               "mfma_f32_16x16x4_per_launch": n_f32, "mfma_bf16_16x16x32_per_launch": n_bf16,
+               "busy_cycles_expected": busy_expected,
+               "busy_over_expected": busy / busy_expected if busy else None,
                "definition": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the "
                              "fraction of SIMD-cycles of the dispatch window in which the matrix core was busy, at "
                              "the clock the chip ran (roofline.frac prices against the 2.4 GHz peak instead). The "
                              "window of a ~30 us dispatch under --pmc includes the profiler's per-dispatch set-up "
                              "(MI355X_MICROARCH.md: GRBM quotients read high below ~0.3 ms), so this is a lower "
-                             "bound; busy_cycles_per_mfma = 32 shows the counter equals 32 x the kernel's MFMA count",
+                             "bound; busy_over_expected = 1 shows the counter equals the MFMAs' busy cycles (32 per f32 16x16x4, 16 per "
+                             "bf16 16x16x32)",
                "workload": "tools/rowpass_workload.py"}
         with open(os.path.join(prof, f"{tag}_rowpass_mfma_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
@@ -93,13 +100,17 @@ def main():
     if os.path.exists(sf) and os.path.exists(sw) and os.path.exists(sm):
         # the post-rowpass chain per launch: HBM bytes (FETCH x2 + WRITE) against
         # the algorithmic bytes, and matrix-core busy cycles (dW2 only has MFMA work)
-        H, mb, S, nwg = 256, 4096, 4, 128
+        # the product's dW2 at this shape: dw2_kx_kernel (k-packed bf16 planes, 8 splits;
+        # round 4) or the hipBLASLt GEMM ("Cijk", 4 splits; SATRL_DW2_KX=0)
+        kx = pmc_per_dispatch(sf, "dw2_kx_kernel", "FETCH_SIZE")[0] is not None
+        H, mb, S, nwg = 256, 4096, (8 if kx else 4), 128
         tot = 2 * H * H + 2 * H * 20 + 6 * H + 12            # flat layout incl. pads (satrl_ppo_layout)
-        alg = {"Cijk": 2 * 2 * mb * H * 4 + 2 * S * H * H * 4,
+        dw2 = "dw2_kx_kernel" if kx else "Cijk"
+        alg = {dw2: (2 * 2 * 3 * mb * H * 2 if kx else 2 * 2 * mb * H * 4) + 2 * S * H * H * 4,
                "reduce_kernel": (2 * S * H * H + nwg * 2 * H * 20 + nwg * (6 * H + 12)) * 4 + tot * 4,
-               "adam_kernel": 4 * tot * 4 + 3 * tot * 4 + 2 * H * H * 4}
+               "adam_kernel": 4 * tot * 4 + 3 * tot * 4 + 2 * H * H * (6 if kx else 4)}
         chain = {}
-        for sub in ("Cijk", "reduce_kernel", "adam_kernel"):
+        for sub in (dw2, "reduce_kernel", "adam_kernel"):
             f_kb, nf = pmc_per_dispatch(sf, sub, "FETCH_SIZE")
             w_kb, nw = pmc_per_dispatch(sw, sub, "WRITE_SIZE")
             busy, nb = pmc_per_dispatch(sm, sub, "SQ_VALU_MFMA_BUSY_CYCLES")
@@ -112,7 +123,8 @@ def main():
                           "mfma_busy_frac_dispatch_window": busy / (grbm / 8.0 * 1024) if busy and grbm else None}
         res = {"kernels": chain, "hidden": H, "minibatch": mb, "dw2_splits": S,
                "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
-               "definition": "per-dispatch medians; Cijk = the hipBLASLt dW2 GEMM (1.07 GFLOP per launch); "
+               "definition": "per-dispatch medians; dw2_kx_kernel = the split-bf16 dW2 on the rowpass's k-packed "
+                             "planes, Cijk = the hipBLASLt dW2 GEMM (1.07 GFLOP per launch, f32-equivalent); "
                              "mfma_busy_frac as in the rowpass summary, over the --pmc dispatch window (a lower "
                              "bound for short dispatches)",
                "workload": "tools/step_workload.py (eager minibatch steps)"}
@@ -121,17 +133,21 @@ def main():
         print(json.dumps(res))
     pol = os.path.join(d, "pmc_policy_mfma", "run_counter_collection.csv")
     if os.path.exists(pol):
-        # the rollout's policy kernel (both agents' forward, 16384 rows each): per row and
-        # agent fc1 (K padded to 32) + fc2 = 72 v_mfma_f32_16x16x4f32
+        # the rollout's policy kernel (both agents' forward, 16384 rows each; 1024 workgroups
+        # of 8 waves, each wave 2 row tiles x 2 column tiles): fc1 (K padded to 32) on
+        # v_mfma_f32_16x16x4f32, 32 per wave; fc2 as split-bf16 v_mfma_f32_16x16x32_bf16,
+        # 8 chunks x 4 tiles x 6 = 192 per wave
         busy, nb = pmc_per_dispatch(pol, "policy_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
         grbm, ng = pmc_per_dispatch(pol, "policy_kernel", "GRBM_GUI_ACTIVE")
-        n_mfma = 2 * 16384 * (2 * 256 * 32 + 2 * 256 * 256) / (16 * 16 * 4 * 2)
-        res = {"kernel": "policy_kernel<256, 16, 0>", "hidden": 256, "num_envs": 16384, "agents": 2,
+        n_f32, n_bf16 = 1024 * 8 * 32, 1024 * 8 * 192
+        n_mfma = n_f32 + n_bf16
+        busy_expected = 32 * n_f32 + 16 * n_bf16
+        res = {"kernel": "policy_kernel<256, 8, 0>", "hidden": 256, "num_envs": 16384, "agents": 2,
                "dispatches": [nb, ng], "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
                "xcd_cycles": grbm / 8.0 if grbm else None,
                "mfma_busy_frac": busy / (grbm / 8.0 * 1024) if busy and grbm else None,
-               "mfma_instructions_per_launch": n_mfma,
-               "busy_cycles_per_mfma": busy / n_mfma if busy else None,
+               "mfma_instructions_per_launch": n_mfma, "busy_cycles_expected": busy_expected,
+               "busy_over_expected": busy / busy_expected if busy else None,
                "definition": "as in the rowpass summary: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 "
                              "SIMDs) over the --pmc dispatch window",
                "workload": "tools/policy_workload.py"}
