@@ -1412,7 +1412,8 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
 #pragma unroll
   for (int c = 0; c < kKxD - 1; ++c) stage(c < nch ? c : nch - 1);
   for (int c = 0; c < nch; ++c) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kKxD - 2) * (RUNS / 4)) : "memory");   // this wave's runs of chunk c
+    // this wave's runs of chunk c landed, and its reads of chunk c-1's slot are done
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kKxD - 2) * (RUNS / 4)) : "memory");
     __builtin_amdgcn_s_barrier();                                                   // every wave's; slot c-1 free
     stage(c + kKxD - 1 < nch ? c + kKxD - 1 : nch - 1);                             // (tail: a harmless reload)
     const int slot = c % kKxD;
