@@ -457,7 +457,13 @@ __device__ __forceinline__ void mfma_rows3(const unsigned short* __restrict__ A,
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int64_t w2x_plane(int H, int net, int which) { return (int64_t)(net * 2 + which) * 3 * H * H; }
 // elements of the W2X buffer, in floats
-__host__ __device__ constexpr int64_t w2x_floats(int H) { return H == 256 ? 6LL * H * H : 2LL * H * H; }
+// kW2Pre: the rowpass reads the pre-split planes (W2X at H = 256 is the
+// planes image) instead of splitting the f32 weights in registers (W2X is then
+// the f32 W2^T at every width).  Measured slower in the update (A/B below and
+// EXPERIMENTS.md round 4: the planes are 1.5x the weight bytes from L2, and
+// that ingest, not the split's VALU, bounds phases B and D), so off.
+constexpr bool kW2Pre = false;
+__host__ __device__ constexpr int64_t w2x_floats(int H) { return H == 256 && kW2Pre ? 6LL * H * H : 2LL * H * H; }
 // early-issued pre-split B chunks: one (two measured no faster, and their
 // registers live through phase C push the rowpass past 104 VGPRs: then a
 // 16-wave workgroup no longer fits beside two waves of another kernel per
@@ -892,7 +898,8 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   const unsigned short* W2p = static_cast<const unsigned short*>(W2X);
   // (H = 256: the H1 store after phase B, not between fc1 and B: 8 fewer VGPRs
   // live through B, so the 32-row kernel stays at <= 104)
-  mlp_forward<H, NW, R, true, BF3>(sm, P, BF3 ? W2p + w2x_plane(H, net, 0) : nullptr, net, mb - r0, gather,
+  constexpr bool W2S = BF3 && kW2Pre;
+  mlp_forward<H, NW, R, true, W2S>(sm, P, W2S ? W2p + w2x_plane(H, net, 0) : nullptr, net, mb - r0, gather,
                                    FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
@@ -900,7 +907,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
   B3Pre<CT> preDs;
-  if constexpr (BF3) mfma_rows3s_pre<H, CT>(W2p + w2x_plane(H, net, 1), n0, preDs);
+  if constexpr (W2S) mfma_rows3s_pre<H, CT>(W2p + w2x_plane(H, net, 1), n0, preDs);
   else mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
@@ -1041,8 +1048,10 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (BF3)
+  if constexpr (W2S)
     mfma_rows3s<H, LDP, PS, H, RT, CT, true>(dzp, W2p + w2x_plane(H, net, 1), n0, acc, &preDs);
+  else if constexpr (BF3)
+    mfma_rows3<H, LDP, PS, H, RT, CT, true>(dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
   else
     mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
@@ -1683,7 +1692,7 @@ __device__ __forceinline__ void w2x_tile(int H, int net, int tb, float4 v, void*
                                          float (&tile)[32][33]) {
   const int t = threadIdx.x, nl = t >> 3, kl = (t & 7) * 4, ntc = H / 32;
   const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
-  const bool bf3 = H == 256;
+  const bool bf3 = H == 256 && kW2Pre;
   unsigned short* X = static_cast<unsigned short*>(W2X);
   const int64_t HH = (int64_t)H * H;
   if (bf3) put3x4(X + w2x_plane(H, net, 0), (int64_t)(n0 + nl) * H + k0 + kl, HH, v);   // W2 [n][k]

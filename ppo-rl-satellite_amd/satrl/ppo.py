@@ -201,11 +201,20 @@ def _split3(x):
     return [t.view(torch.int16) for t in (hi, mid, lo)]
 
 
-def w2x_image(W2, H):
+def w2x_presplit(H):
+    """True when the library's fc2 operand image at this width is the bf16
+    planes image (its kW2Pre build), else the f32 fc2.weight^T."""
+    return w2x_floats(H) == 6 * H * H
+
+
+def w2x_image(W2, H, presplit=None):
     """Host statement of satrl_ppo_w2x_sync: the fc2 operand image of the two
-    nets' fc2.weight W2 (flat [2*H*H] f32), as the f32 tensor the kernels read."""
+    nets' fc2.weight W2 (flat [2*H*H] f32), as the f32 tensor the kernels read
+    (presplit None: the loaded library's format)."""
     W2 = W2.reshape(2, H, H)
-    if H != 256:
+    if presplit is None:
+        presplit = w2x_presplit(H)
+    if not presplit:
         return W2.transpose(1, 2).contiguous().reshape(-1)
     planes = [torch.stack(_split3(w.contiguous())) for n in range(2) for w in (W2[n], W2[n].t())]
     return torch.stack(planes).reshape(-1).view(torch.float32).clone()
@@ -213,7 +222,7 @@ def w2x_image(W2, H):
 
 def w2x_decode(img, H):
     """fc2.weight^T per net [2, H, H] f32 from an operand image."""
-    if H != 256:
+    if img.numel() == 2 * H * H:
         return img.view(2, H, H)
     p = img.view(torch.int16).view(2, 2, 3, H, H).view(torch.bfloat16).float()
     return (p[:, 1, 0] + p[:, 1, 1]) + p[:, 1, 2]
