@@ -9,8 +9,13 @@ mkdir -p gpurun_out
 HB=$!
 trap 'kill $HB 2>/dev/null || true' EXIT
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-      > gpurun_out/r4_gpu_tests.log 2>&1
+  # test failures are recorded and the profile round still runs; a time limit,
+  # abort or crash (rc >= 124) ends the script before any further GPU step
+  rc=0
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+      > gpurun_out/r4_gpu_tests.log 2>&1 || rc=$?
+  echo "gpu tests rc=$rc" | tee gpurun_out/r4_gpu_tests.rc
+  [ "$rc" -ge 124 ] && exit "$rc"
 fi
 timeout -k 10 1500 bash tools/profile_round.sh r4 > gpurun_out/r4_profile.log 2>&1
 timeout -k 10 400 python3 bench.py --profile-tag r4 > gpurun_out/r4_bench.json 2> gpurun_out/r4_bench.err
