@@ -1481,8 +1481,8 @@ int dw2_splits(int H, int mb, int net) {
 //   [0, nb2)          W2 region: 64 float4 columns x 4 chunks, S split-K slabs [2][S][H][H]
 //   [nb2, nb2+nb1)    W1 region: 32 float4 columns x 8 chunks, nw1 slabs [nw1][2][H][20]
 //   [nb2+nb1, ...)    tail: 8 float4 columns x 32 chunks, nwg slabs [nwg][6H+12]
-// A chunk sums slabs c, c+CH, ... (all loads independent: one or two
-// latency rounds), then chunk 0 adds the CH partials in order.
+// A chunk sums slabs c, c+CH, ... in that order, every load issued before the
+// first add (one latency round), then chunk 0 adds the CH partials in order.
 // ---------------------------------------------------------------------------
 struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
 constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;   // chunks per column: W1, tail, W2 regions
@@ -1498,6 +1498,24 @@ __device__ __forceinline__ double sq4(float4 v) {
   return (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
 }
 
+// s += part[w] for w = first, first + step, ... < nparts (at most NL terms), in
+// that order: the NL loads go out first (clamped indices, so none is a branch)
+// and the terms past nparts are selected to +0, so the sum is the plain loop's
+// bit for bit (s starts at +0 and a round-to-nearest sum is never -0, so
+// s + 0 == s).  (A runtime-trip loop unrolled by the compiler puts its
+// remainder iterations in a prologue of one load, wait, add each: the tail
+// region's four slabs per thread were four serial load round trips.)
+template <int NL>
+__device__ __forceinline__ void sum_strided4(float4& s, const float4* __restrict__ part, int64_t stride4,
+                                             int first, int step, int nparts, int64_t col) {
+  float4 v[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) v[i] = part[(int64_t)min(first + i * step, nparts - 1) * stride4 + col];
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s = f4add(s, first + i * step < nparts ? v[i] : z);
+}
+
 template <int CH>
 __device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, int64_t stride4, int nparts,
                                              int64_t col, bool valid, float4* red) {
@@ -1505,8 +1523,12 @@ __device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, in
   const int t = threadIdx.x, e = t % EB, c = t / EB;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (valid) {
-#pragma unroll 16
-    for (int w = c; w < nparts; w += CH) s = f4add(s, part[(int64_t)w * stride4 + col]);
+    const int m = (nparts + CH - 1) / CH;                          // terms of the longest chunk (uniform)
+    if (m <= 2) sum_strided4<2>(s, part, stride4, c, CH, nparts, col);
+    else if (m <= 4) sum_strided4<4>(s, part, stride4, c, CH, nparts, col);
+    else if (m <= 8) sum_strided4<8>(s, part, stride4, c, CH, nparts, col);
+    else   // (H = 64's 128 dW2 slabs: two rounds of 16; one round of 32 measured 1.1 us slower)
+      for (int w = c; w < nparts; w += 16 * CH) sum_strided4<16>(s, part, stride4, w, CH, nparts, col);
   }
   red[t] = s;
   __syncthreads();
@@ -1548,13 +1570,21 @@ __device__ __forceinline__ void wave_sum2(double& a, double& c) {
   a = ((lane_d(a, 0) + lane_d(a, 16)) + lane_d(a, 32)) + lane_d(a, 48);
   c = ((lane_d(c, 0) + lane_d(c, 16)) + lane_d(c, 32)) + lane_d(c, 48);
 }
+// (256-thread blocks: reduce, adam and the peer all-reduce.  The four wave
+// pairs are read at once; a loop over blockDim's wave count was one LDS read
+// round trip per wave)
 __device__ __forceinline__ void block_sum2(double& a, double& c, double* sh) {
+  constexpr int NW = 4;
   wave_sum2(a, c);
-  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh[2 * w] = a; sh[2 * w + 1] = c; }
   __syncthreads();
+  double v[2 * NW];
+#pragma unroll
+  for (int k = 0; k < 2 * NW; ++k) v[k] = sh[k];
   a = 0.0; c = 0.0;
-  for (int k = 0; k < nw; ++k) { a += sh[2 * k]; c += sh[2 * k + 1]; }
+#pragma unroll
+  for (int k = 0; k < NW; ++k) { a += v[2 * k]; c += v[2 * k + 1]; }
 }
 
 // what a reduce thread ends with: the float4 of G it wrote (lead threads
