@@ -28,9 +28,11 @@ VARIANTS = {
     bs[2] = __builtin_bit_cast(s8v, b[t][0]);""")],
     # timing probe (wrong results): Adam's bias corrections as constants, no
     # dependent table load behind the step-count load
-    "t_nobct": [("""    const double bc1 = st < bct_len ? bct[2 * st] : 1.0;
-    const double bc2s = st < bct_len ? bct[2 * st + 1] : 1.0;""", """    const double bc1 = st < 0 ? bct[0] : 0.5;
-    const double bc2s = st < 0 ? bct[1] : 0.25;""")],
+    "t_nobct": [("""  const double2 bca = bct2[ka < bct_len ? ka : bct_len - 1], bcc = bct2[kc < bct_len ? kc : bct_len - 1];""",
+                 """  const double2 bca = bct2[0], bcc = bct2[1];""")],
+    # dW2 (k-packed) split-K ways: about 128 / 512 workgroups instead of 256
+    "kx128": [("constexpr int kKxWgs = 256;", "constexpr int kKxWgs = 128;")],
+    "kx512": [("constexpr int kKxWgs = 256;", "constexpr int kKxWgs = 512;")],
     "t_noalds": [("""    } else {
       a3_chunk<LDP, PS, RT>(ap + 32 * c, aa[0]);
     }""", """    } else {
