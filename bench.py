@@ -517,13 +517,15 @@ def run(a, world):
     # the rollout's policy kernel (both agents' forward, the (num_envs x hidden)
     # GEMMs): per row and agent fc1 2*18*H + H, fc2 2*H*H + H, mean layer 2*3*H + 3
     policy_roof = None
-    pol_us = prof_avg_us("policy_kernel<%d;%d;0>" % (a.hidden, a.hidden // 16))
+    pol_nw = 8 if a.hidden == 256 else a.hidden // 16      # waves per policy workgroup (csrc kPolNW at H 256)
+    pol_us = prof_avg_us("policy_kernel<%d;%d;0>" % (a.hidden, pol_nw))
     if pol_us:
         pol_flop = 2 * a.num_envs * (2 * 18 * a.hidden + a.hidden + 2 * a.hidden * a.hidden + a.hidden
                                      + 2 * 3 * a.hidden + 3)
         pol_tfs = pol_flop / (pol_us * 1e-6) / 1e12
-        policy_roof = {"kernel": f"policy_kernel<{a.hidden},{a.hidden // 16},0> (both agents' choose_action, "
-                                 "f32 MFMA)",
+        policy_roof = {"kernel": f"policy_kernel<{a.hidden},{pol_nw},0> (both agents' choose_action; "
+                                 + ("fc1 on f32 MFMA, fc2 on split-bf16 MFMA, FLOPs counted as f32)" if a.hidden == 256
+                                    else "f32 MFMA)"),
                        "bound": "mfma", "achieved": pol_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                        "frac": pol_tfs / FP32_MFMA_PEAK_TFS, "avg_launch_us": pol_us, "flop_per_launch": pol_flop,
                        "timing": f"rocprofv3 average over the rollout's launches "
