@@ -33,6 +33,9 @@ VARIANTS = {
     # dW2 (k-packed) split-K ways: about 128 / 512 workgroups instead of 256
     "kx128": [("constexpr int kKxWgs = 256;", "constexpr int kKxWgs = 128;")],
     "kx512": [("constexpr int kKxWgs = 256;", "constexpr int kKxWgs = 512;")],
+    # dw2_kx LDS ring depth (slots; chunks kKxD - 1 ahead; 24 KB + pad per slot)
+    "kxd4": [("constexpr int kKxD = 3; ", "constexpr int kKxD = 4; ")],
+    "kxd6": [("constexpr int kKxD = 3; ", "constexpr int kKxD = 6; ")],
     "t_noalds": [("""    } else {
       a3_chunk<LDP, PS, RT>(ap + 32 * c, aa[0]);
     }""", """    } else {
