@@ -188,7 +188,10 @@ def test_update_matches_reference():
         step_ref = np.abs(ref - p0).max()
         diff = np.abs(got - ref)
         worst = max(worst, float(diff.max()))
-        assert np.allclose(got, ref, rtol=1e-3, atol=2 * lr_a * nsteps * 0.01 + 1e-6), (name, diff.max(), step_ref)
+        # 5e-5 absolute: about 1 % of the movement 24 Adam steps at lr 2e-4 can
+        # make (lr * nsteps = 4.8e-3), 2.8x the measured worst (1.8e-5, the
+        # f32 gradient sums adding in another order than torch's)
+        assert np.allclose(got, ref, rtol=0, atol=5e-5), (name, diff.max(), step_ref)
     print(f"update parity: worst abs param diff {worst:.3e} after {nsteps} Adam steps")
     la, lc = agent.L.lr_now
     # lr lives in an f32 device tensor (the reference keeps a python float)
