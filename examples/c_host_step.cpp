@@ -153,7 +153,7 @@ int main(int argc, char** argv) {
   PPO_OK(satrl_ppo_sizes(H, mb, &nwg, &nblk));
 
   float* d_P = dev(P);
-  // the fc2 operand image (pre-split bf16 planes at H = 256), built on the device from P
+  // the fc2 operand image (the f32 fc2.weight^T), built on the device from P
   const int64_t w2x = satrl_ppo_w2x_floats(H);
   float* d_W2X = dev<float>((size_t)w2x);
   PPO_OK(satrl_ppo_w2x_sync(H, -1, d_P, d_W2X, st));

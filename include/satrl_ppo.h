@@ -108,11 +108,10 @@ int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* step
                    void* stream);
 
 /* The fc2 operand image W2X the rowpass reads for its two H x H products
- * (and satrl_ppo_adam keeps current), satrl_ppo_w2x_floats(H) floats:
- *   H <= 128  f32 fc2.weight^T per net, [2][H][H];
- *   H = 256   fc2.weight and its transpose split once into three bf16 planes
- *             (hi + mid + lo == the f32 weight exactly), the split-bf16 MFMA's
- *             B operands: u16 [net][W2, W2^T][hi, mid, lo][H][H].
+ * (and satrl_ppo_adam keeps current), satrl_ppo_w2x_floats(H) floats: the
+ * f32 fc2.weight^T per net, [2][H][H], at every width (phase D's B operand;
+ * at H = 256 the rowpass splits it into bf16 planes in registers -- a
+ * pre-split planes image measured slower).
  * satrl_ppo_w2x_sync builds it from P (net -1: both) -- after a load or any
  * write to fc2.weight outside satrl_ppo_adam.                               */
 int64_t satrl_ppo_w2x_floats(int H);

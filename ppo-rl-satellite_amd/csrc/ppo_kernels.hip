@@ -387,14 +387,6 @@ __device__ __forceinline__ void mfma3_regs(const s8v (&a)[RT][3], const float4 (
     for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma6(a[rt], bs, acc[rt][t]);
   }
 }
-// the same on B planes split beforehand (the fc2 operand image, below)
-template <int RT, int CT>
-__device__ __forceinline__ void mfma3s_regs(const s8v (&a)[RT][3], const s8v (&b)[CT][3], f4 (&acc)[RT][CT]) {
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt][t] = mfma6(a[rt], b[t], acc[rt][t]);
-}
 template <int LDP, int PS, int RT>
 __device__ __forceinline__ void a3_chunk(const unsigned short* __restrict__ ap, s8v (&a)[RT][3]) {
 #pragma unroll
@@ -444,86 +436,14 @@ __device__ __forceinline__ void mfma_rows3(const unsigned short* __restrict__ A,
 }
 
 // ---------------------------------------------------------------------------
-// The fc2 operand image (W2X) at H = 256: fc2.weight and its transpose split
-// into their three bf16 planes ONCE per parameter change -- by adam_kernel
-// beside the f32 update, or by satrl_ppo_w2x_sync from P -- instead of in the
-// registers of every rowpass workgroup (256 workgroups x two phases, each
-// splitting the whole net: 36 VALU per chunk and wave, ≈3.4 us of the step
-// measured, EXPERIMENTS.md round 4).  The splits are the same RNE conversions
-// and exact subtractions, so every plane -- hence every MFMA input and result
-// bit -- is the in-register split's.  Layout (bf16 elements):
-//   [net][0: W2 [n][k] (phase B), 1: W2^T [k][n] (phase D)][plane hi, mid, lo][H][H]
-// At H <= 128 W2X is the f32 W2^T [2][H][H] the f32 path reads.
+// The fc2 operand image W2X: the f32 W2^T [2][H][H] of both nets (phases D of
+// the rowpass read fc2.weight transposed), written by adam_kernel beside each
+// updated 32x32 tile and by satrl_ppo_w2x_sync from P.  A pre-split bf16
+// planes image at H = 256 (no split VALU in the rowpass) was built and
+// measured slower -- 1.5x the weight bytes from L2 (EXPERIMENTS.md round 4,
+// commit e2546b9) -- so every width keeps the f32 image.
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int64_t w2x_plane(int H, int net, int which) { return (int64_t)(net * 2 + which) * 3 * H * H; }
-// elements of the W2X buffer, in floats
-// kW2Pre: the rowpass reads the pre-split planes (W2X at H = 256 is the
-// planes image) instead of splitting the f32 weights in registers (W2X is then
-// the f32 W2^T at every width).  Measured slower in the update (A/B below and
-// EXPERIMENTS.md round 4: the planes are 1.5x the weight bytes from L2, and
-// that ingest, not the split's VALU, bounds phases B and D), so off.
-constexpr bool kW2Pre = false;
-__host__ __device__ constexpr int64_t w2x_floats(int H) { return H == 256 && kW2Pre ? 6LL * H * H : 2LL * H * H; }
-// early-issued pre-split B chunks: one (two measured no faster, and their
-// registers live through phase C push the rowpass past 104 VGPRs: then a
-// 16-wave workgroup no longer fits beside two waves of another kernel per
-// SIMD -- the peer all-reduce of a second rank on the same device)
-constexpr int kPre3 = 1;
-template <int CT>
-struct B3Pre {
-  s8v bb[kPre3][CT][3];
-};
-// one 32-wide k chunk of pre-split B: the three planes (plane stride PSB) of
-// the lane's 8 k, as the f32 path's b_chunk holds them before its split
-template <int CT, int LDB, int PSB>
-__device__ __forceinline__ void b3_chunk(const unsigned short* __restrict__ bp, s8v (&b)[CT][3]) {
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int p = 0; p < 3; ++p) b[t][p] = *reinterpret_cast<const s8v*>(bp + (int64_t)p * PSB + 16 * t * LDB);
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <int LDB, int CT>
-__device__ __forceinline__ void mfma_rows3s_pre(const unsigned short* __restrict__ B, int n0, B3Pre<CT>& pre) {
-  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const unsigned short* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
-#pragma unroll
-  for (int c = 0; c < kPre3; ++c) b3_chunk<CT, LDB, LDB * LDB>(bp + 32 * c, pre.bb[c]);
-}
-// mfma_rows3 on B planes split beforehand: B = three bf16 planes [K rows of
-// LDB] (plane stride K * LDB), kBPD3 chunks ahead, the first kBPD optionally
-// issued early (pre); the MFMA sequence is mfma_rows3's
-template <int K, int LDP, int PS, int LDB, int RT, int CT, bool PRE = false>
-__device__ __forceinline__ void mfma_rows3s(const unsigned short* __restrict__ A, const unsigned short* __restrict__ B,
-                                            int n0, f4 (&acc)[RT][CT], const B3Pre<CT>* pre = nullptr) {
-  constexpr int NC = K / 32, PSB = K * LDB;
-  constexpr int BPD = kBPD3 < NC ? kBPD3 : NC, NB = BPD + 1;
-  static_assert(!PRE || BPD >= kPre3, "early-issued chunks fit the ring");
-  const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-  const unsigned short* ap = A + i * LDP + 8 * g;
-  const unsigned short* bp = B + (int64_t)(n0 + i) * LDB + 8 * g;
-  s8v bb[NB][CT][3];
-  s8v aa[RT][3];
-  if constexpr (PRE) {
-#pragma unroll
-    for (int c = 0; c < kPre3; ++c)
-#pragma unroll
-      for (int t = 0; t < CT; ++t)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) bb[c][t][p] = pre->bb[c][t][p];
-#pragma unroll
-    for (int c = kPre3; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);
-  } else {
-#pragma unroll
-    for (int c = 0; c < BPD; ++c) b3_chunk<CT, LDB, PSB>(bp + 32 * c, bb[c]);
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (c + BPD < NC) b3_chunk<CT, LDB, PSB>(bp + 32 * (c + BPD), bb[(c + BPD) % NB]);
-    a3_chunk<LDP, PS, RT>(ap + 32 * c, aa);
-    mfma3s_regs<RT, CT>(aa, bb[c % NB], acc);
-  }
-}
+__host__ __device__ constexpr int64_t w2x_floats(int H) { return 2LL * H * H; }
 // the three planes of 4 consecutive elements v (at e, plane stride PS) as
 // three 8-B stores
 __device__ __forceinline__ void put3x4(unsigned short* __restrict__ img, int64_t e, int64_t PS, float4 v) {
@@ -599,11 +519,6 @@ __device__ __forceinline__ void store_rows(float* __restrict__ out, int ld, int 
 // barriers that leave the global stores and early weight chunks in flight
 // measured no faster, EXPERIMENTS.md round 3).
 __device__ __forceinline__ void rp_barrier() { __syncthreads(); }
-// a workgroup barrier that waits for this wave's LDS operations only, not for
-// its outstanding global loads / stores
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-constexpr bool kPreB3 = true;     // split-bf16 fc2: phase B's first weight chunks issued under fc1
-constexpr bool kLdsBar3 = false;  // split-bf16 fc2: an LDS-only barrier before phase B
 
 // Shared-memory block and forward pass (phases A, B and the output-layer dot
 // products of C) common to rowpass_kernel and policy_kernel, so the rollout's
@@ -627,9 +542,9 @@ struct MlpSmem {
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
 // tanh(fc1) goes to h1out[r * H + n].
-template <int H, int NW, int R, bool APRE, bool W2S, class Gather>
+template <int H, int NW, int R, bool APRE, class Gather>
 __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P,
-                                            const unsigned short* __restrict__ w2s, int net, int nvalid,
+                                            int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
                                             f4 (&acc)[R / 16][H / 16 / NW],
                                             float (&h1)[R / 16][H / 16 / NW][4],
@@ -674,13 +589,10 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(8);
   rp_barrier();
   PHASE_PROBE(9);
-  // (split-bf16 fc2) phase B's first weight chunks go out now, under fc1
-  // (W2S: from the pre-split planes of this net's fc2.weight, w2s)
-  static_assert(!W2S || kBf3<H>, "pre-split weights feed the split-bf16 path");
+  // (split-bf16 fc2) phase B's first weight chunks go out now, under fc1 (an
+  // LDS-only barrier below, leaving them in flight, measured no faster)
   WPre<CT> preB;
-  B3Pre<CT> preBs;
-  if constexpr (W2S) mfma_rows3s_pre<H, CT>(w2s, n0, preBs);
-  else if constexpr (kBf3<H> && kPreB3) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
+  if constexpr (kBf3<H>) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   float4 bw1[CT][2];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -714,15 +626,12 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
     }
   if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
   PHASE_PROBE(11);
-  if constexpr (kBf3<H> && kLdsBar3) lds_barrier();               // (the early chunks stay in flight)
-  else rp_barrier();
+  rp_barrier();
   PHASE_PROBE(1);
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
-  if constexpr (W2S)
-    mfma_rows3s<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, true>(sm.h1p, w2s, n0, acc, &preBs);
-  else if constexpr (kBf3<H>)
-    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, kPreB3>(
+  if constexpr (kBf3<H>)
+    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, true>(
         sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   else
     mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
@@ -893,22 +802,18 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
       head_consts();
     }
   };
-  // the fc2 operand image: pre-split bf16 planes at H = 256, else f32 W2^T
+  // the fc2 operand image: the f32 W2^T
   const float* W2T = static_cast<const float*>(W2X);
-  const unsigned short* W2p = static_cast<const unsigned short*>(W2X);
   // (H = 256: the H1 store after phase B, not between fc1 and B: 8 fewer VGPRs
   // live through B, so the 32-row kernel stays at <= 104)
-  constexpr bool W2S = BF3 && kW2Pre;
-  mlp_forward<H, NW, R, true, W2S>(sm, P, W2S ? W2p + w2x_plane(H, net, 0) : nullptr, net, mb - r0, gather,
+  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather,
                                    FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
   else if constexpr (BF3 && !FDW2) store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, h1);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
-  B3Pre<CT> preDs;
-  if constexpr (W2S) mfma_rows3s_pre<H, CT>(W2p + w2x_plane(H, net, 1), n0, preDs);
-  else mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
+  mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -1048,9 +953,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (W2S)
-    mfma_rows3s<H, LDP, PS, H, RT, CT, true>(dzp, W2p + w2x_plane(H, net, 1), n0, acc, &preDs);
-  else if constexpr (BF3)
+  if constexpr (BF3)
     mfma_rows3<H, LDP, PS, H, RT, CT, true>(dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
   else
     mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
@@ -1171,7 +1074,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW, R, false, false>(sm, P, nullptr, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  mlp_forward<H, NW, R, false>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
@@ -1715,23 +1618,19 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
 // into W2T (coalesced).  Blocks [nbw, ...): the rest of the layout, float4.
 // ---------------------------------------------------------------------------
 // The updated 32x32 tile tb of net's fc2.weight (thread t holds row n0 + t/8,
-// columns k0 + (t%8)*4 .. +3 in v) into the fc2 operand image: at H = 256
-// its bf16 planes and those of its transpose, else the f32 transpose (through
-// LDS, so every store is coalesced).  Every thread of the block calls it.
+// columns k0 + (t%8)*4 .. +3 in v) into the fc2 operand image, the f32
+// transpose (through LDS, so every store is coalesced).  Every thread of the
+// block calls it.
 __device__ __forceinline__ void w2x_tile(int H, int net, int tb, float4 v, void* __restrict__ W2X,
                                          float (&tile)[32][33]) {
   const int t = threadIdx.x, nl = t >> 3, kl = (t & 7) * 4, ntc = H / 32;
   const int n0 = (tb / ntc) * 32, k0 = (tb % ntc) * 32;
-  const bool bf3 = H == 256 && kW2Pre;
-  unsigned short* X = static_cast<unsigned short*>(W2X);
   const int64_t HH = (int64_t)H * H;
-  if (bf3) put3x4(X + w2x_plane(H, net, 0), (int64_t)(n0 + nl) * H + k0 + kl, HH, v);   // W2 [n][k]
   tile[nl][kl] = v.x; tile[nl][kl + 1] = v.y; tile[nl][kl + 2] = v.z; tile[nl][kl + 3] = v.w;
   __syncthreads();
   // W2T[net][k0 + t/8][n0 + (t%8)*4 + q] = W2[net][n0 + (t%8)*4 + q][k0 + t/8]
   const float4 o = make_float4(tile[kl][nl], tile[kl + 1][nl], tile[kl + 2][nl], tile[kl + 3][nl]);
-  if (bf3) put3x4(X + w2x_plane(H, net, 1), (int64_t)(k0 + nl) * H + n0 + kl, HH, o);
-  else reinterpret_cast<float4*>(W2X)[((int64_t)net * HH + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
+  reinterpret_cast<float4*>(W2X)[((int64_t)net * HH + (int64_t)(k0 + nl) * H + n0 + kl) / 4] = o;
 }
 
 // the fc2 operand image of P (satrl_ppo_w2x_sync): adam_kernel's W2 blocks

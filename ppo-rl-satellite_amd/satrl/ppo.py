@@ -780,8 +780,9 @@ class PPOLearner:
         self.critic = critic.to(self.device)
         P = self.P
         self.W2v = P[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
-        # the fc2 operand image the rowpass reads (f32 fc2.weight^T, or at H = 256 the
-        # pre-split bf16 planes of fc2.weight and its transpose; satrl_ppo.h)
+        # the fc2 operand image the rowpass reads (the f32 fc2.weight^T; satrl_ppo.h;
+        # w2x_image also writes the pre-split planes layout a kW2Pre build of
+        # commit e2546b9 reads)
         self.W2T = torch.zeros(w2x_floats(H), **f32)
         self.GW2v = self.G[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
         W1 = P[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)

@@ -15,10 +15,10 @@ VARIANTS = {
     # (round 4: L2 warm-up of W2 / W2T, reduce chunk counts, Adam's table load,
     # bf16x3 prefetch depth / A buffering / wave counts, dW2 split counts were
     # measured against this harness; EXPERIMENTS.md)
-    # the rowpass on the pre-split fc2 operand image (bf16 planes written by Adam)
-    "w2pre": [("constexpr bool kW2Pre = false;", "constexpr bool kW2Pre = true;")],
-    "nopreb": [("constexpr bool kPreB3 = true;", "constexpr bool kPreB3 = false;")],
-    "ldsbar": [("constexpr bool kLdsBar3 = false;", "constexpr bool kLdsBar3 = true;")],
+    # (the pre-split fc2 image `kW2Pre`, phase B without early chunks `kPreB3`
+    # and the LDS-only barrier `kLdsBar3` were knobs of the product source until
+    # they were measured and rejected; build them from commit e2546b9's source:
+    # make variant VSRC=<git show e2546b9:ppo-rl-satellite_amd/csrc/ppo_kernels.hip>)
     # timing probes only (wrong results): the split-bf16 fc2 without the weights' split VALU / without
     # the per-chunk A-plane LDS reads
     "t_nosplit": [("""    s8v bs[3];
