@@ -1425,7 +1425,7 @@ __device__ __forceinline__ float4 chunk_sum4(const float4* __restrict__ part, in
   constexpr int EB = 256 / CH;
   const int t = threadIdx.x, e = t % EB, c = t / EB;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid) {
+  if (valid && nparts > 0) {                                       // (the clamped index needs a slab)
     const int m = (nparts + CH - 1) / CH;                          // terms of the longest chunk (uniform)
     if (m <= 2) sum_strided4<2>(s, part, stride4, c, CH, nparts, col);
     else if (m <= 4) sum_strided4<4>(s, part, stride4, c, CH, nparts, col);
