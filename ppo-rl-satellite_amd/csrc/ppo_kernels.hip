@@ -1292,72 +1292,78 @@ __global__ void __launch_bounds__(256) dw2_bf3_kernel(int mb, int S, int KR, int
 // (row groups 16 B apart in bank space).  Every sum has a fixed order.
 // ---------------------------------------------------------------------------
 constexpr int kKxD = 3;                         // ring slots (chunks kKxD - 1 ahead)
-constexpr int kKxG = 1024 + 16;                 // bytes per (tensor, plane, row group) run in LDS
+// output tile width TW (64: 16 tiles per net, 8 splits of 512 rows at mb 4096;
+// 128: 4 tiles per net, half the plane bytes per workgroup, 32 splits)
+constexpr int kKxTW = 64;
+template <int TW>
 __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int net_sel,
                                                      const unsigned short* __restrict__ H1x,
                                                      const unsigned short* __restrict__ dZ2x, float* __restrict__ p2) {
-  constexpr int H = 256, TT = H / 64, RUNS = 2 * 3 * 4;         // runs per chunk: tensor x plane x row group
-  __shared__ __attribute__((aligned(16))) unsigned char ring[kKxD][RUNS][kKxG];
+  constexpr int H = 256, TT = H / TW, RUNS = 2 * 3 * 4;         // runs per chunk: tensor x plane x row group
+  constexpr int PPR = TW / 64, KG = TW * 16 + 16;               // 1-KB pieces per run, LDS bytes per run
+  constexpr int XN = TW / 32, PW = RUNS * PPR / 4;              // 16x16 tiles per wave side, pieces per wave
+  __shared__ __attribute__((aligned(16))) unsigned char ring[kKxD][RUNS][KG];
   const int t = threadIdx.x, w = t >> 6, l = t & 63, li = l & 15, lg = l >> 4;
   const int b = blockIdx.x, s = b % S, tile = (b / S) % (TT * TT);
   const int net = net_sel < 0 ? b / (S * TT * TT) : net_sel;
-  const int o0 = (tile / TT) * 64, n0 = (tile % TT) * 64;
+  const int o0 = (tile / TT) * TW, n0 = (tile % TT) * TW;
   const int64_t PL = kx_rows(mb) * H;
   const int c_begin = s * (KR / 32), nch = (int)((min((int64_t)(s + 1) * KR, kx_rows(mb)) - (int64_t)s * KR) / 32);
-  // run u = (tensor, plane, group) of chunk c: 64 columns x 8 rows, 1 KB contiguous in the plane
+  // piece v = (run u, 64-column half h) of chunk c: 64 columns x 8 rows, 1 KB contiguous in the plane
   auto stage = [&](int c) {
     const int slot = c % kKxD, cg = 4 * (c_begin + c);             // first row group of the chunk
 #pragma unroll
-    for (int k = 0; k < RUNS / 4; ++k) {
-      const int u = 4 * k + w, tz = u / 12, p = (u / 4) % 3, q = u % 4;   // wave w: runs w, w+4, ...
+    for (int k = 0; k < PW; ++k) {
+      const int v = 4 * k + w, u = v / PPR, h = v % PPR;            // wave w: pieces w, w+4, ...
+      const int tz = u / 12, p = (u / 4) % 3, q = u % 4;
       const unsigned short* src = (tz == 0 ? dZ2x : H1x) + (int64_t)net * 3 * PL + p * PL +
-                                  ((int64_t)(cg + q) * H + (tz == 0 ? o0 : n0) + l) * 8;
-      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)&ring[slot][u][0], 16, 0, 0);
+                                  ((int64_t)(cg + q) * H + (tz == 0 ? o0 : n0) + 64 * h + l) * 8;
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)&ring[slot][u][1024 * h], 16, 0, 0);
     }
   };
   const int wo = w >> 1, wn = w & 1;
-  f4 acc[2][2];
+  f4 acc[XN][XN];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < XN; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < XN; ++y) acc[x][y] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < kKxD - 1; ++c) stage(c < nch ? c : nch - 1);
   for (int c = 0; c < nch; ++c) {
-    // this wave's runs of chunk c landed, and its reads of chunk c-1's slot are done
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kKxD - 2) * (RUNS / 4)) : "memory");
+    // this wave's pieces of chunk c landed, and its reads of chunk c-1's slot are done
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((kKxD - 2) * PW) : "memory");
     __builtin_amdgcn_s_barrier();                                                   // every wave's; slot c-1 free
     stage(c + kKxD - 1 < nch ? c + kKxD - 1 : nch - 1);                             // (tail: a harmless reload)
     const int slot = c % kKxD;
-    s8v a[2][3], bq[2][3];
+    s8v a[XN][3], bq[XN][3];
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < XN; ++x)
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         // A[o][k] = dZ2[row 8lg + k'][o], B[k][n] = H1[row][n]: group lg of plane p
-        a[x][p] = *reinterpret_cast<const s8v*>(&ring[slot][0 * 12 + p * 4 + lg][(32 * wo + 16 * x + li) * 16]);
-        bq[x][p] = *reinterpret_cast<const s8v*>(&ring[slot][1 * 12 + p * 4 + lg][(32 * wn + 16 * x + li) * 16]);
+        a[x][p] = *reinterpret_cast<const s8v*>(&ring[slot][0 * 12 + p * 4 + lg][((TW / 2) * wo + 16 * x + li) * 16]);
+        bq[x][p] = *reinterpret_cast<const s8v*>(&ring[slot][1 * 12 + p * 4 + lg][((TW / 2) * wn + 16 * x + li) * 16]);
       }
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < XN; ++x)
 #pragma unroll
-      for (int y = 0; y < 2; ++y) acc[x][y] = mfma6(a[x], bq[y], acc[x][y]);
+      for (int y = 0; y < XN; ++y) acc[x][y] = mfma6(a[x], bq[y], acc[x][y]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // acc[x][y][q] = dW2[o0 + 32wo + 16x + 4lg + q][n0 + 32wn + 16y + li]
+  // acc[x][y][q] = dW2[o0 + (TW/2)wo + 16x + 4lg + q][n0 + (TW/2)wn + 16y + li]
   float* out = p2 + ((int64_t)net * S + s) * H * H;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < XN; ++x)
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
+    for (int y = 0; y < XN; ++y)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        out[(int64_t)(o0 + 32 * wo + 16 * x + 4 * lg + q) * H + n0 + 32 * wn + 16 * y + li] = acc[x][y][q];
+        out[(int64_t)(o0 + (TW / 2) * wo + 16 * x + 4 * lg + q) * H + n0 + (TW / 2) * wn + 16 * y + li] = acc[x][y][q];
 }
 // split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split
 constexpr int kKxWgs = 256;
 int kx_splits(int mb, int net, int target = kKxWgs) {
-  const int tiles = (net < 0 ? 2 : 1) * 16, nch = (int)(kx_rows(mb) / 32);
+  const int tiles = (net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW), nch = (int)(kx_rows(mb) / 32);
   int S = target / tiles;
   if (S > nch) S = nch;
   if (S < 1) S = 1;
@@ -2066,8 +2072,8 @@ int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void*
   if (H != 256 || mb <= 0 || net < -1 || net > 1 || S < 1 || !H1x || !dZ2x || !p2) return -1;
   const int nch = (int)(kx_rows(mb) / 32), cps = (nch + S - 1) / S;
   if ((int64_t)cps * (S - 1) >= nch) return -1;                  // an empty split: use satrl_ppo_dw2_kx_splits
-  const dim3 g((unsigned)((net < 0 ? 2 : 1) * 16 * S));
-  hipLaunchKernelGGL(dw2_kx_kernel, g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net,
+  const dim3 g((unsigned)((net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW) * S));
+  hipLaunchKernelGGL(dw2_kx_kernel<kKxTW>, g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net,
                      static_cast<const unsigned short*>(H1x), static_cast<const unsigned short*>(dZ2x), p2);
   LAUNCH_CHECK();
   return 0;

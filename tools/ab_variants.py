@@ -36,6 +36,8 @@ VARIANTS = {
     # dw2_kx LDS ring depth (slots; chunks kKxD - 1 ahead; 24 KB + pad per slot)
     "kxd4": [("constexpr int kKxD = 3; ", "constexpr int kKxD = 4; ")],
     "kxd6": [("constexpr int kKxD = 3; ", "constexpr int kKxD = 6; ")],
+    # dw2_kx on 128x128 output tiles (half the plane bytes per workgroup, 32 splits)
+    "kxt128": [("constexpr int kKxTW = 64;", "constexpr int kKxTW = 128;")],
     "t_noalds": [("""    } else {
       a3_chunk<LDP, PS, RT>(ap + 32 * c, aa[0]);
     }""", """    } else {
