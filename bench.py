@@ -31,6 +31,13 @@ SURROGATE_FLOP_PER_ENV = 2 * (5 * 256 + 256 * 128 + 128 * 64 + 64 * 10)   # Impr
 ENV_BYTES_PER_STEP = 381       # DESIGN.md "Roofline": state 16 f64 + 3 i32 planes r/w, actions, obs, reward, done
 
 
+def dw2_kernel_name(st):
+    """Which hand-written kernel computes dW2 on a FusedMinibatch's path."""
+    if st.kx(st.mb):
+        return "dw2_kx (split-bf16 from k-packed planes)"
+    return "rowpass_dw2 (fused)" if st.fused_dw2 else "dw2_kernel (f32)"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -733,9 +740,7 @@ def run(a, world):
         dp = {"world": n_gpus, "backend": dist.get_backend(pg), "dp_minibatch": tr.dp_minibatch,
               "allreduce": a.allreduce,
               "gradient_bucket_bytes": L.G.numel() * 4, "minibatch_step_us": t_chain,
-              "dw2_plan": {"kernel": "dw2_kx (split-bf16)" if st.kx(st.mb) else "library",
-                           "solution": getattr(st, "dw2_algo", None) if st.lib_gemm else None,
-                           "source": getattr(st, "dw2_source", None) if st.lib_gemm else None}}
+              "dw2_kernel": dw2_kernel_name(st)}
         if L.comm is not None:
             scratch = torch.zeros_like(L.G)
             L.comm.warm(scratch)
@@ -755,7 +760,7 @@ def run(a, world):
         # the peer all-reduce (fused with reduce_dp) on the same bucket, A/B beside RCCL
         try:
             from satrl.peer import PeerComm
-            peer = L.peer if L.peer is not None else PeerComm(pg, L.G.numel(), "cuda")
+            peer = L.peer if L.peer is not None else PeerComm(pg, L.G.numel(), "cuda", L.H)
             scratch = torch.randn(L.G.numel(), device="cuda")
             nsq_s = torch.zeros_like(st.nsq[0])
             steps_s = torch.zeros(2, dtype=torch.float64, device="cuda")
@@ -801,9 +806,7 @@ def run(a, world):
             dp["configs3_semantics_slice"] = {
                 "global_minibatch": a.minibatch, "rows_per_rank": mbg, "minibatches": a.global_slice,
                 "us_per_global_minibatch_step": us_g,
-                "dw2_plan": {"kernel": "dw2_kx (split-bf16)" if stg.kx(stg.mb) else "library",
-                           "solution": getattr(stg, "dw2_algo", None) if stg.lib_gemm else None,
-                             "source": getattr(stg, "dw2_source", None) if stg.lib_gemm else None},
+                "dw2_kernel": dw2_kernel_name(stg),
                 "note": ("global-minibatch mode (the reference's BatchSampler(..., 4096) semantics, "
                          "ppo_continuous.py:215) timed on a bounded slice after the run: wall time of "
                          f"{a.global_slice} minibatch steps between barriers, max over ranks; the "

@@ -1,12 +1,12 @@
 // A C++ host with no Python and no torch in the process driving the hot path
 // through the C ABI alone (include/satenv.h, include/satrl_ppo.h): the
 // training loop's env steps (satenv_step_autoreset, CPPO_main.py:119-153) and
-// one PPO minibatch step at H = 256 (rowpass -> dW2 -> reduce -> Adam,
-// ppo_continuous.py:213-239).  It writes its inputs and outputs as raw
+// PPO minibatch steps at H = 256 (rowpass -> dW2 -> reduce -> Adam,
+// ppo_continuous.py:213-239) at mb 4096 and 512.  It writes its inputs and outputs as raw
 // little-endian arrays so tests/test_c_host_gpu.py can run the same inputs
 // through the Python package and compare.
 //
-//   c_host_step <out_dir> [dw2_solution_index [dw2_kernel_name]]
+//   c_host_step <out_dir>
 //
 // Built by `make -C ppo-rl-satellite_amd/csrc c-host` (__graft_entry__.build()).
 #include <hip/hip_runtime.h>
@@ -82,50 +82,13 @@ void save(const std::string& dir, const char* name, const std::vector<T>& v) {
   std::fclose(f);
 }
 
-}  // namespace
-
-int main(int argc, char** argv) {
-  if (argc < 2) {
-    std::fprintf(stderr, "usage: %s <out_dir> [dw2_solution_index [dw2_kernel_name]]\n", argv[0]);
-    return 1;
-  }
-  const std::string out = argv[1];
-  hipStream_t st;
-  HIP_OK(hipStreamCreate(&st));
-
-  // ---- env: N envs, T autoreset steps of uniform actions --------------------------
-  const int64_t N = 2048;
-  const int T = 40;
-  satenv_params p;
-  ENV_OK(satenv_default_params(&p));
-  p.d_capture = 15000.0;
-  p.max_episode_steps = 12;                       // episodes end and reset inside the window
-  satenv_env* env = nullptr;
-  ENV_OK(satenv_create(&env, N, &p, 0));
-  std::vector<float> pa((size_t)T * N * 3), ea((size_t)T * N * 3);
-  for (auto& v : pa) v = unif(-1.6f, 1.6f);
-  for (auto& v : ea) v = unif(-1.6f, 1.6f);
-  float* d_pa = dev(pa);
-  float* d_ea = dev(ea);
-  float* d_obs = dev<float>((size_t)N * 18);
-  float* d_rew = dev<float>((size_t)T * N);
-  uint8_t* d_done = dev<uint8_t>((size_t)T * N);
-  double* d_stats = dev<double>(4);
-  ENV_OK(satenv_reset(env, 0, nullptr, d_obs, nullptr, st));
-  for (int t = 0; t < T; ++t)
-    ENV_OK(satenv_step_autoreset(env, d_pa + (size_t)t * N * 3, d_ea + (size_t)t * N * 3, d_obs, d_rew + (size_t)t * N,
-                                 d_done + (size_t)t * N, d_stats, st));
-  HIP_OK(hipStreamSynchronize(st));
-  save(out, "env_pa.f32", pa);
-  save(out, "env_ea.f32", ea);
-  save(out, "env_obs.f32", host(d_obs, (size_t)N * 18));
-  save(out, "env_rew.f32", host(d_rew, (size_t)T * N));
-  save(out, "env_done.u8", host(d_done, (size_t)T * N));
-  save(out, "env_stats.f64", host(d_stats, 4));
-  ENV_OK(satenv_destroy(env));
-
-  // ---- one PPO minibatch step, H = 256, mb = 4096 ------------------------------------
-  const int H = 256, mb = 4096, S = 4;
+// one PPO minibatch step at H = 256 on mb packed rows, the product's kernel
+// sequence (rowpass with k-packed bf16 H1 / dZ2 planes -> dW2 on them ->
+// reduce -> Adam), plus the f32-row rowpass's H1 / dZ2 for comparison; the
+// outputs go to <out>/ppo<mb>_*
+void ppo_step(const std::string& out, int mb, hipStream_t st) {
+  const int H = 256;
+  const std::string tag = "ppo" + std::to_string(mb) + "_";
   int64_t off[SATRL_PPO_NOFF];
   PPO_OK(satrl_ppo_layout(H, off));
   const int64_t total = off[SATRL_PPO_TOTAL];
@@ -165,56 +128,90 @@ int main(int argc, char** argv) {
   float* d_dZ2 = dev<float>(2 * (size_t)mb * H);
   float* d_pt = dev<float>((size_t)nwg * (6 * H + 12));
   float* d_pw = dev<float>((size_t)nwg * 2 * H * 20);
-  float* d_p2 = dev<float>(2 * (size_t)S * H * H);
   double* d_nsq = dev<double>(2 * (size_t)nblk);
   double* d_steps = dev<double>(2);
   double* d_bct = dev(bct);
   float* d_lr = dev(lr);
 
-  int pinned = 0;
-  if (argc > 2) {                                 // the Python host's pinned solution, when this library has it
-    pinned = satrl_ppo_dw2_lib_pin(H, mb, -1, S, std::atoi(argv[2]), argc > 3 ? argv[3] : nullptr) == 0;
-    if (!pinned) std::printf("c_host_step: dW2 solution %s not in this hipBLASLt (%s); tuning\n", argv[2],
-                             satrl_ppo_last_error());
-  }
-  int64_t wsb = 0;
-  int algo = -1;
-  PPO_OK(satrl_ppo_dw2_lib_workspace(H, mb, -1, S, &wsb, &algo));
-  uint8_t* d_ws = wsb > 0 ? dev<uint8_t>((size_t)wsb) : nullptr;
-
   PPO_OK(satrl_ppo_rowpass(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1, d_dZ2, d_pt, d_pw, st));
   HIP_OK(hipStreamSynchronize(st));
-  save(out, "ppo_H1.f32", host(d_H1, 2 * (size_t)mb * H));
-  save(out, "ppo_dZ2.f32", host(d_dZ2, 2 * (size_t)mb * H));
-  // the product step at this shape: the rowpass with k-packed bf16 H1 / dZ2
-  // planes and the split-bf16 dW2 on them (the library GEMM above serves the
-  // short minibatches; kept here as the plan-pinning example)
-  PPO_OK(satrl_ppo_dw2_lib(H, mb, -1, S, d_H1, d_dZ2, d_p2, d_ws, wsb, st));
+  save(out, (tag + "H1.f32").c_str(), host(d_H1, 2 * (size_t)mb * H));
+  save(out, (tag + "dZ2.f32").c_str(), host(d_dZ2, 2 * (size_t)mb * H));
+  // the product step: the rowpass with k-packed bf16 H1 / dZ2 planes and the
+  // split-bf16 dW2 on them (every kernel hand-written, no library tiles)
   const int64_t kxe = satrl_ppo_kx_elems(H, mb);
   uint16_t* d_H1x = dev<uint16_t>((size_t)kxe);
   uint16_t* d_dZ2x = dev<uint16_t>((size_t)kxe);
-  const int Sx = satrl_ppo_dw2_kx_splits(H, mb, -1);
-  float* d_p2x = dev<float>(2 * (size_t)Sx * H * H);
+  const int S = satrl_ppo_dw2_kx_splits(H, mb, -1);
+  float* d_p2 = dev<float>(2 * (size_t)S * H * H);
   PPO_OK(satrl_ppo_rowpass_kx(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1x, d_dZ2x, d_pt, d_pw,
                               st));
-  PPO_OK(satrl_ppo_dw2_kx(H, mb, -1, Sx, d_H1x, d_dZ2x, d_p2x, st));
-  PPO_OK(satrl_ppo_reduce(H, mb, -1, Sx, 3, d_p2x, d_pw, d_pt, d_G, d_nsq, d_steps, st));
+  PPO_OK(satrl_ppo_dw2_kx(H, mb, -1, S, d_H1x, d_dZ2x, d_p2, st));
+  PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, d_pw, d_pt, d_G, d_nsq, d_steps, st));
   PPO_OK(satrl_ppo_adam(H, mb, -1, d_nsq, d_steps, d_bct, (int)(bct.size() / 2), d_lr, 0.9f, 0.999f, 1e-5f, 0.5f, 1,
                         d_G, d_P, d_M, d_V, d_W2X, st));
   HIP_OK(hipStreamSynchronize(st));
-  save(out, "ppo_P0.f32", P);
-  save(out, "ppo_src.f32", src);
-  save(out, "ppo_bct.f64", bct);
-  save(out, "ppo_G.f32", host(d_G, (size_t)total));
-  save(out, "ppo_P.f32", host(d_P, (size_t)total));
-  save(out, "ppo_M.f32", host(d_M, (size_t)total));
-  save(out, "ppo_V.f32", host(d_V, (size_t)total));
-  save(out, "ppo_W2T.f32", host(d_W2X, (size_t)w2x));
-  save(out, "ppo_steps.f64", host(d_steps, 2));
-  char kname[256] = {0};
-  int used = -1;
-  PPO_OK(satrl_ppo_dw2_lib_plan_info(H, mb, -1, S, &used, kname, (int)sizeof(kname)));
-  std::printf("c_host_step: %lld envs x %d steps, one minibatch step (H %d, mb %d); dW2 solution %d %s%s\n",
-              (long long)N, T, H, mb, used, kname, pinned ? " (pinned)" : "");
+  save(out, (tag + "P0.f32").c_str(), P);
+  save(out, (tag + "src.f32").c_str(), src);
+  save(out, (tag + "bct.f64").c_str(), bct);
+  save(out, (tag + "G.f32").c_str(), host(d_G, (size_t)total));
+  save(out, (tag + "P.f32").c_str(), host(d_P, (size_t)total));
+  save(out, (tag + "M.f32").c_str(), host(d_M, (size_t)total));
+  save(out, (tag + "V.f32").c_str(), host(d_V, (size_t)total));
+  save(out, (tag + "W2T.f32").c_str(), host(d_W2X, (size_t)w2x));
+  save(out, (tag + "steps.f64").c_str(), host(d_steps, 2));
+  for (void* q : {(void*)d_P, (void*)d_W2X, (void*)d_M, (void*)d_V, (void*)d_G, (void*)d_src, (void*)d_H1,
+                  (void*)d_dZ2, (void*)d_pt, (void*)d_pw, (void*)d_nsq, (void*)d_steps, (void*)d_bct, (void*)d_lr,
+                  (void*)d_H1x, (void*)d_dZ2x, (void*)d_p2})
+    HIP_OK(hipFree(q));
+  std::printf("c_host_step: one minibatch step (H %d, mb %d, dW2 split %d ways)\n", H, mb, S);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s <out_dir>\n", argv[0]);
+    return 1;
+  }
+  const std::string out = argv[1];
+  hipStream_t st;
+  HIP_OK(hipStreamCreate(&st));
+
+  // ---- env: N envs, T autoreset steps of uniform actions --------------------------
+  const int64_t N = 2048;
+  const int T = 40;
+  satenv_params p;
+  ENV_OK(satenv_default_params(&p));
+  p.d_capture = 15000.0;
+  p.max_episode_steps = 12;                       // episodes end and reset inside the window
+  satenv_env* env = nullptr;
+  ENV_OK(satenv_create(&env, N, &p, 0));
+  std::vector<float> pa((size_t)T * N * 3), ea((size_t)T * N * 3);
+  for (auto& v : pa) v = unif(-1.6f, 1.6f);
+  for (auto& v : ea) v = unif(-1.6f, 1.6f);
+  float* d_pa = dev(pa);
+  float* d_ea = dev(ea);
+  float* d_obs = dev<float>((size_t)N * 18);
+  float* d_rew = dev<float>((size_t)T * N);
+  uint8_t* d_done = dev<uint8_t>((size_t)T * N);
+  double* d_stats = dev<double>(4);
+  ENV_OK(satenv_reset(env, 0, nullptr, d_obs, nullptr, st));
+  for (int t = 0; t < T; ++t)
+    ENV_OK(satenv_step_autoreset(env, d_pa + (size_t)t * N * 3, d_ea + (size_t)t * N * 3, d_obs, d_rew + (size_t)t * N,
+                                 d_done + (size_t)t * N, d_stats, st));
+  HIP_OK(hipStreamSynchronize(st));
+  save(out, "env_pa.f32", pa);
+  save(out, "env_ea.f32", ea);
+  save(out, "env_obs.f32", host(d_obs, (size_t)N * 18));
+  save(out, "env_rew.f32", host(d_rew, (size_t)T * N));
+  save(out, "env_done.u8", host(d_done, (size_t)T * N));
+  save(out, "env_stats.f64", host(d_stats, 4));
+  ENV_OK(satenv_destroy(env));
+
+  // ---- one PPO minibatch step, H = 256: the bench's minibatch and configs[3]'s per-rank one
+  ppo_step(out, 4096, st);
+  ppo_step(out, 512, st);
+  std::printf("c_host_step: %lld envs x %d autoreset steps\n", (long long)N, T);
   return 0;
 }

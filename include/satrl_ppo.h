@@ -50,37 +50,14 @@ int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
  * two streams (each with its own nsq buffer).                              */
 
 /* dW2 = dZ2^T H1 per net (the fc2 weight gradient) split-K S ways into the
- * slabs p2 [2][S][H][H] (f32 MFMA, fixed summation order).  S must be
- * satrl_ppo_dw2_splits(H, mb) (about one workgroup per CU, no empty split). */
+ * slabs p2 [2][S][H][H] (f32 MFMA, fixed summation order) from the f32 rows
+ * satrl_ppo_rowpass writes, at every width.  S must be
+ * satrl_ppo_dw2_splits(H, mb) (about one workgroup per CU, no empty split).
+ * The product paths: H = 64 / 128 fuse the product into the rowpass
+ * (satrl_ppo_rowpass_dw2), H = 256 runs it from k-packed planes
+ * (satrl_ppo_rowpass_kx + satrl_ppo_dw2_kx).                              */
 int satrl_ppo_dw2_splits(int H, int mb);
 int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream);
-
-/* The same slabs through hipBLASLt (the H = 256 path): one strided-batched
- * f32 matmul over nets x S splits, mb % S == 0.  The solution is tuned when
- * the plan is made (the fastest that repeats its output bit for bit; the
- * library heuristic's choice when within 15 % of it).
- * H1 / dZ2 / p2 point at the first selected net's block (net 1 alone: the
- * critic's).  _workspace builds and caches the plan for
- * (H, mb, S, nets) -- call it outside stream capture -- and reports the
- * workspace bytes satrl_ppo_dw2_lib needs and the solution index chosen.  */
-int satrl_ppo_dw2_lib_workspace(int H, int mb, int net, int S, int64_t* ws_bytes, int* algo_index);
-int satrl_ppo_dw2_lib(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* workspace,
-                      int64_t ws_bytes, void* stream);
-/* Reproducible plans: _pin makes (or remakes, outside capture) the plan of
- * (H, mb, S, nets) with solution `algo_index`; `kernel` (nullable) must be
- * that solution's kernel name in the loaded hipBLASLt (an index names another
- * solution in another library build): -3 when it is unsupported or differs.
- * _plan_info reports a made plan's solution index and kernel name.  The
- * Python host pins every shape from a committed table (satrl/dw2_plans.json)
- * and, under data parallelism, to rank 0's choice, so every rank and every
- * run sums dW2 with the same tiles.                                        */
-int satrl_ppo_dw2_lib_pin(int H, int mb, int net, int S, int algo_index, const char* kernel);
-int satrl_ppo_dw2_lib_plan_info(int H, int mb, int net, int S, int* algo_index, char* kernel, int kernel_len);
-/* Plan tooling (tools/dw2_pin.py): up to `cap` solutions of the shape that
- * repeat their output bit for bit, fastest first by back-to-back time on
- * scratch slabs (us, nullable); returns how many (< 0 on error).  Outside
- * capture: it allocates and synchronises.                                  */
-int satrl_ppo_dw2_lib_candidates(int H, int mb, int net, int S, int* algo_index, float* us, int cap);
 
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
@@ -151,8 +128,8 @@ int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_
                           const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
                           float* pw1, void* stream);
 
-/* H = 256, mb above the short-minibatch threshold (1024): the rowpass with
- * H1 and dZ2 written as k-packed bf16 planes (each element split hi + mid +
+/* H = 256, every minibatch (32-row workgroups above 1024 rows, 16-row ones
+ * up to it): the rowpass with H1 and dZ2 written as k-packed bf16 planes (each element split hi + mid +
  * lo exactly; element (r, n) of a net's plane at ((r/8)*H + n)*8 + r%8,
  * rows padded with zeros to whole 32-row chunks): u16 H1x / dZ2x
  * [2][3][ceil(mb/32)*32][H], satrl_ppo_kx_elems(H, mb) elements each.

@@ -4,8 +4,8 @@
 //   rowpass  gather, fc1, fc2 (f32 MFMA), output layers, losses, backprop to
 //            dZ2 and through fc2 (f32 MFMA) and fc1's tanh; writes H1, dZ2
 //            and partial slabs of every small gradient
-//   dW2      dZ2^T @ H1 split-K S ways: dw2_kernel (H <= 128), dw2_bf3_kernel (H = 256) or hipBLASLt
-//            (H = 256, dw2_blas.cpp)
+//   dW2      dZ2^T @ H1 split-K S ways: fused into the rowpass (H <= 128, rowpass_dw2), from the
+//            rowpass's k-packed bf16 planes (H = 256, dw2_kx_kernel), or dw2_kernel on f32 rows
 //   reduce   partial slabs -> G (fixed order), per-block squared norms per net
 //   adam     clip coefficient per net + Adam (torch single-tensor formula),
 //            also refreshes fc2.weight^T used by the next rowpass
@@ -713,8 +713,9 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
   // KX: H1 / dZ2 go out as k-packed bf16 planes (store_kx; H1g / dZ2g point at
-  // u16 [2][3][kx_rows(mb)][H]) for satrl_ppo_dw2_kx, whole 32-row chunks
-  static_assert(!KX || (R == 32 && kBf3<H> && !FDW2), "k-packed outputs: 32-row blocks, split-bf16 width");
+  // u16 [2][3][kx_rows(mb)][H]) for satrl_ppo_dw2_kx, whole 32-row chunks (a
+  // 16-row kernel's last block zero-fills the chunk's other half)
+  static_assert(!KX || ((R == 32 || R == kRowsShort) && kBf3<H> && !FDW2), "k-packed outputs: split-bf16 width");
   const int64_t PLX = kx_rows(mb) * H;                             // (KX) plane elements per net
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
@@ -809,7 +810,14 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather,
                                    FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
-  if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
+  if constexpr (KX) {
+    store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
+    if (R < 32 && r0 + R < kx_rows(mb) && r0 + R >= mb) {            // (uniform) the padded chunk's rows past this block
+      const float z[R / 16][CT][4] = {};
+      store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0 + R, n0, z);
+      store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(dZ2g) + net * 3 * PLX, PLX, r0 + R, n0, z);
+    }
+  }
   else if constexpr (BF3 && !FDW2) store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, h1);
   // phase D's first W2T chunks go out now, under the loss head and the tail
   WPre<CT> preD;
@@ -1171,113 +1179,6 @@ __global__ void __launch_bounds__(256) dw2_kernel(int mb, int S, int KR, int net
 }
 
 // ---------------------------------------------------------------------------
-// dW2 at H = 256 on the split-bf16 MFMA (kBf3; the rowpass's fc2 products'
-// arithmetic): the same grid and slabs as dw2_kernel -- workgroup (net,
-// 64x64 output tile, split s), rows [s*KR, (s+1)*KR) -- with each wave on a
-// 32x32 quarter of the tile (2 x 2 tiles of v_mfma_f32_16x16x32_bf16).
-// The reduction index (rows) must be the MFMA's k, so each 32-row chunk is
-// transposed on its way to LDS: thread (column l, row group w) loads eight
-// rows of one column of dZ2 and of H1 (each load instruction 256 contiguous
-// bytes), splits them (split3x8) and writes each plane's 8 bf16 as one 16-B
-// store at [column][k] (80-B rows: the stores and the operand reads are
-// bank-conflict free).  Two LDS buffers: chunk c+1's loads are in flight
-// under chunk c's MFMAs, one barrier per chunk.  Every sum has a fixed order.
-// ---------------------------------------------------------------------------
-template <int H>
-__global__ void __launch_bounds__(256) dw2_bf3_kernel(int mb, int S, int KR, int net_sel,
-                                                      const float* __restrict__ H1g, const float* __restrict__ dZ2g,
-                                                      float* __restrict__ p2) {
-  constexpr int TT = H / 64, LK = 40;                               // plane row: 32 k + 16-B pad
-  __shared__ __attribute__((aligned(16))) unsigned short pl[2][2][3][64][LK];   // [buf][dZ2 | H1][plane][col][k]
-  const int t = threadIdx.x, w = t >> 6, l = t & 63, li = l & 15, lg = l >> 4;
-  const int b = blockIdx.x, s = b % S, tile = (b / S) % (TT * TT);
-  const int net = net_sel < 0 ? b / (S * TT * TT) : net_sel;
-  const int o0 = (tile / TT) * 64, n0 = (tile % TT) * 64;
-  const int r_begin = s * KR, nvalid = min(mb, r_begin + KR) - r_begin;
-  const float* Z = dZ2g + (int64_t)net * mb * H + o0 + l;
-  const float* Y = H1g + (int64_t)net * mb * H + n0 + l;
-  const int nchunks = (nvalid + 31) / 32;
-  // two register slots of staged rows: chunk c+2's loads go out while chunk
-  // c's MFMAs run and chunk c+1 is split into the other LDS buffer
-  float za[2][8], ya[2][8];
-  auto load = [&](int c, float (&zr)[8], float (&yr)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int r = min(r_begin + 32 * c + 8 * w + j, mb - 1);      // rows past the end: zeroed in put
-      zr[j] = Z[(int64_t)r * H];
-      yr[j] = Y[(int64_t)r * H];
-    }
-  };
-  auto put = [&](int c, int buf, float (&zr)[8], float (&yr)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (32 * c + 8 * w + j >= nvalid) { zr[j] = 0.0f; yr[j] = 0.0f; }
-    s8v zp[3], yp[3];
-    const float4 zf[2] = {make_float4(zr[0], zr[1], zr[2], zr[3]), make_float4(zr[4], zr[5], zr[6], zr[7])};
-    const float4 yf[2] = {make_float4(yr[0], yr[1], yr[2], yr[3]), make_float4(yr[4], yr[5], yr[6], yr[7])};
-    split3x8(zf, zp);
-    split3x8(yf, yp);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      *reinterpret_cast<s8v*>(&pl[buf][0][p][l][8 * w]) = zp[p];
-      *reinterpret_cast<s8v*>(&pl[buf][1][p][l][8 * w]) = yp[p];
-    }
-  };
-  const int wo = w >> 1, wn = w & 1;
-  f4 acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = f4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](int buf) {
-    s8v a[2][3], bq[2][3];
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        a[x][p] = *reinterpret_cast<const s8v*>(&pl[buf][0][p][32 * wo + 16 * x + li][8 * lg]);
-        bq[x][p] = *reinterpret_cast<const s8v*>(&pl[buf][1][p][32 * wn + 16 * x + li][8 * lg]);
-      }
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y) {
-        acc[x][y] = mfma_bf16(a[x][2], bq[y][0], acc[x][y]);
-        acc[x][y] = mfma_bf16(a[x][0], bq[y][2], acc[x][y]);
-        acc[x][y] = mfma_bf16(a[x][1], bq[y][1], acc[x][y]);
-        acc[x][y] = mfma_bf16(a[x][1], bq[y][0], acc[x][y]);
-        acc[x][y] = mfma_bf16(a[x][0], bq[y][1], acc[x][y]);
-        acc[x][y] = mfma_bf16(a[x][0], bq[y][0], acc[x][y]);
-      }
-  };
-  load(0, za[0], ya[0]);
-  if (nchunks > 1) load(1, za[1], ya[1]);
-  put(0, 0, za[0], ya[0]);
-  __syncthreads();
-  // chunk c (even) in LDS buffer 0, its successor in slot 1; slots swap per chunk
-  for (int c = 0; c < nchunks; c += 2) {
-    if (c + 2 < nchunks) load(c + 2, za[0], ya[0]);
-    mma(0);
-    if (c + 1 < nchunks) put(c + 1, 1, za[1], ya[1]);
-    __syncthreads();
-    if (c + 1 >= nchunks) break;
-    if (c + 3 < nchunks) load(c + 3, za[1], ya[1]);
-    mma(1);
-    if (c + 2 < nchunks) put(c + 2, 0, za[0], ya[0]);
-    __syncthreads();
-  }
-  // acc[x][y][q] = dW2[o0 + 32wo + 16x + 4lg + q][n0 + 32wn + 16y + li]
-  float* out = p2 + ((int64_t)net * S + s) * H * H;
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        out[(int64_t)(o0 + 32 * wo + 16 * x + 4 * lg + q) * H + n0 + 32 * wn + 16 * y + li] = acc[x][y][q];
-}
-
-// ---------------------------------------------------------------------------
 // dW2 at H = 256 from k-packed bf16 planes (satrl_ppo_dw2_kx): the rowpass
 // wrote H1 and dZ2 already split and laid out so that the reduction index
 // (rows) runs along each 16-B run (store_kx), so no transpose, no split and
@@ -1371,10 +1272,9 @@ int kx_splits(int mb, int net, int target = kKxWgs) {
   return (nch + cps - 1) / cps;
 }
 
-constexpr int kDw3Wgs = 512;      // dw2_bf3_kernel workgroups to aim for (splits = this / tiles; 256 / 1024 slower)
 int dw2_splits(int H, int mb, int net) {
   const int tiles = (net < 0 ? 2 : 1) * (H / 64) * (H / 64);
-  int S = (H == 256 ? kDw3Wgs : 256) / tiles;
+  int S = 256 / tiles;
   const int maxS = (mb + kDwKC - 1) / kDwKC;
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
@@ -1394,6 +1294,7 @@ int dw2_splits(int H, int mb, int net) {
 // first add (one latency round), then chunk 0 adds the CH partials in order.
 // ---------------------------------------------------------------------------
 struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
+__host__ __device__ inline int n_blocks_dev(const RedGeom& g) { return g.nb2 + g.nb1 + g.nbt; }
 constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;   // chunks per column: W1, tail, W2 regions
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
@@ -1776,14 +1677,10 @@ __global__ void __launch_bounds__(256) tanh_kernel(int64_t n, const float* __res
 }
 
 // rows per rowpass workgroup for a minibatch of mb rows: kRowsShort at
-// H = 256 up to kShortMb rows (SATRL_RP_SHORT_MB, dev A/B; 0 turns it off)
-int short_mb() {
-  static const int v = [] {
-    const char* e = std::getenv("SATRL_RP_SHORT_MB");
-    return e ? std::atoi(e) : 1024;
-  }();
-  return v;
-}
+// H = 256 up to kShortMb rows (twice the workgroups on the chip; measured
+// faster up to mb 1024, even at 2048, slower at 4096: DESIGN.md §3.4)
+constexpr int kShortMb = 1024;
+int short_mb() { return kShortMb; }
 int rows_per_wg(int H, int mb) {
   return (H == 256 && kRows == 32 && mb <= short_mb()) ? kRowsShort : kRows;
 }
@@ -1843,12 +1740,17 @@ bool valid_h(int H) { return H == 64 || H == 128 || H == 256; }
 // Each slice is summed once, in rank order, then broadcast, so every rank
 // gets identical bits (and, at W = 2, the bits of c10d's SUM / 2).  Phase
 // 3 hands out G exactly as reduce_kernel's blocks do (a float4 per lead
-// thread), so nsq is bitwise reduce_dp's.  The tag is the call count: block
-// b keeps its own counter in this rank's buffer and every call advances
-// every counter once, on every rank.  Waits are bounded (0.5 s of
-// s_memrealtime): a peer that never pushes sets the error word instead of
-// hanging the GPU.  Every block of every rank must be resident at once
-// (the grid is reduce_kernel's, a few blocks per CU).
+// thread of each of reduce_dp's blocks), so nsq is bitwise reduce_dp's.
+// The grid is at most one workgroup per CU (satrl_ppo_allreduce_peer checks
+// that every block is resident): a block takes reduce_dp's blocks
+// blockIdx.x, + gridDim.x, ... in turn, so its spinning waves leave every CU
+// room for the kernels of other streams or of a rank sharing the device.
+// The tag is the call count: block b keeps its own counter in this rank's
+// buffer and every call advances every counter once, on every rank (the
+// grid size must be the same on every rank).  Waits are bounded (the
+// caller's deadline in s_memrealtime ticks): a peer that never pushes sets
+// the error word instead of hanging the GPU; satrl_peer_reset re-arms the
+// counters and the word once every rank has stopped.
 // ---------------------------------------------------------------------------
 constexpr int kPeerMaxW = 8, kPeerMaxBlocks = 1024;
 constexpr int64_t kPeerHdr = 4 * kPeerMaxBlocks + 256;           // epoch counters, error word
@@ -1867,26 +1769,39 @@ __device__ __forceinline__ void peer_push(unsigned long long* base, int64_t word
   __hip_atomic_store((gu64*)(base) + word, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// the value of a granule once its tag is `tag` (bounded wait)
+// the value of a granule once its tag is `tag` (bounded wait: once a wait of
+// this thread has run out, the rest return at once, the call being invalid)
 __device__ __forceinline__ float peer_pull(const unsigned long long* base, int64_t word, unsigned tag,
-                                           unsigned long long t0, bool& ok) {
+                                           unsigned long long t0, unsigned long long ticks, bool& ok) {
   const gu64* g = (const gu64*)(base) + word;
   unsigned long long x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  while ((unsigned)(x >> 32) != tag) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) { ok = false; break; }   // 0.5 s at 100 MHz
+  while (ok && (unsigned)(x >> 32) != tag) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { ok = false; break; }   // 100 MHz ticks
     __builtin_amdgcn_s_sleep(1);
     x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   return __uint_as_float((unsigned)x);
 }
 
+// the float4 of G reduce_dp's block rb hands thread t (its lead threads), or -1
+__device__ __forceinline__ int64_t peer_col(const Layout& L, const RedGeom& g, int H, int rb, int t) {
+  if (rb < g.nb2) return t < 256 / kRedCH2 ? (int64_t)rb * (256 / kRedCH2) + t : -1;
+  if (rb < g.nb2 + g.nb1) {
+    const int64_t c = (int64_t)(rb - g.nb2) * (256 / kRedCH1) + t;
+    return t < 256 / kRedCH1 && c < 2LL * H * 20 / 4 ? L.W1 / 4 + c : -1;
+  }
+  const int64_t c = (int64_t)(rb - g.nb2 - g.nb1) * (256 / kRedCHt) + t;
+  return t < 256 / kRedCHt && c < L.tail / 4 ? L.b2 / 4 + c : -1;
+}
+
 __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, int world, int rank, PeerBufs pb,
                                                              float* __restrict__ G, double* __restrict__ nsq,
-                                                             double* __restrict__ steps) {
+                                                             double* __restrict__ steps,
+                                                             unsigned long long ticks) {
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ unsigned tag_s;
-  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+  const int t = threadIdx.x, b = blockIdx.x, nb = gridDim.x, nred = n_blocks_dev(g);
   const int64_t n = L.total, sl = peer_slice(n, world);
   unsigned long long* mine = pb.buf[rank];
   const int64_t rs = kPeerHdr / 8, ag = rs + (int64_t)world * sl;  // word offsets of the two slot arrays
@@ -1902,61 +1817,58 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
   if (b == 0 && t == 0) { st0 = steps[0]; st1 = steps[1]; }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   bool ok = true;
-  // this thread's float4 of G, as reduce_kernel hands them out (lead threads)
-  int64_t col = -1;
-  if (b < g.nb2) {
-    if (t < 256 / kRedCH2) col = (int64_t)b * (256 / kRedCH2) + t;
-  } else if (b < g.nb2 + g.nb1) {
-    const int64_t c = (int64_t)(b - g.nb2) * (256 / kRedCH1) + t;
-    if (t < 256 / kRedCH1 && c < 2LL * H * 20 / 4) col = L.W1 / 4 + c;
-  } else {
-    const int64_t c = (int64_t)(b - g.nb2 - g.nb1) * (256 / kRedCHt) + t;
-    if (t < 256 / kRedCHt && c < L.tail / 4) col = L.b2 / 4 + c;
-  }
-  // 1: push this float4 to the owners' reduce-scatter slot [rank]
-  if (col >= 0) {
-    const float4 v = reinterpret_cast<const float4*>(G)[col];
-    const float e4[4] = {v.x, v.y, v.z, v.w};
+  // 1: push this thread's float4 of each of the block's reduce_dp blocks to
+  // the owners' reduce-scatter slot [rank]
+  for (int rb = b; rb < nred; rb += nb) {
+    const int64_t col = peer_col(L, g, H, rb, t);
+    if (col >= 0) {
+      const float4 v = reinterpret_cast<const float4*>(G)[col];
+      const float e4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t e = col * 4 + q, j = e / sl;
-      peer_push(pb.buf[j], rs + (int64_t)rank * sl + (e - j * sl), tag, e4[q]);
+      for (int q = 0; q < 4; ++q) {
+        const int64_t e = col * 4 + q, j = e / sl;
+        peer_push(pb.buf[j], rs + (int64_t)rank * sl + (e - j * sl), tag, e4[q]);
+      }
     }
   }
   // 2: this rank's slice, summed in rank order, / world, to every gather slot [rank]
   const int64_t mylen = min(sl, n - (int64_t)rank * sl);
   for (int64_t k = (int64_t)b * 256 + t; k < mylen; k += (int64_t)nb * 256) {
-    float v = peer_pull(mine, rs + k, tag, t0, ok);
-    for (int j = 1; j < world; ++j) v += peer_pull(mine, rs + (int64_t)j * sl + k, tag, t0, ok);
+    float v = peer_pull(mine, rs + k, tag, t0, ticks, ok);
+    for (int j = 1; j < world; ++j) v += peer_pull(mine, rs + (int64_t)j * sl + k, tag, t0, ticks, ok);
     v = v / (float)world;                                         // G.div_(world) (reduce_dp's IEEE division)
     for (int j = 0; j < world; ++j) peer_push(pb.buf[j], ag + (int64_t)rank * sl + k, tag, v);
   }
-  // 3: gather this float4 into G; its squares to the block's norm pair
-  double sa = 0.0, sc = 0.0;
-  if (col >= 0) {
-    float e4[4];
+  // 3: gather each float4 into G; its squares to that reduce_dp block's norm pair
+  for (int rb = b; rb < nred; rb += nb) {
+    const int64_t col = peer_col(L, g, H, rb, t);
+    double sa = 0.0, sc = 0.0;
+    if (col >= 0) {
+      float e4[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t e = col * 4 + q, j = e / sl;
-      e4[q] = peer_pull(mine, ag + j * sl + (e - j * sl), tag, t0, ok);
+      for (int q = 0; q < 4; ++q) {
+        const int64_t e = col * 4 + q, j = e / sl;
+        e4[q] = peer_pull(mine, ag + j * sl + (e - j * sl), tag, t0, ticks, ok);
+      }
+      const float4 v = make_float4(e4[0], e4[1], e4[2], e4[3]);
+      reinterpret_cast<float4*>(G)[col] = v;
+      const double q = sq4(v);
+      const bool crit = net_of(L, col * 4, H);
+      sa += crit ? 0.0 : q;
+      sc += crit ? q : 0.0;
     }
-    const float4 v = make_float4(e4[0], e4[1], e4[2], e4[3]);
-    reinterpret_cast<float4*>(G)[col] = v;
-    const double q = sq4(v);
-    const bool crit = net_of(L, col * 4, H);
-    sa += crit ? 0.0 : q;
-    sc += crit ? q : 0.0;
+    block_sum2(sa, sc, sh);
+    if (t == 0) {
+      nsq[2 * rb] = sa;
+      nsq[2 * rb + 1] = sc;
+    }
+    __syncthreads();                                               // sh is reused by the next block_sum2
   }
   if (!ok) {                                                       // a peer never pushed: flag it
     gu64* err = (gu64*)(mine) + (4 * kPeerMaxBlocks) / 8;
     __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  block_sum2(sa, sc, sh);
-  if (t == 0) {
-    nsq[2 * b] = sa;
-    nsq[2 * b + 1] = sc;
-    if (b == 0) { steps[0] = st0 + 1.0; steps[1] = st1 + 1.0; }
-  }
+  if (b == 0 && t == 0) { steps[0] = st0 + 1.0; steps[1] = st1 + 1.0; }
 }
 
 }  // namespace
@@ -2004,6 +1916,8 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
     hipLaunchKernelGGL((rowpass_kernel<128, 8, kRows, true>), g, dim3(512), 0, s, RP_ARGS);
   else if (H == 128)
     hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, RP_ARGS);
+  else if (kx && R == kRowsShort)
+    hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort, false, true>), g, dim3(16 * 64), 0, s, RP_ARGS);
   else if (kx)
     hipLaunchKernelGGL((rowpass_kernel<256, kNW256, kRows, false, true>), g, dim3(kNW256 * 64), 0, s, RP_ARGS);
   else if (R == kRowsShort)
@@ -2056,7 +1970,7 @@ int64_t satrl_ppo_kx_elems(int H, int mb) {
 int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
                          float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, float* ptail,
                          float* pw1, void* stream) {
-  if (H != 256 || mb <= short_mb() || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !H1x || !dZ2x ||
+  if (H != 256 || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !H1x || !dZ2x ||
       !ptail || !pw1)
     return -1;
   return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, static_cast<float*>(H1x),
@@ -2095,7 +2009,7 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
   else if (H == 128)
     hipLaunchKernelGGL(dw2_kernel<128>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
   else
-    hipLaunchKernelGGL(dw2_bf3_kernel<256>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
+    hipLaunchKernelGGL(dw2_kernel<256>, g, dim3(256), 0, st, mb, S, KR, net, H1, dZ2, p2);
   LAUNCH_CHECK();
   return 0;
 }
@@ -2160,28 +2074,65 @@ int satrl_peer_open(const void* ipc_handle, void** buf) {
 int satrl_peer_close(void* buf) { return buf && hipIpcCloseMemHandle(buf) == hipSuccess ? 0 : -2; }
 int satrl_peer_free(void* buf) { return buf && hipFree(buf) == hipSuccess ? 0 : -2; }
 
-int satrl_peer_error(const void* buf, uint64_t* err) {
+int satrl_peer_error(const void* buf, uint64_t* err, void* stream) {
   if (!buf || !err) return -1;
-  return hipMemcpy(err, static_cast<const char*>(buf) + 4 * kPeerMaxBlocks, 8, hipMemcpyDeviceToHost) == hipSuccess
+  hipStream_t st = (hipStream_t)stream;               // ordered after the calls queued on `stream`
+  return hipMemcpyAsync(err, static_cast<const char*>(buf) + 4 * kPeerMaxBlocks, 8, hipMemcpyDeviceToHost, st) ==
+                     hipSuccess &&
+                 hipStreamSynchronize(st) == hipSuccess
              ? 0
              : -2;
 }
 
+int satrl_peer_reset(void* buf, int64_t bytes, void* stream) {
+  if (!buf || bytes < kPeerHdr) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  return hipMemsetAsync(buf, 0, (size_t)bytes, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess ? 0 : -2;
+}
+
+// the peer kernel's grid at width H: reduce_dp's block count, capped at one
+// block per CU of the current device and at what can be resident at once
+int satrl_peer_blocks(int H, int* blocks) {
+  if (!valid_h(H) || !blocks) return -1;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, peer_allreduce_kernel, 256, 0) != hipSuccess) {
+    g_err = "satrl_peer_blocks: device query failed";
+    return -2;
+  }
+  const int nb = n_blocks(geom(H, 1, 1, -1));
+  *blocks = std::min(nb, std::min(cus, cus * per_cu));
+  return *blocks > 0 ? 0 : -2;
+}
+
 int satrl_ppo_allreduce_peer(int H, int mb, int world, int rank, void* const* bufs, float* G, double* nsq,
-                             double* steps, void* stream) {
+                             double* steps, int blocks, double timeout_s, void* stream) {
   if (!valid_h(H) || mb <= 0 || world < 1 || world > kPeerMaxW || rank < 0 || rank >= world || !bufs || !G || !nsq ||
-      !steps)
+      !steps || blocks < 1 || blocks > kPeerMaxBlocks || !(timeout_s > 0.0) || timeout_s > 1e7)
     return -1;
   PeerBufs pb{};
   for (int j = 0; j < world; ++j) {
     if (!bufs[j]) return -1;
     pb.buf[j] = static_cast<unsigned long long*>(bufs[j]);
   }
+  // every block must be resident at once (a block waits on values other blocks push)
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, peer_allreduce_kernel, 256, 0) != hipSuccess) {
+    g_err = "satrl_ppo_allreduce_peer: device query failed";
+    return -2;
+  }
+  if (blocks > cus * per_cu) {
+    g_err = "satrl_ppo_allreduce_peer: " + std::to_string(blocks) + " blocks cannot all be resident (" +
+            std::to_string(cus) + " CUs x " + std::to_string(per_cu) + ")";
+    return -1;
+  }
   const RedGeom g = geom(H, mb, 1, -1);
-  const int nb = n_blocks(g);
-  if (nb > kPeerMaxBlocks) return -1;
-  hipLaunchKernelGGL(peer_allreduce_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, H, g, world, rank, pb, G, nsq,
-                     steps);
+  const unsigned long long ticks = (unsigned long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(peer_allreduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, g, world, rank, pb, G,
+                     nsq, steps, ticks);
   LAUNCH_CHECK();
   return 0;
 }
@@ -2278,8 +2229,6 @@ const char* satrl_ppo_last_error(void) { return g_err.c_str(); }
 
 }  // extern "C"
 
-// (dw2_blas.cpp reports through satrl_ppo_last_error too)
-void satrl_ppo_set_error(const char* msg) { g_err = msg; }
 
 #ifdef SATRL_PHASE_PROBE
 extern "C" int satrl_probe_read(unsigned long long* out) {

@@ -107,11 +107,6 @@ _SIGS = {
     "satrl_ppo_sizes": ([C.c_int, C.c_int, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
     "satrl_ppo_dw2_splits": ([C.c_int, C.c_int], C.c_int),
     "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_dw2_lib_workspace": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp], C.c_int),
-    "satrl_ppo_dw2_lib": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_int64, _vp], C.c_int),
-    "satrl_ppo_dw2_lib_pin": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p], C.c_int),
-    "satrl_ppo_dw2_lib_plan_info": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.c_char_p, C.c_int], C.c_int),
-    "satrl_ppo_dw2_lib_candidates": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, C.c_int], C.c_int),
     "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
@@ -135,8 +130,11 @@ _SIGS = {
     "satrl_peer_open": ([_vp, _vp], C.c_int),
     "satrl_peer_close": ([_vp], C.c_int),
     "satrl_peer_free": ([_vp], C.c_int),
-    "satrl_peer_error": ([_vp, _vp], C.c_int),
-    "satrl_ppo_allreduce_peer": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_peer_error": ([_vp, _vp, _vp], C.c_int),
+    "satrl_peer_reset": ([_vp, _i64, _vp], C.c_int),
+    "satrl_peer_blocks": ([C.c_int, _vp], C.c_int),
+    "satrl_ppo_allreduce_peer": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_int, C.c_double,
+                                  _vp], C.c_int),
     "satrl_policy_act": ([C.c_int, _i64, _vp, _vp, _vp, C.c_float, C.c_uint64, _i64, C.c_uint64, _vp, _vp, _vp, _vp,
                           _vp, _vp], C.c_int),
     "satrl_policy_value": ([C.c_int, _i64, _vp, _vp, _vp, _vp], C.c_int),

@@ -11,14 +11,23 @@ the result to every rank, so every rank holds identical bits; it then writes
 reduce_dp's squared-norm partials and advances the step counters.  It holds
 no host state between calls, so it lives inside the update's hipGraphs like
 the kernels around it.
+
+Its grid is at most one workgroup per CU (satrl_peer_blocks, the minimum
+over the ranks so every rank launches the same grid), and every wait for a
+peer's value is bounded by the data-parallel timeout (SATRL_DP_TIMEOUT_S):
+a rank that stops makes the others' calls give up and set an error word,
+which ``check`` reads between graph replays (FusedMinibatch.run) and after
+the update.  ``reset`` re-arms every rank's buffer after a barrier.
 """
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import torch
 
 from . import _lib
+from . import dist as _dist
 from ._lib import check, ptr, stream_ptr
 
 HANDLE_BYTES = 64            # SATRL_PEER_HANDLE_BYTES
@@ -29,12 +38,24 @@ class PeerError(RuntimeError):
     """A peer's value never arrived within the kernel's bounded wait."""
 
 
+def _release(lib, opened, own):
+    """Unmap the peers' buffers and free this rank's (PeerComm.close and the
+    finalizer of a PeerComm that was never closed)."""
+    for p in opened:
+        lib.satrl_peer_close(p)
+    opened.clear()
+    if own.value:
+        lib.satrl_peer_free(own)
+        own.value = None
+
+
 class PeerComm:
     """Exchange buffers of `n`-float all-reduces over the ranks of `pg` (an
     initialised torch.distributed group; its backend only carries the IPC
-    handles).  Every rank constructs it with the same n, in the same order."""
+    handles).  Every rank constructs it with the same n and H, in the same
+    order."""
 
-    def __init__(self, pg, n, device):
+    def __init__(self, pg, n, device, H, timeout_s=None):
         import torch.distributed as dist
         self.pg = pg
         self.world = dist.get_world_size(pg)
@@ -42,21 +63,26 @@ class PeerComm:
         if not 1 <= self.world <= MAX_WORLD:
             raise ValueError(f"peer all-reduce supports 1..{MAX_WORLD} ranks, got {self.world}")
         self.device = torch.device(device)
+        self.timeout_s = float(_dist.dp_timeout_s() if timeout_s is None else timeout_s)
         lib = _lib.lib()
         nbytes = C.c_int64()
         check(lib.satrl_peer_buffer_bytes(int(n), self.world, C.byref(nbytes)), "satrl_peer_buffer_bytes")
-        self.n = int(n)
+        self.n, self.nbytes = int(n), nbytes.value
         own = C.c_void_p()
         handle = (C.c_ubyte * HANDLE_BYTES)()
+        blocks = C.c_int()
         with torch.cuda.device(self.device):
-            check(lib.satrl_peer_alloc(nbytes.value, C.byref(own), handle), "satrl_peer_alloc")
+            check(lib.satrl_peer_blocks(int(H), C.byref(blocks)), "satrl_peer_blocks")
+            check(lib.satrl_peer_alloc(self.nbytes, C.byref(own), handle), "satrl_peer_alloc")
         self._own = own
-        handles = [None] * self.world
-        dist.all_gather_object(handles, bytes(handle), group=pg)
         self._opened = []
+        self._fin = weakref.finalize(self, _release, lib, self._opened, own)
+        gathered = [None] * self.world
+        dist.all_gather_object(gathered, (bytes(handle), blocks.value), group=pg)
+        self.blocks = min(b for _, b in gathered)            # the same grid on every rank
         ptrs = []
         with torch.cuda.device(self.device):
-            for r, h in enumerate(handles):
+            for r, (h, _) in enumerate(gathered):
                 if r == self.rank:
                     ptrs.append(own.value)
                     continue
@@ -72,24 +98,29 @@ class PeerComm:
         """G <- (sum over ranks) / world, identical on every rank, and
         reduce_dp's norm partials / step counters (satrl_ppo_allreduce_peer),
         on the current stream (capturable)."""
-        check(_lib.lib().satrl_ppo_allreduce_peer(int(H), int(mb), self.world, self.rank, C.cast(self.bufs, C.c_void_p), ptr(G),
-                                                  ptr(nsq), ptr(steps), stream_ptr()), "satrl_ppo_allreduce_peer")
+        check(_lib.lib().satrl_ppo_allreduce_peer(int(H), int(mb), self.world, self.rank, C.cast(self.bufs, C.c_void_p),
+                                                  ptr(G), ptr(nsq), ptr(steps), self.blocks, self.timeout_s,
+                                                  stream_ptr()), "satrl_ppo_allreduce_peer")
         return G
 
     def error(self) -> int:
+        """The sticky error word, after the work queued on the current stream."""
         err = C.c_uint64()
-        check(_lib.lib().satrl_peer_error(self._own, C.byref(err)), "satrl_peer_error")
+        check(_lib.lib().satrl_peer_error(self._own, C.byref(err), stream_ptr()), "satrl_peer_error")
         return int(err.value)
 
     def check(self):
         if self.error():
-            raise PeerError("peer all-reduce: a peer's granule never arrived (a rank stalled or died)")
+            raise PeerError("peer all-reduce: a peer's granule never arrived within "
+                            f"{self.timeout_s:g} s (a rank stalled or died); PeerComm.reset re-arms the buffers")
+
+    def reset(self):
+        """Re-arm after a failure: every rank zeroes its own buffer (counters,
+        slots, error word), then all meet at a barrier (a collective call)."""
+        import torch.distributed as dist
+        torch.cuda.synchronize(self.device)
+        check(_lib.lib().satrl_peer_reset(self._own, self.nbytes, stream_ptr()), "satrl_peer_reset")
+        dist.barrier(group=self.pg)
 
     def close(self):
-        lib = _lib.lib()
-        for p in self._opened:
-            lib.satrl_peer_close(p)
-        self._opened = []
-        if self._own:
-            lib.satrl_peer_free(self._own)
-            self._own = C.c_void_p()
+        self._fin()

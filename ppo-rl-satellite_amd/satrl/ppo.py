@@ -177,13 +177,6 @@ def ppo_layout(H):
     return dict(zip(OFF_NAMES, [int(v) for v in off]))
 
 
-def _short_mb():
-    """Minibatch rows up to which H = 256 runs the 16-row rowpass (the
-    library's SATRL_RP_SHORT_MB threshold, default 1024)."""
-    v = os.environ.get("SATRL_RP_SHORT_MB")
-    return int(v) if v is not None else 1024
-
-
 def w2x_floats(H):
     """f32 elements of the fc2 operand image (satrl_ppo_w2x_floats)."""
     n = int(_lib.lib().satrl_ppo_w2x_floats(int(H)))
@@ -192,98 +185,15 @@ def w2x_floats(H):
     return n
 
 
-def _split3(x):
-    """x (f32) = hi + mid + lo exactly, each round-to-nearest bf16 (as int16 bits)."""
-    hi = x.to(torch.bfloat16)
-    r = x - hi.float()
-    mid = r.to(torch.bfloat16)
-    lo = (r - mid.float()).to(torch.bfloat16)
-    return [t.view(torch.int16) for t in (hi, mid, lo)]
-
-
-def w2x_presplit(H):
-    """True when the library's fc2 operand image at this width is the bf16
-    planes image (its kW2Pre build), else the f32 fc2.weight^T."""
-    return w2x_floats(H) == 6 * H * H
-
-
-def w2x_image(W2, H, presplit=None):
+def w2x_image(W2, H):
     """Host statement of satrl_ppo_w2x_sync: the fc2 operand image of the two
-    nets' fc2.weight W2 (flat [2*H*H] f32), as the f32 tensor the kernels read
-    (presplit None: the loaded library's format)."""
-    W2 = W2.reshape(2, H, H)
-    if presplit is None:
-        presplit = w2x_presplit(H)
-    if not presplit:
-        return W2.transpose(1, 2).contiguous().reshape(-1)
-    planes = [torch.stack(_split3(w.contiguous())) for n in range(2) for w in (W2[n], W2[n].t())]
-    return torch.stack(planes).reshape(-1).view(torch.float32).clone()
+    nets' fc2.weight W2 (flat [2*H*H] f32), the f32 fc2.weight^T per net."""
+    return W2.reshape(2, H, H).transpose(1, 2).contiguous().reshape(-1)
 
 
 def w2x_decode(img, H):
     """fc2.weight^T per net [2, H, H] f32 from an operand image."""
-    if img.numel() == 2 * H * H:
-        return img.view(2, H, H)
-    p = img.view(torch.int16).view(2, 2, 3, H, H).view(torch.bfloat16).float()
-    return (p[:, 1, 0] + p[:, 1, 1]) + p[:, 1, 2]
-
-
-DW2_PLANS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dw2_plans.json")
-_dw2_table = None
-
-
-def dw2_plan_table():
-    """{(H, mb, S, nets): (solution index, kernel name)} of the committed
-    table (SATRL_DW2_PLANS overrides the path; "none" disables it)."""
-    global _dw2_table
-    if _dw2_table is None:
-        import json
-        path = os.environ.get("SATRL_DW2_PLANS", DW2_PLANS)
-        _dw2_table = {}
-        if path != "none" and os.path.exists(path):
-            with open(path) as f:
-                for e in json.load(f)["plans"]:
-                    _dw2_table[(e["H"], e["mb"], e["S"], e["nets"])] = (int(e["index"]), e["kernel"])
-    return _dw2_table
-
-
-def dw2_plan_info(H, mb, net, S):
-    """(solution index, kernel name) of a made dW2 plan."""
-    idx, name = C.c_int(), C.create_string_buffer(512)
-    check(_lib.lib().satrl_ppo_dw2_lib_plan_info(H, mb, net, S, C.byref(idx), name, 512), "satrl_ppo_dw2_lib_plan_info")
-    return idx.value, name.value.decode()
-
-
-def dw2_pin_plan(H, mb, net, S, pg=None):
-    """Make the hipBLASLt dW2 plan of (H, mb, S, nets) reproducibly and
-    return (solution index, kernel name, source).  Single process: the
-    committed table's solution when it names one for the shape and the
-    loaded library has that kernel ("table"), else the tuner's
-    ("tuned").  Under data parallelism rank 0 decides that way and every
-    rank pins rank 0's solution ("rank0"), so all ranks sum their dW2
-    partials with the same tiles (a collective call: every rank plans the
-    same shapes in the same order)."""
-    lib = _lib.lib()
-    nets = 2 if net < 0 else 1
-    source = None
-    if _dist.world_size(pg) == 1 or _dist.rank(pg) == 0:
-        hit = dw2_plan_table().get((H, mb, S, nets))
-        if hit is not None and lib.satrl_ppo_dw2_lib_pin(H, mb, net, S, hit[0], hit[1].encode()) == 0:
-            source = "table"
-        else:
-            wsb, idx = C.c_int64(), C.c_int()
-            check(lib.satrl_ppo_dw2_lib_workspace(H, mb, net, S, C.byref(wsb), C.byref(idx)),
-                  "satrl_ppo_dw2_lib_workspace")
-            source = "tuned"
-        idx, name = dw2_plan_info(H, mb, net, S)
-    else:
-        idx, name = -1, ""
-    if _dist.world_size(pg) > 1:
-        idx, name = _dist.broadcast_object((idx, name), pg)
-        if _dist.rank(pg) != 0:
-            check(lib.satrl_ppo_dw2_lib_pin(H, mb, net, S, idx, name.encode()), "satrl_ppo_dw2_lib_pin")
-            source = "rank0"
-    return idx, name, source
+    return img.view(2, H, H)
 
 
 class FusedMinibatch:
@@ -298,63 +208,46 @@ class FusedMinibatch:
     all-reduce.  Groups of ``group`` minibatches are captured into a hipGraph
     and replayed over [group, mb] blocks of a device permutation."""
 
-    def __init__(self, learner, mb, group, use_graph=True, split_chains=False, kx=None):
+    def __init__(self, learner, mb, group, use_graph=True, split_chains=False):
         self.L = learner
         self.mb = int(mb)
         self.group = int(group)
         self.use_graph = use_graph
-        # dW2: the hand-written split-K kernel for H <= 128 (hipBLASLt picks
-        # K-serial tiles there: 12.5 us vs 3 us at H = 64); at H = 256 a
-        # plain library GEMM (satrl_ppo_dw2_lib: hipBLASLt from the C ABI,
-        # split-K 4, 11.7 us; satrl_ppo_dw2's split-bf16 kernel measured 1.5 us
-        # slower per step, its f32 predecessor 3 us; the plan times the
-        # library's solutions per shape, which matters for short splits)
-        self.lib_gemm = learner.H >= 256
-        if os.environ.get("SATRL_DW2_LIB") is not None:             # dev A/B knob
-            self.lib_gemm = os.environ["SATRL_DW2_LIB"] == "1"
+        # dW2 (the fc2 weight gradient dZ2^T H1), hand-written at every width:
         # H = 64 (configs[1]): the rowpass multiplies each block's dW2 partial
         # out of LDS itself (satrl_ppo_rowpass_dw2), bitwise the dw2_kernel's
-        # one-chunk splits, so a minibatch step is three launches instead of four
-        self.fused_dw2 = learner.H == 64 and not self.lib_gemm
-        # H = 256, mb above the short threshold: the rowpass writes H1 / dZ2 as
-        # k-packed bf16 planes and dW2 runs on the split-bf16 MFMA from them
-        # (satrl_ppo_rowpass_kx / satrl_ppo_dw2_kx); shorter minibatches (the
-        # 16-row rowpass) keep the library GEMM
-        if kx is None:
-            kx = os.environ.get("SATRL_DW2_KX", "1") != "0"              # dev A/B knob
-        self.kx_on = bool(kx) and learner.H == 256 and not split_chains
+        # one-chunk splits, so a minibatch step is three launches;
+        # H = 256: the rowpass writes H1 / dZ2 as k-packed bf16 planes and dW2
+        # runs on the split-bf16 MFMA from them (satrl_ppo_rowpass_kx /
+        # satrl_ppo_dw2_kx), for every minibatch size (16-row rowpass blocks up
+        # to 1024 rows: configs[3]'s per-rank minibatch, ragged tails);
+        # H = 128: f32 rows and dw2_kernel (satrl_ppo_dw2)
+        self.fused_dw2 = learner.H == 64
+        self.kx_on = learner.H == 256
         self.kx_elems = 0
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
         self.split = bool(split_chains) and learner.pg is None
-        self.offset_cycles = int(os.environ.get("SATRL_CHAIN_OFFSET", "0"))   # dev knob (split chains)
         H, dev = learner.H, learner.device
         nwg, nblk = C.c_int64(), C.c_int64()
         check(_lib.lib().satrl_ppo_sizes(H, self.mb, C.byref(nwg), C.byref(nblk)), "satrl_ppo_sizes")
         self.nwg, self.nblk = nwg.value, nblk.value
         self.S = self.splits(learner.H, self.mb)
         f32 = dict(dtype=torch.float32, device=dev)
+        # f32 H1 / dZ2 rows: satrl_ppo_rowpass (the roofline's rowpass timing,
+        # tests) and the H = 128 dW2; the H = 256 step hands them over as planes
         self.H1 = torch.empty(2 * self.mb * H, **f32)
         self.dZ2 = torch.empty(2 * self.mb * H, **f32)
-        if self.kx(self.mb):
+        if self.kx_on:
             self.kx_elems = int(_lib.lib().satrl_ppo_kx_elems(H, self.mb))
             self.H1x = torch.empty(self.kx_elems, dtype=torch.int16, device=dev)
             self.dZ2x = torch.empty(self.kx_elems, dtype=torch.int16, device=dev)
         self.ptail = torch.empty(self.nwg * (6 * H + 12), **f32)
         self.pw1 = torch.empty(self.nwg * 2 * H * 20, **f32)
-        # sized for the largest split count any minibatch size can produce
-        # (dw2_splits caps S at 256 / tiles), so a ragged tail minibatch whose
-        # S exceeds the full minibatch's never writes past the slabs
+        # sized for the largest split count any minibatch size can produce, so
+        # a ragged tail minibatch whose S exceeds the full minibatch's never
+        # writes past the slabs
         self.p2 = torch.empty(2 * self.max_splits(H) * H * H, **f32)
-        # hipBLASLt workspaces of the dW2 plans, one per concurrent chain: the
-        # stream-K solutions keep partial tiles in the workspace, so the
-        # actor and critic chains of split mode must never share one
-        self.ws = {}
-        self._ws_retired = []
-        self._ws_for = {}                  # (mb, S, net) -> the workspace its plan was checked against
-        if self.lib_gemm and torch.cuda.is_available() and not self.kx(self.mb):
-            for net in ((0, 1) if self.split else (-1,)):
-                self._ws_for[(self.mb, self.S, net)] = (self._dw2_plan(self.mb, self.S, net),)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
@@ -369,10 +262,9 @@ class FusedMinibatch:
         self.perm_buf = None
         self.grp = torch.zeros(1, dtype=torch.int64, device=dev)
         if learner.pg is not None and _dist.world_size(learner.pg) > 1 and torch.cuda.is_available():
-            # every rank's first step of this shape starts together: the peer
-            # all-reduce waits a bounded 0.5 s for its peers, so a rank still
-            # setting up must not hold the others past that (the library dW2
-            # plan's broadcast used to be this sync point)
+            # every rank's first step of this shape starts together (a rank
+            # still setting up must not run into the peer all-reduce's bounded
+            # wait)
             import torch.distributed as dist
             torch.cuda.synchronize()
             dist.barrier(group=learner.pg)
@@ -394,8 +286,8 @@ class FusedMinibatch:
 
     def kx(self, mb):
         """True when a minibatch of mb rows takes the k-packed split-bf16 dW2
-        path (H = 256, 32-row rowpass blocks)."""
-        return self.kx_on and int(mb) > _short_mb()
+        path (H = 256, every minibatch size)."""
+        return self.kx_on
 
     def rowpass_kx(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass_kx: the rowpass with H1 / dZ2 written as k-packed
@@ -455,14 +347,15 @@ class FusedMinibatch:
 
     def max_splits(self, H):
         """Upper bound of splits(H, mb) over every mb (the p2 capacity)."""
-        if self.lib_gemm:
-            return max(self.S, 4, 8 if self.kx_on else 0)        # (dw2_kx: <= 256 / 32 tiles splits)
         if self.fused_dw2:
             return self.nwg                  # row blocks of the longest minibatch at or below mb
+        if self.kx_on:
+            return max(self.S, 256 // 32)    # (dw2_kx: <= 256 / 32 tiles splits over both nets)
         return max(self.S, 256 // (2 * (H // 64) ** 2))
 
     def splits(self, H, mb):
-        """split-K ways of the dW2 product for a minibatch of mb rows."""
+        """split-K ways of the dW2 product for a minibatch of mb rows (both
+        nets' count: a one-net chain of split mode uses the same)."""
         if self.fused_dw2:
             S = _lib.lib().satrl_ppo_row_blocks(int(H), int(mb))      # one slab per rowpass row block
             if S < 1:
@@ -473,69 +366,15 @@ class FusedMinibatch:
             if S < 1:
                 raise _lib.NativeError(f"satrl_ppo_dw2_kx_splits({H}, {mb}) failed")
             return S
-        if self.lib_gemm:
-            S = int(os.environ.get("SATRL_DW2_SPLITS", "4"))          # dev A/B knob; 4 measured best
-            return S if mb % S == 0 else 1
         S = _lib.lib().satrl_ppo_dw2_splits(int(H), int(mb))
-        if os.environ.get("SATRL_DW2_S"):                               # dev A/B knob
-            S = int(os.environ["SATRL_DW2_S"])
         if S < 1:
             raise _lib.NativeError(f"satrl_ppo_dw2_splits({H}, {mb}) failed")
         return S
 
     def _dw2(self, H1, dZ2, mb, S, net):
-        """dW2 = dZ2^T @ H1 split-K S ways into the slabs p2 [2][S][H][H]."""
-        H = self.L.H
-        if not self.lib_gemm:
-            check(_lib.lib().satrl_ppo_dw2(H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), stream_ptr()),
-                  "satrl_ppo_dw2")
-            return
-        lo = 0 if net < 0 else net
-        hit = self._ws_for.get((mb, S, net))
-        if hit is None:
-            if torch.cuda.is_current_stream_capturing():
-                raise _lib.NativeError(f"dW2 shape (mb {mb}, S {S}) reached graph capture unplanned: "
-                                       "plan it first (FusedMinibatch.plan_shape)")
-            hit = self._ws_for[(mb, S, net)] = (self._dw2_plan(mb, S, net),)
-        ws = hit[0]
-        o = 4 * lo * mb * H                # byte offset of the first selected net's block
-        check(_lib.lib().satrl_ppo_dw2_lib(H, mb, net, S, H1.data_ptr() + o, dZ2.data_ptr() + o,
-                                           self.p2.data_ptr() + 4 * lo * S * H * H,
-                                           None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
-                                           stream_ptr()), "satrl_ppo_dw2_lib")
-
-    def plan_shape(self, mb):
-        """Make the dW2 plan of a minibatch of mb rows (e.g. the epoch's
-        ragged tail) before the update loop, so no plan is tuned between
-        minibatch steps and none inside a capture."""
-        mb = int(mb)
-        if not self.lib_gemm or not torch.cuda.is_available() or self.kx(mb):
-            return
-        S = self.S if mb == self.mb else self.splits(self.L.H, mb)
-        for net in ((0, 1) if self.split else (-1,)):
-            if (mb, S, net) not in self._ws_for:
-                self._ws_for[(mb, S, net)] = (self._dw2_plan(mb, S, net),)
-
-    def _dw2_plan(self, mb, S, net):
-        """Create (or look up) the hipBLASLt plan of a dW2 shape and grow the
-        chain's workspace to its size.  Plans made here, before any capture,
-        keep graph capture free of library set-up.  The solution is
-        reproducible (dw2_pin_plan): the committed table's, else the tuner's,
-        and under data parallelism rank 0's on every rank."""
-        H = self.L.H
-        self.dw2_algo, self.dw2_kernel, self.dw2_source = dw2_pin_plan(H, int(mb), int(net), int(S), self.L.pg)
-        wsb, idx = C.c_int64(), C.c_int()
-        check(_lib.lib().satrl_ppo_dw2_lib_workspace(H, int(mb), int(net), int(S), C.byref(wsb), C.byref(idx)),
-              "satrl_ppo_dw2_lib_workspace")
-        chain = 1 if (self.split and net == 1) else 0
-        ws = self.ws.get(chain)
-        if wsb.value > 0 and (ws is None or ws.numel() < wsb.value):
-            if torch.cuda.is_current_stream_capturing():
-                raise _lib.NativeError("dW2 workspace must grow during graph capture; plan the shape first")
-            if ws is not None:
-                self._ws_retired.append(ws)          # captured graphs may still point at it
-            ws = self.ws[chain] = torch.empty(wsb.value, dtype=torch.uint8, device=self.L.device)
-        return ws
+        """dW2 = dZ2^T @ H1 split-K S ways into the slabs p2 [2][S][H][H] (f32 rows)."""
+        check(_lib.lib().satrl_ppo_dw2(self.L.H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), stream_ptr()),
+              "satrl_ppo_dw2")
 
     def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False):
         """One minibatch step of one chain.  Bench-only knobs: `events` (a pair
@@ -602,11 +441,6 @@ class FusedMinibatch:
         self.side.wait_stream(cur)
         fn(0)
         with torch.cuda.stream(self.side):
-            if self.offset_cycles > 0:
-                # the critic chain starts this many shader cycles behind the actor's
-                # (a GPU spin), so one net's rowpass runs beside the other's
-                # dW2 / reduce / Adam instead of in lockstep with its rowpass
-                torch.cuda._sleep(self.offset_cycles)
             fn(1)
         cur.wait_stream(self.side)
 
@@ -642,13 +476,6 @@ class FusedMinibatch:
         check(_lib.lib().satrl_ppo_group_advance(ptr(self.grp), stream_ptr()), "satrl_ppo_group_advance")
 
     def _capture(self, src):
-        if self.lib_gemm:
-            # hipBLASLt sets up a GEMM shape on its first call per stream, which is
-            # not capture-safe: run the dW2 products once eagerly into the scratch slabs
-            for net in ((0, 1) if self.split else (-1,)):
-                with torch.cuda.stream(self.side if net == 1 else torch.cuda.current_stream()):
-                    self._dw2(self.H1, self.dZ2, self.mb, self.S, net)
-            torch.cuda.synchronize()
         if self.L.comm is not None:
             self.L.comm.warm(self.L.G)        # RCCL connects lazily: never inside the capture
         s = torch.cuda.Stream()
@@ -664,8 +491,6 @@ class FusedMinibatch:
         B = perm.numel()
         mb, G = self.mb, self.group
         nfull = B // mb
-        if B % mb:
-            self.plan_shape(B % mb)          # the ragged tail's dW2 plan, before any step of the epoch
         graphable = self.use_graph and torch.cuda.is_available() and (self.L.pg is None or self.L.comm is not None
                                                                        or self.L.peer is not None)
         k = 0
@@ -678,19 +503,25 @@ class FusedMinibatch:
             if self.graph is None or self._src_ptr != src.data_ptr():
                 self._capture(src)
             self.grp.zero_()
-            comm = self.L.comm
+            comm, peer = self.L.comm, self.L.peer
             inflight = []
             for _ in range(nfull // G):
                 self.graph.replay()
-                if comm is not None:
-                    # RCCL watchdog between replays: at most two replays queued
-                    # ahead of the host, each waited for with the deadline while
-                    # ncclCommGetAsyncError is polled (rccl.Comm.wait_event)
+                if comm is not None or peer is not None:
+                    # watchdog between replays: at most two replays queued ahead
+                    # of the host.  RCCL: the oldest is waited for with the
+                    # deadline while ncclCommGetAsyncError is polled
+                    # (rccl.Comm.wait_event); peer: once it has finished, the
+                    # error word is read, so a lost rank stops the update there
                     ev = torch.cuda.Event()
                     ev.record()
                     inflight.append(ev)
                     if len(inflight) > 2:
-                        comm.wait_event(inflight.pop(0), _dist.dp_timeout_s())
+                        if comm is not None:
+                            comm.wait_event(inflight.pop(0), _dist.dp_timeout_s())
+                        else:
+                            inflight.pop(0).synchronize()
+                            peer.check()
             k = (nfull // G) * G
         while k < nfull:                      # the rest of the full minibatches, eagerly
             ng = min(G, nfull - k)
@@ -760,7 +591,7 @@ class PPOLearner:
         self.peer = None
         if on_gpus and mode == "peer":
             from .peer import PeerComm
-            self.peer = PeerComm(pg, ppo_layout(int(args.hidden_width))["total"], self.device)
+            self.peer = PeerComm(pg, ppo_layout(int(args.hidden_width))["total"], self.device, int(args.hidden_width))
         self.graph_group = graph_group
         self.use_graph = use_graph
         # CPU init with the reference's RNG consumption order (actor, then critic)
@@ -780,9 +611,7 @@ class PPOLearner:
         self.critic = critic.to(self.device)
         P = self.P
         self.W2v = P[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
-        # the fc2 operand image the rowpass reads (the f32 fc2.weight^T; satrl_ppo.h;
-        # w2x_image also writes the pre-split planes layout a kW2Pre build of
-        # commit e2546b9 reads)
+        # the fc2 operand image the rowpass reads (the f32 fc2.weight^T; satrl_ppo.h)
         self.W2T = torch.zeros(w2x_floats(H), **f32)
         self.GW2v = self.G[o["W2"]:o["W2"] + 2 * H * H].view(2, H, H)
         W1 = P[o["W1"]:o["W1"] + 2 * H * 20].view(2, H, 20)
@@ -854,8 +683,7 @@ class PPOLearner:
             self.W2T.copy_(w2x_image(self.P[:2 * self.H * self.H], self.H))
 
     def w2t_f32(self):
-        """fc2.weight^T per net [2, H, H] f32 decoded from the operand image
-        (planes summed: hi + mid + lo is the weight exactly)."""
+        """fc2.weight^T per net [2, H, H] f32 from the operand image."""
         return w2x_decode(self.W2T, self.H)
 
     def stepper(self, mb):

@@ -19,25 +19,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_two_ranks_one_device(allreduce):
     """... and with --allreduce peer the whole update runs through the peer
     all-reduce kernel (IPC within the device); either way the line carries
-    the peer kernel's all-reduce time beside the c10d path.
+    the peer kernel's all-reduce time beside the c10d path.  Both at the
+    product's hidden width (256).
 
-    The peer variant runs at hidden 64.  Both ranks share ONE device here, so
-    rank 0's peer all-reduce blocks spin on CUs while rank 1's next kernel
-    must still be placed: at H = 256 a 16-wave rowpass workgroup (~104 VGPRs
-    per wave) fits on a CU beside two spinning waves per SIMD but not three,
-    and the rehearsal then fails its 0.5 s peer bound by placement, not by
-    the path (one pass, one fail on the same tree, EXPERIMENTS.md round 4).
-    On the driver's node every rank has its own GPU and nothing shares a CU
-    with a peer kernel; the peer path's H = 256 arithmetic is covered by
-    test_dp_gpu.py::test_peer_allreduce_world2_one_device."""
+    Both ranks share ONE device here, so rank 0's peer all-reduce waves spin
+    on CUs while rank 1's next kernel must still be placed: the peer grid is
+    at most one 256-thread workgroup per CU (satrl_peer_blocks), i.e. one
+    spinning wave per SIMD, which leaves every CU room for a 16-wave rowpass
+    workgroup (a 641-block grid, up to three spinning waves per SIMD, starved
+    it in round 4).  The peer waits are bounded by SATRL_DP_TIMEOUT_S (30 s
+    here, so a stall fails the test instead of the box's hang check)."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    width = ["--hidden", "64"] if allreduce == "peer" else []
+    env["SATRL_DP_TIMEOUT_S"] = "30"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--one-device",
                         "--num-envs", "512", "--horizon", "32", "--epochs", "1", "--minibatch", "4096",
                         "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--kernel-iters", "10",
-                        "--global-slice", "8", "--allreduce", allreduce] + width, env=env, capture_output=True,
+                        "--global-slice", "8", "--allreduce", allreduce], env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]

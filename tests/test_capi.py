@@ -84,10 +84,6 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_rowpass(256, 64, -1, None, *args[1:]) == -1           # null rows
     assert lib.satrl_ppo_dw2(256, 4096, -1, 0, fake, fake, fake, None) == -1   # S < 1
     assert lib.satrl_ppo_dw2(256, 64, -1, 64, fake, fake, fake, None) == -1    # an empty split
-    assert lib.satrl_ppo_dw2_lib(256, 4096, -1, 3, fake, fake, fake, fake, 1 << 20, None) == -1   # mb % S
-    assert lib.satrl_ppo_dw2_lib(256, 4096, -1, 4, None, fake, fake, fake, 1 << 20, None) == -1   # null H1
-    assert lib.satrl_ppo_dw2_lib_workspace(256, 4096, 2, 4, fake, None) == -1                    # net
-    assert lib.satrl_ppo_dw2_lib_workspace(256, 4096, -1, 4, None, None) == -1                   # no output
     assert lib.satrl_ppo_reduce(256, 64, -1, 1, 4, fake, fake, fake, fake, fake, fake, None) == -1   # mode
     assert lib.satrl_ppo_reduce(256, 64, -1, 1, 2, fake, fake, fake, fake, None, None, None) == -1   # no nsq
     assert lib.satrl_gae(0, 4, fake, fake, fake, 0.99, 0.95, fake, fake, None) == -1
@@ -96,18 +92,29 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
                                 None) == -1                                   # second agent without outputs
     assert lib.satrl_ppo_tanh(0, fake, fake, None) == -1
     # the fc2 operand image and the k-packed dW2 path (H = 256, mb above the 16-row threshold)
-    assert lib.satrl_ppo_w2x_floats(256) in (2 * 256 * 256, 6 * 256 * 256)   # f32 W2^T, or the planes build
+    assert lib.satrl_ppo_w2x_floats(256) == 2 * 256 * 256                    # the f32 W2^T at every width
     assert lib.satrl_ppo_w2x_floats(64) == 2 * 64 * 64
     assert lib.satrl_ppo_w2x_floats(100) == -1
     assert lib.satrl_ppo_w2x_sync(100, -1, fake, fake, None) == -1 and lib.satrl_ppo_w2x_sync(256, -1, None, fake, None) == -1
     assert lib.satrl_ppo_kx_elems(256, 4096) == 2 * 3 * 4096 * 256 and lib.satrl_ppo_kx_elems(256, 1500) == 6 * 1504 * 256
     assert lib.satrl_ppo_kx_elems(64, 4096) == -1
-    assert lib.satrl_ppo_rowpass_kx(256, 1024, -1, *args) == -1                 # the 16-row kernel's minibatch
+    assert lib.satrl_ppo_rowpass_kx(256, 512, -1, None, *args[1:]) == -1        # null rows (16-row kernel's minibatch)
     assert lib.satrl_ppo_rowpass_kx(64, 4096, -1, *args) == -1                  # H 256 only
     assert lib.satrl_ppo_dw2_kx_splits(256, 4096, -1) == 8 and lib.satrl_ppo_dw2_kx_splits(256, 4096, 0) == 16
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, fake, None) == -1     # S < 1
     assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, fake, None) == -1       # an empty split (2 chunks)
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, fake, None) == -1     # null H1x
+    # the peer all-reduce: grid, deadline, buffers
+    bufs = (C.c_void_p * 2)(16, 16)
+    pa = [C.cast(bufs, C.c_void_p), fake, fake, fake]
+    assert lib.satrl_ppo_allreduce_peer(256, 512, 2, 0, *pa, 0, 10.0, None) == -1            # no blocks
+    assert lib.satrl_ppo_allreduce_peer(256, 512, 2, 0, *pa, 2048, 10.0, None) == -1         # > kPeerMaxBlocks
+    assert lib.satrl_ppo_allreduce_peer(256, 512, 2, 0, *pa, 256, 0.0, None) == -1           # no deadline
+    assert lib.satrl_ppo_allreduce_peer(256, 512, 2, 2, *pa, 256, 10.0, None) == -1          # rank >= world
+    assert lib.satrl_ppo_allreduce_peer(256, 512, 9, 0, *pa, 256, 10.0, None) == -1          # world > 8
+    assert lib.satrl_peer_blocks(100, C.byref(C.c_int())) == -1 and lib.satrl_peer_blocks(256, None) == -1
+    assert lib.satrl_peer_error(None, C.byref(C.c_uint64()), None) == -1
+    assert lib.satrl_peer_reset(fake, 8, None) == -1                                         # smaller than the header
 
 
 def test_product_has_no_cpu_fallback():
@@ -162,20 +169,13 @@ def test_improvednn_matches_reference_state_dict():
 
 def test_w2x_image_host_statement():
     """The fc2 operand image's host statement (satrl.ppo.w2x_image, what
-    satrl_ppo_w2x_sync writes): at H = 256 every plane is a round-to-nearest
-    bf16 and hi + mid + lo is the f32 weight exactly, for fc2.weight and its
-    transpose; w2x_decode recovers fc2.weight^T bit for bit (H 64: the f32
-    transpose itself)."""
+    satrl_ppo_w2x_sync writes): the f32 fc2.weight^T of both nets at every
+    width, and w2x_decode recovers it bit for bit."""
     import torch
     from satrl.ppo import w2x_decode, w2x_image
     g = torch.Generator().manual_seed(0)
-    for H, pre in ((64, False), (256, False), (256, True)):
+    for H in (64, 256):
         W2 = torch.randn(2 * H * H, generator=g) * torch.exp(torch.randn(2 * H * H, generator=g) * 4)
-        img = w2x_image(W2, H, presplit=pre)
-        assert img.dtype == torch.float32 and img.numel() == (6 if pre else 2) * H * H
+        img = w2x_image(W2, H)
+        assert img.dtype == torch.float32 and img.numel() == 2 * H * H
         assert torch.equal(w2x_decode(img, H), W2.view(2, H, H).transpose(1, 2))
-        if pre:
-            p = img.view(torch.int16).view(2, 2, 3, H, H).view(torch.bfloat16).float()
-            assert torch.equal((p[:, 0, 0] + p[:, 0, 1]) + p[:, 0, 2], W2.view(2, H, H))
-            assert torch.equal(p[:, 0, 0], W2.view(2, H, H).to(torch.bfloat16).float())      # hi: RNE of w
-            assert torch.equal(p[:, 1], p[:, 0].transpose(2, 3))                            # W2^T planes

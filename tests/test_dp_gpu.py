@@ -321,6 +321,7 @@ def _peer_rank(rank, port, q):
     IPC-mapped buffers) against c10d's SUM / world + satrl_ppo_reduce_dp, on
     a raw gradient and through whole DP updates (eager and graph-replayed)."""
     import torch.distributed as dist
+    os.environ["SATRL_DP_TIMEOUT_S"] = "30"           # the peer waits' bound: a stall fails, never hangs
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
     try:
@@ -353,6 +354,31 @@ def _peer_rank(rank, port, q):
         torch.cuda.synchronize()
         out["raw"] = (torch.equal(Gp, Gg), torch.equal(nsq_p, nsq_g), torch.equal(steps_p, steps_g), Gp.cpu().numpy())
         assert Lp.peer.error() == 0
+        props = torch.cuda.get_device_properties(0)
+        assert 1 <= Lp.peer.blocks <= props.multi_processor_count       # at most one spinning block per CU
+        # (1b) a rank that skips a call: the other's waits run out (2 s here),
+        # the error word is set and check raises; after reset on both ranks
+        # the next call is bitwise the c10d path again
+        from satrl.peer import PeerError
+        if rank == 0:
+            Lp.peer.timeout_s = 2.0
+            Gp.copy_(G0)
+            Lp.peer.all_reduce_dp_(256, 512, Gp, nsq_p, steps_p)
+            try:
+                Lp.peer.check()
+                raise AssertionError("a missing peer was not reported")
+            except PeerError:
+                pass
+            Lp.peer.timeout_s = 30.0
+        dist.barrier()
+        Lp.peer.reset()
+        assert Lp.peer.error() == 0
+        Gp.copy_(G0)
+        steps_p.fill_(2.0)
+        Lp.peer.all_reduce_dp_(256, 512, Gp, nsq_p, steps_p)
+        torch.cuda.synchronize()
+        out["reset"] = (torch.equal(Gp, Gg), torch.equal(nsq_p, nsq_g), torch.equal(steps_p, steps_g),
+                        Lp.peer.error() == 0)
         # (2) DP updates, H 64: peer path (graph-replayed and eager) vs the gloo path
         res = {}
         for mode, graph in (("peer", True), ("peer", False), ("rccl", False)):
@@ -389,7 +415,8 @@ def test_peer_allreduce_world2_one_device():
     """satrl_ppo_allreduce_peer over two ranks on one GPU (IPC within the
     device): bitwise c10d's SUM / world and reduce_dp's norms and step
     counters on a raw gradient over three calls, bitwise identical on both
-    ranks; whole DP updates (2 epochs of 5 minibatches + a ragged tail,
+    ranks; a call one rank skips times out into the error word, and after
+    PeerComm.reset the next call is bitwise right again; whole DP updates (2 epochs of 5 minibatches + a ragged tail,
     graph-replayed and eager) bitwise equal to the gloo-all-reduce path."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -418,6 +445,7 @@ def test_peer_allreduce_world2_one_device():
     for r in (0, 1):
         eqG, eqN, eqS, _ = res[r]["raw"]
         assert eqG and eqN and eqS, (r, eqG, eqN, eqS)
+        assert all(res[r]["reset"]), (r, res[r]["reset"])
         assert all(res[r]["update"][0]), (r, res[r]["update"][0])
     import numpy as np
     assert np.array_equal(res[0]["raw"][3], res[1]["raw"][3])

@@ -13,6 +13,7 @@ import pytest
 import torch
 
 from conftest import golden
+from update_replay import h256_case, run_reference_update
 
 pytestmark = pytest.mark.gpu
 
@@ -146,66 +147,36 @@ def test_policy_forward_one_layer_checkpoint():
 
 def test_update_matches_reference():
     """ppo_continuous.py:191-250 with the reference's own buffer and
-    minibatch permutations (captured), through the drop-in PPO_continuous."""
-    from satrl.buffer import ReplayBuffer
-    from satrl.ppo import PPO_continuous
+    minibatch permutations (captured), through the drop-in PPO_continuous.
+    5e-5 absolute: about 1 % of the movement 24 Adam steps at lr 2e-4 can
+    make (lr * nsteps = 4.8e-3), 2.8x the measured worst (1.8e-5, the f32
+    gradient sums adding in another order than torch's)."""
     u = golden("update_case")
-    B, mb, H, K, mts, lr_a, lr_c, gamma, lamda, eps, ent = u["hp"]
-    args = _args(batch_size=int(B), mini_batch_size=int(mb), hidden_width=int(H), K_epochs=int(K),
-                 max_train_steps=int(mts))
-    agent = PPO_continuous(args, "pursuer")
-    sd_a = {k[len("p0.actor."):]: torch.tensor(u[k]) for k in u.files if k.startswith("p0.actor.")}
-    sd_c = {k[len("p0.critic."):]: torch.tensor(u[k]) for k in u.files if k.startswith("p0.critic.")}
-    agent.actor.load_state_dict(sd_a)
-    agent.critic.load_state_dict(sd_c)
-    buf = ReplayBuffer(args)
-    for i in range(int(B)):
-        buf.store(u["s"][i], u["a"][i], u["logp"][i], u["r"][i], u["s_"][i], u["dw"][i], u["done"][i])
-    # reproduce the reference's torch global RNG state: the fixture's perms were
-    # drawn right after the buffer was filled; replay them through the sampler
-    perms = u["perms"]
-    import torch.utils.data.sampler as S
-    orig = S.SubsetRandomSampler.__iter__
-    it = iter(perms)
+    run_reference_update({k: u[k] for k in u.files})
 
-    def fake_iter(self):
-        return iter(next(it).tolist())
-    S.SubsetRandomSampler.__iter__ = fake_iter
-    try:
-        agent.update(buf, int(u["total_steps"]))
-    finally:
-        S.SubsetRandomSampler.__iter__ = orig
-    worst = 0.0
-    nsteps = int(K) * int(np.ceil(B / mb))
-    for k in u.files:
-        if not k.startswith("p1."):
-            continue
-        name = k[3:]
-        net, pname = name.split(".", 1)
-        got = dict((agent.actor if net == "actor" else agent.critic).state_dict())[pname].cpu().numpy()
-        ref = u[k]
-        p0 = u["p0." + name]
-        step_ref = np.abs(ref - p0).max()
-        diff = np.abs(got - ref)
-        worst = max(worst, float(diff.max()))
-        # 5e-5 absolute: about 1 % of the movement 24 Adam steps at lr 2e-4 can
-        # make (lr * nsteps = 4.8e-3), 2.8x the measured worst (1.8e-5, the
-        # f32 gradient sums adding in another order than torch's)
-        assert np.allclose(got, ref, rtol=0, atol=5e-5), (name, diff.max(), step_ref)
-    print(f"update parity: worst abs param diff {worst:.3e} after {nsteps} Adam steps")
-    la, lc = agent.L.lr_now
-    # lr lives in an f32 device tensor (the reference keeps a python float)
-    assert abs(la - u["lr_after"][0]) <= 1e-6 * u["lr_after"][0] and abs(lc - u["lr_after"][1]) <= 1e-6 * u["lr_after"][1]
+
+@pytest.mark.parametrize("case", ["kx", "short", "ragged"])
+def test_update_matches_reference_h256(case):
+    """The product's own update kernels pinned to the reference's update() at
+    H = 256 (tests/golden/capture_update_h256.py): "kx" B 8192 / mb 4096 (the
+    32-row rowpass with k-packed planes and dw2_kx, the bench's path), "short"
+    B 2048 / mb 512 (configs[3]'s per-rank minibatch, the 16-row rowpass),
+    "ragged" B 4873 / mb 4096 (a kx minibatch and a 777-row tail).  Same bar
+    as the H = 64 case: 5e-5 absolute after 4 (short: 8) Adam steps that move
+    a parameter by up to 8e-4 (1.6e-3)."""
+    run_reference_update(h256_case(case))
 
 
 @pytest.mark.parametrize("H,split,mb", [(64, False, 512), (256, False, 512), (256, True, 512),
                                          (256, False, 777), (64, False, 100),
                                          (256, False, 4096), (64, False, 4096)])
 def test_fused_step_vs_torch_autograd(H, split, mb):
-    """satrl_ppo_rowpass (f32 MFMA) + hipBLASLt dW2 + reduce + Adam vs plain torch fp32 autograd +
-    clip_grad_norm_ + torch.optim.Adam on the same minibatch; mb 777 / 100 are
-    ragged (the last BatchSampler minibatch with drop_last=False, a partial
-    32-row block and split-K remainder)."""
+    """The product's minibatch step (H 64: rowpass_dw2 + reduce + Adam; H 256:
+    rowpass_kx + dw2_kx + reduce + Adam, 16-row blocks at mb <= 1024) vs plain
+    torch fp32 autograd + clip_grad_norm_ + torch.optim.Adam on the same
+    minibatch; mb 777 / 100 are ragged (the last BatchSampler minibatch with
+    drop_last=False, a partial row block and split-K remainder); split: the
+    actor and critic chains on two streams."""
     from satrl.ppo import PPOLearner
     from torch_reference import reference_step
     torch.manual_seed(11)
@@ -240,8 +211,7 @@ def test_fused_step_vs_torch_autograd(H, split, mb):
         got = P[k].reshape(ref.shape)
         assert torch.allclose(got, ref, rtol=1e-5, atol=2e-7), (k, (got - ref).abs().max().item())
     assert L.steps.cpu().tolist() == [1.0, 1.0]
-    # Adam also refreshed the fc2 operand image (fc2.weight^T, or at H = 256 the
-    # pre-split planes of fc2.weight and its transpose): bitwise the image of P
+    # Adam also refreshed the fc2 operand image (fc2.weight^T): bitwise the image of P
     from satrl.ppo import w2x_image
     assert torch.equal(L.W2T.view(torch.int32), w2x_image(L.P[:2 * H * H], H).view(torch.int32))
     assert torch.equal(L.w2t_f32(), L.P[:2 * H * H].view(2, H, H).transpose(1, 2))
@@ -564,44 +534,6 @@ def test_dw2_kernel_vs_torch(H, mb):
     assert err <= 1e-5 * ref.abs().max().item() + 1e-4, err
 
 
-@pytest.mark.parametrize("mb,S,net", [(4096, 4, -1), (4096, 4, 1), (4096, 1, -1), (776, 4, 0)])
-def test_dw2_lib_vs_fp64_and_deterministic(mb, S, net):
-    """satrl_ppo_dw2_lib (hipBLASLt, fixed stream-K solution) at H = 256:
-    each slab == its split's dZ2^T @ H1 in fp64 within f32 accumulation
-    error, only the selected net's slabs written, and a second call
-    reproduces every slab bit for bit (the stream-K fix-up has a fixed
-    order)."""
-    import ctypes as C
-    from satrl import _lib
-    H = 256
-    lib = _lib.lib()
-    g = torch.Generator(device="cuda").manual_seed(mb + S)
-    H1 = torch.randn(2 * mb * H, device="cuda", generator=g)
-    dZ2 = torch.randn(2 * mb * H, device="cuda", generator=g)
-    wsb, idx = C.c_int64(), C.c_int()
-    _lib.check(lib.satrl_ppo_dw2_lib_workspace(H, mb, net, S, C.byref(wsb), C.byref(idx)), "workspace")
-    print(f"solution index {idx.value}, workspace {wsb.value} B")
-    ws = torch.empty(max(wsb.value, 1), dtype=torch.uint8, device="cuda")
-    lo = 0 if net < 0 else net
-    outs = []
-    for _ in range(2):
-        p2 = torch.full((2 * S * H * H,), float("nan"), device="cuda")
-        _lib.check(lib.satrl_ppo_dw2_lib(H, mb, net, S, _lib.ptr(H1[lo * mb * H:]), _lib.ptr(dZ2[lo * mb * H:]),
-                                         _lib.ptr(p2[lo * S * H * H:]), _lib.ptr(ws), wsb.value, _lib.stream_ptr()),
-                   "satrl_ppo_dw2_lib")
-        torch.cuda.synchronize()
-        outs.append(p2.view(2, S, H, H))
-    assert torch.equal(outs[0].view(-1).view(torch.int32), outs[1].view(-1).view(torch.int32))
-    K = mb // S
-    ref = torch.bmm(dZ2.view(2 * S, K, H).double().transpose(1, 2), H1.view(2 * S, K, H).double()).view(2, S, H, H)
-    for n in range(2):
-        if net >= 0 and n != net:
-            assert torch.isnan(outs[0][n]).all()                 # the other net untouched
-            continue
-        err = (outs[0][n].double() - ref[n]).abs().max().item()
-        assert err <= 1e-5 * ref[n].abs().max().item() + 1e-4, err
-
-
 @pytest.mark.parametrize("mb,contig", [(4096, True), (777, False), (256, True)])
 def test_fused_dw2_rowpass_bitwise_equals_separate(mb, contig):
     """H 64 (configs[1]): satrl_ppo_rowpass_dw2 writes each 32-row block's
@@ -678,14 +610,16 @@ def test_rollout_logp_equals_update_recomputation(H, mb):
 
 
 
-@pytest.mark.parametrize("mb,contig", [(4096, True), (1500, False)])
+@pytest.mark.parametrize("mb,contig", [(4096, True), (1500, False), (512, True), (777, False), (520, True)])
 def test_kx_rowpass_planes_and_dw2(mb, contig):
     """H 256: satrl_ppo_rowpass_kx writes H1 / dZ2 as k-packed bf16 planes
     whose sum hi + mid + lo is bitwise the f32 rowpass's H1 / dZ2 (rows past
     the minibatch zero), with the same [dW1|db1] / tail slabs; satrl_ppo_dw2_kx
     sums dZ2^T H1 from them on the split-bf16 MFMA within the f32 bound of an
     f64 reference (ppo_continuous.py:227-233: fc2.weight.grad).  1500: a ragged
-    last chunk on the index-gather path."""
+    last chunk on the index-gather path.  512 / 777 / 520: the 16-row rowpass
+    (configs[3]'s per-rank minibatch, ragged tails), whose last block zero-fills
+    the padded half of its 32-row chunk (777: rows 784-799, 520: 528-543)."""
     import satrl._lib as _L
     from satrl.ppo import PPOLearner
     torch.manual_seed(5)

@@ -29,7 +29,7 @@ def rank_main(rank, port, world):
     from satrl.ppo import ppo_layout
     n = ppo_layout(int(os.environ.get("PROBE_H", "64")))["total"]
     H = int(os.environ.get("PROBE_H", "64"))
-    pc = PeerComm(dist.group.WORLD, n, "cuda:0")
+    pc = PeerComm(dist.group.WORLD, n, "cuda:0", H)
     say(f"peer comm up, n {n}, bufs {[hex(b or 0) for b in pc.bufs]}")
     G = torch.full((n,), float(rank + 1), device="cuda:0")
     nsq = torch.zeros(2 * 1024, dtype=torch.float64, device="cuda:0")

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Development tool (not shipped, not a test): in-graph time of one fused
-minibatch step (rowpass -> dW2 -> reduce -> Adam) at H 256 (PROBE_H sets
-another width) for the given minibatch sizes, replaying the update's graphs
-over a 16-minibatch epoch; SATRL_LIB_PATH selects a library build.
-Usage: python tools/minibatch_time.py 512 1024 2048 4096"""
+minibatch step for FusedMinibatch variants side by side (constructor
+keywords), replaying the update's graphs over a 16-minibatch epoch.
+Usage: python tools/step_ab.py H mb variant[,variant...] [reps]
+  variants: "product" (defaults), or key=value pairs joined by '+', e.g. kx=0"""
 import os
 import sys
 
@@ -11,28 +11,42 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
-from satrl.ppo import PPOLearner  # noqa: E402
+from satrl.ppo import FusedMinibatch, PPOLearner  # noqa: E402
 from satrl.trainer import args_param  # noqa: E402
 
-H = int(os.environ.get("PROBE_H", "256"))
-for mb in [int(x) for x in sys.argv[1:]] or [4096]:
+
+def parse(v):
+    if v == "product":
+        return {}
+    return {k: int(x) for k, x in (kv.split("=") for kv in v.split("+"))}
+
+
+def time_variant(H, mb, kw, n=20):
     B = 16 * mb
     a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=B, chkpt_dir="/tmp")
     L = PPOLearner(a, "pursuer", graph_group=16)
     g = torch.Generator(device="cuda").manual_seed(0)
     src = torch.randn((B, 32), device="cuda", generator=g)
     src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
-    st = L.stepper(mb)
+    st = FusedMinibatch(L, mb, 16, **kw)
     perm = torch.randperm(B, device="cuda", generator=g)
+    L.sync_w2t()
     for _ in range(3):
         st.run(src, perm)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n = 20
     e0.record()
     for _ in range(n):
         st.run(src, perm)
     e1.record()
     torch.cuda.synchronize()
-    print(f"H {H} mb {mb:5d}: {e0.elapsed_time(e1) * 1e3 / (n * 16):7.2f} us per minibatch step ({ROOT})",
-          flush=True)
+    return e0.elapsed_time(e1) * 1e3 / (n * 16)
+
+
+if __name__ == "__main__":
+    H, mb = int(sys.argv[1]), int(sys.argv[2])
+    variants = sys.argv[3].split(",")
+    reps = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    for r in range(reps):
+        for v in variants:
+            print(f"H {H} mb {mb:5d} {v:>12s}: {time_variant(H, mb, parse(v)):7.2f} us per minibatch step", flush=True)
