@@ -509,8 +509,12 @@ def run(a, world):
                     return float(r["avg_ns"]) / 1e3
         return None
 
+    # PMC summaries per shape: the bench's H 256 ones, "_h64" for configs[1]'s
+    # (tools/profile_round.sh), each used only when its shape is this run's
+    sfx = {256: "", 64: "_h64"}.get(a.hidden, "_none")
+
     def pmc(kind, **match):
-        pmc_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_{kind}_pmc.json")
+        pmc_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_{kind}{sfx}_pmc.json")
         if os.path.exists(pmc_file):
             with open(pmc_file) as f:
                 d = json.load(f)
@@ -537,24 +541,27 @@ def run(a, world):
                        "frac": pol_tfs / FP32_MFMA_PEAK_TFS, "avg_launch_us": pol_us, "flop_per_launch": pol_flop,
                        "timing": f"rocprofv3 average over the rollout's launches "
                                  f"(profiles/{os.path.basename(ks_file)})"}
-        pol_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_policy_mfma_pmc.json")
+        pol_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_policy{sfx}_mfma_pmc.json")
+        d = None
         if os.path.exists(pol_file):
             with open(pol_file) as f:
                 d = json.load(f)
+        # (only a pass over this very kernel and shape: hidden width and env count)
+        if d is not None and d.get("hidden") == a.hidden and d.get("num_envs") == a.num_envs:
             policy_roof["mfma_utilisation"] = {
                 "mfma_busy_cycles_per_launch": d["SQ_VALU_MFMA_BUSY_CYCLES_median"],
                 "mfma_busy_frac_dispatch_window": d["mfma_busy_frac"],
-                "source": f"profiles/{a.profile_tag}_policy_mfma_pmc.json (lower bound: the --pmc dispatch "
+                "source": f"profiles/{a.profile_tag}_policy{sfx}_mfma_pmc.json (lower bound: the --pmc dispatch "
                           "window includes the profiler's set-up)"}
     mfma_util = None                   # SQ_VALU_MFMA_BUSY_CYCLES pass (tools/profile_round.sh)
-    mfma_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_rowpass_mfma_pmc.json")
+    mfma_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_rowpass{sfx}_mfma_pmc.json")
     if os.path.exists(mfma_file):
         with open(mfma_file) as f:
             d = json.load(f)
         if d.get("hidden") == a.hidden and d.get("minibatch") == mb_local:
             mfma_util = {"mfma_busy_cycles_per_launch": d["SQ_VALU_MFMA_BUSY_CYCLES_median"],
                          "mfma_busy_frac_dispatch_window": d["mfma_busy_frac"],
-                         "source": f"profiles/{a.profile_tag}_rowpass_mfma_pmc.json (lower bound: the --pmc "
+                         "source": f"profiles/{a.profile_tag}_rowpass{sfx}_mfma_pmc.json (lower bound: the --pmc "
                                    "dispatch window includes the profiler's set-up)"}
 
     # ---- env kernel: in the rollout (live: eager rollout steps -- policy kernel,
@@ -879,7 +886,7 @@ def run(a, world):
                                             if ks_file else None),
                          "back_to_back_avg_launch_us": b2b_us,
                          "back_to_back_frac": rowpass_flop / (b2b_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS,
-                         "traffic_source": f"profiles/{a.profile_tag}_rowpass_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
+                         "traffic_source": f"profiles/{a.profile_tag}_rowpass{sfx}_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
                                            "bytes/launch)",
                          "mfma_utilisation": mfma_util,
                          "note": "f32 MFMA; one net per workgroup of 32 rows, each streams that net's fc2 weights "

@@ -91,6 +91,12 @@ int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, in
 int satenv_destroy(satenv_env* h);
 int satenv_num_envs(const satenv_env* h, int64_t* n);                /* host int64 */
 int satenv_set_params(satenv_env* h, const satenv_params* p);        /* host struct */
+/* which step kernel satenv_step / satenv_step_autoreset launch (propagators 0
+ * and 1): 2 = the wide kernel (default; one env's chain over the four waves
+ * of a workgroup, wide_envs = 64 envs per workgroup, 16 / 32 for A/B), 1 =
+ * the four-solve split kernel, 0 = one lane per env.  All three compute
+ * every step bit for bit the same (tests/test_env_gpu.py).                 */
+int satenv_set_step_kernel(satenv_env* h, int32_t kind, int32_t wide_envs);
 
 /* reset(Flag) for the envs whose env_mask byte is non-zero (NULL = all);
  * writes obs of ALL envs (f32 [N][18] and/or f64 [N][18], either nullable). */

@@ -1197,15 +1197,22 @@ constexpr int kKxD = 3;                         // ring slots (chunks kKxD - 1 a
 // 128: 4 tiles per net, half the plane bytes per workgroup, 32 splits)
 constexpr int kKxTW = 64;
 template <int TW>
-__global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int net_sel,
-                                                     const unsigned short* __restrict__ H1x,
-                                                     const unsigned short* __restrict__ dZ2x, float* __restrict__ p2) {
-  constexpr int H = 256, TT = H / TW, RUNS = 2 * 3 * 4;         // runs per chunk: tensor x plane x row group
-  constexpr int PPR = TW / 64, KG = TW * 16 + 16;               // 1-KB pieces per run, LDS bytes per run
+struct KxSmem {
+  static constexpr int RUNS = 2 * 3 * 4, KG = TW * 16 + 16;     // runs per chunk (tensor x plane x row group), LDS bytes per run
+  unsigned char ring[kKxD][RUNS][KG];
+};
+// the body of dw2_kx_kernel for workgroup b: the slab tile of (net, tile, split)
+template <int TW>
+__device__ __forceinline__ void dw2_kx_body(int b, int mb, int S, int KR, int net_sel,
+                                            const unsigned short* __restrict__ H1x,
+                                            const unsigned short* __restrict__ dZ2x, float* __restrict__ p2,
+                                            KxSmem<TW>& sm) {
+  constexpr int H = 256, TT = H / TW, RUNS = KxSmem<TW>::RUNS;
+  constexpr int PPR = TW / 64;                                   // 1-KB pieces per run
   constexpr int XN = TW / 32, PW = RUNS * PPR / 4;              // 16x16 tiles per wave side, pieces per wave
-  __shared__ __attribute__((aligned(16))) unsigned char ring[kKxD][RUNS][KG];
+  auto& ring = sm.ring;
   const int t = threadIdx.x, w = t >> 6, l = t & 63, li = l & 15, lg = l >> 4;
-  const int b = blockIdx.x, s = b % S, tile = (b / S) % (TT * TT);
+  const int s = b % S, tile = (b / S) % (TT * TT);
   const int net = net_sel < 0 ? b / (S * TT * TT) : net_sel;
   const int o0 = (tile / TT) * TW, n0 = (tile % TT) * TW;
   const int64_t PL = kx_rows(mb) * H;
@@ -1260,6 +1267,13 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         out[(int64_t)(o0 + (TW / 2) * wo + 16 * x + 4 * lg + q) * H + n0 + (TW / 2) * wn + 16 * y + li] = acc[x][y][q];
+}
+template <int TW>
+__global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int net_sel,
+                                                     const unsigned short* __restrict__ H1x,
+                                                     const unsigned short* __restrict__ dZ2x, float* __restrict__ p2) {
+  __shared__ __attribute__((aligned(16))) KxSmem<TW> sm;
+  dw2_kx_body<TW>(blockIdx.x, mb, S, KR, net_sel, H1x, dZ2x, p2, sm);
 }
 // split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split
 constexpr int kKxWgs = 256;
@@ -1870,6 +1884,7 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
   }
   if (b == 0 && t == 0) { steps[0] = st0 + 1.0; steps[1] = st1 + 1.0; }
 }
+
 
 }  // namespace
 

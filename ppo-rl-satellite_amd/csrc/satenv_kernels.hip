@@ -669,30 +669,16 @@ struct satenv_env {
   int32_t* i32 = nullptr;
   int32_t* err = nullptr;
   int split = 2;   // step_kernel_wide (2), step_kernel_split (1) or the one-lane step_kernel (0)
+  int wide_envs = 64;
 };
 
 namespace {
 
 int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
-// env-step kernel choice (dev A/B: SATENV_STEP_SPLIT=0 the one-lane kernel,
-// 1 the four-solve split kernel, 2 the wide kernel)
-int pick_split(int64_t n) {
-  (void)n;
-  const char* e = std::getenv("SATENV_STEP_SPLIT");
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] - '0';
-  return 2;
-}
-
-// envs per workgroup of the wide kernel (dev A/B: SATENV_WIDE_ENVS = 16/32/64)
-int wide_envs(int64_t n) {
-  const char* e = std::getenv("SATENV_WIDE_ENVS");
-  if (e) {
-    const int v = std::atoi(e);
-    if (v == 16 || v == 32 || v == 64) return v;
-  }
-  return 64;
-}
+// envs per workgroup of the wide kernel: 64 (satenv_set_step_kernel: 16 / 32
+// for A/B; fewer envs per workgroup measured no faster)
+int wide_envs(const satenv_env* h) { return h->wide_envs; }
 
 template <bool AR>
 void launch_step(satenv_env* h, const StepIO& io, void* stream) {
@@ -701,7 +687,7 @@ void launch_step(satenv_env* h, const StepIO& io, void* stream) {
     hipLaunchKernelGGL((step_kernel_split<AR, true>), grid, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
                        h->i32, io);
   else if (h->split == 2) {
-    const int envs = wide_envs(h->n);
+    const int envs = wide_envs(h);
     const dim3 gw(grid_for(h->n, envs));
     if (envs == 16)
       hipLaunchKernelGGL((step_kernel_wide<AR, 16>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
@@ -775,6 +761,14 @@ int satenv_default_params(satenv_params* p) {
   return SATENV_OK;
 }
 
+int satenv_set_step_kernel(satenv_env* h, int32_t kind, int32_t wide_envs) {
+  if (!h || kind < 0 || kind > 2 || (wide_envs != 16 && wide_envs != 32 && wide_envs != 64))
+    return fail(SATENV_ERR_ARG, "satenv_set_step_kernel: kind 0/1/2, wide_envs 16/32/64");
+  h->split = kind;
+  h->wide_envs = wide_envs;
+  return SATENV_OK;
+}
+
 int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, int device) {
   if (!out || !p || num_envs <= 0) return fail(SATENV_ERR_ARG, "satenv_create: bad arguments");
   if (!params_ok(p)) return fail(SATENV_ERR_ARG, "satenv_create: propagator must be 0/1/2, rk4_substeps >= 1");
@@ -783,7 +777,6 @@ int satenv_create(satenv_env** out, int64_t num_envs, const satenv_params* p, in
   h->n = num_envs;
   h->device = device;
   h->prm = *p;
-  h->split = pick_split(num_envs);
   hipError_t e = hipMalloc(&h->f64, sizeof(double) * kF64Planes * num_envs);
   if (e == hipSuccess) e = hipMalloc(&h->i32, sizeof(int32_t) * kI32Planes * num_envs);
   if (e == hipSuccess) e = hipMalloc(&h->err, sizeof(int32_t));

@@ -66,6 +66,7 @@ _SIGS = {
     "satenv_destroy": ([_vp], C.c_int),
     "satenv_num_envs": ([_vp, C.POINTER(_i64)], C.c_int),
     "satenv_set_params": ([_vp, C.POINTER(SatenvParams)], C.c_int),
+    "satenv_set_step_kernel": ([_vp, C.c_int32, C.c_int32], C.c_int),
     "satenv_reset": ([_vp, _i32, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_step": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satenv_step_autoreset": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),

@@ -180,6 +180,14 @@ class VecSatellites:
         self._p.d_range = float(v)
         self._push_params()
 
+    def set_step_kernel(self, kind: int = 2, wide_envs: int = 64):
+        """Which step kernel the device build launches (satenv_set_step_kernel):
+        2 the wide kernel (default), 1 the four-solve split kernel, 0 one lane
+        per env; every one computes the same bits."""
+        if self.host:
+            raise _lib.NativeError("the host build has one step loop")
+        check(_lib.lib().satenv_set_step_kernel(self._h, int(kind), int(wide_envs)), "satenv_set_step_kernel")
+
     # -- API -----------------------------------------------------------------
     def reset(self, Flag: int = 0, mask=None, obs_out=None, obs64_out=None):
         """environment.py:66-79 for all envs (or those with mask != 0). Returns obs f32 [N,18]."""

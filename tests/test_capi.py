@@ -73,6 +73,8 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     bad.propagator = 7
     assert lib.satenv_create(C.byref(h), 4, C.byref(bad), 0) == -1
     assert b"propagator" in lib.satenv_last_error()
+    assert lib.satenv_set_step_kernel(None, 2, 64) == -1 and lib.satenv_set_step_kernel(fake, 3, 64) == -1
+    assert lib.satenv_set_step_kernel(fake, 2, 48) == -1                       # 16 / 32 / 64 envs per workgroup
     # learner side: unsupported hidden width, empty minibatch, net out of range, null buffers
     off = (C.c_int64 * 16)()
     assert lib.satrl_ppo_layout(100, off) == -1 and lib.satrl_ppo_layout(256, off) == 0

@@ -161,10 +161,12 @@ def test_update_matches_reference_h256(case):
     H = 256 (tests/golden/capture_update_h256.py): "kx" B 8192 / mb 4096 (the
     32-row rowpass with k-packed planes and dw2_kx, the bench's path), "short"
     B 2048 / mb 512 (configs[3]'s per-rank minibatch, the 16-row rowpass),
-    "ragged" B 4873 / mb 4096 (a kx minibatch and a 777-row tail).  Same bar
-    as the H = 64 case: 5e-5 absolute after 4 (short: 8) Adam steps that move
-    a parameter by up to 8e-4 (1.6e-3)."""
-    run_reference_update(h256_case(case))
+    "ragged" B 4873 / mb 4096 (a kx minibatch and a 777-row tail).  1e-6
+    absolute after 4 (short: 8) Adam steps that move a parameter by up to
+    8e-4 (1.6e-3): 0.1 % of the update, 8x the measured worst (1.27e-7 on
+    MI355X; the f32 sums in another order than torch's CPU ones -- on the CPU
+    the same cases move by <= 8e-8 when fc1 is summed in f64 instead)."""
+    run_reference_update(h256_case(case), atol=1e-6)
 
 
 @pytest.mark.parametrize("H,split,mb", [(64, False, 512), (256, False, 512), (256, True, 512),
@@ -669,3 +671,4 @@ def test_kx_rowpass_planes_and_dw2(mb, contig):
     mag = torch.einsum("brn,brm->bnm", dZ2.double().abs(), H1.double().abs())
     err = ((got - ref).abs() / mag.clamp_min(1e-30)).max().item()
     assert err < 2e-6, err                 # per-slab split-bf16 sums (<= 2.2e-7 each) + f32 slab rounding
+

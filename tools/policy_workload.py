@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Workload for the policy-kernel MFMA pass of tools/profile_round.sh: the
-rollout's fused choose_action (satrl_policy_act, both agents, H 256) on
-16384 observations, launched back to back with random-init (orthogonal)
+rollout's fused choose_action (satrl_policy_act, both agents; argv: iters
+H envs, default 40 256 16384; configs[1]: 64 4096), launched back to back with random-init (orthogonal)
 pursuer and evader parameters, as in the bench's rollout."""
 import os
 import sys
@@ -17,7 +17,8 @@ from satrl.trainer import args_param  # noqa: E402
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 40
-    H, n = 256, 16384
+    H = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else 16384
     a = args_param(hidden_width=H, mini_batch_size=4096, batch_size=n * 2048, chkpt_dir="/tmp")
     pursuer = PPOLearner(a, "pursuer", use_graph=False)
     evader = PPOLearner(a, "evader", use_graph=False)

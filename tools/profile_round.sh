@@ -26,7 +26,12 @@ pmc pmc_env_fetch FETCH_SIZE -- "$W/env_workload.py" 40
 pmc pmc_env_write WRITE_SIZE -- "$W/env_workload.py" 40
 pmc pmc_mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/rowpass_workload.py" 40
 pmc pmc_policy_mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/policy_workload.py" 40
-# the post-rowpass chain (hipBLASLt dW2, reduce, Adam) of eager minibatch steps
+# BASELINE configs[1] (H 64, 4096 envs): its rowpass (dW2 fused) and policy kernel
+pmc pmc_fetch_h64 FETCH_SIZE -- "$W/rowpass_workload.py" 40 64 4096
+pmc pmc_write_h64 WRITE_SIZE -- "$W/rowpass_workload.py" 40 64 4096
+pmc pmc_mfma_h64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/rowpass_workload.py" 40 64 4096
+pmc pmc_policy_mfma_h64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/policy_workload.py" 40 64 4096
+# the post-rowpass chain (dw2_kx, reduce, Adam) of eager minibatch steps
 pmc pmc_step_fetch FETCH_SIZE -- "$W/step_workload.py" 40
 pmc pmc_step_write WRITE_SIZE -- "$W/step_workload.py" 40
 pmc pmc_step_mfma SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -- "$W/step_workload.py" 40

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Workload for the post-rowpass PMC passes of tools/profile_round.sh: whole
-minibatch steps (rowpass -> hipBLASLt dW2 -> reduce -> Adam) at the bench
+minibatch steps (rowpass_kx -> dw2_kx -> reduce -> Adam) at the bench
 configuration (H 256, mb 4096, both nets), eager so every kernel is its own
 dispatch.  summarize_profiles.py keeps the dW2 / reduce / Adam dispatches."""
 import os

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Turns rocprofv3 CSV output (tools/profile_round.sh) into the committed
 summaries under profiles/: the kernel-stats table of the bench command and
-the per-launch HBM traffic of satrl_ppo_rowpass from the FETCH_SIZE /
-WRITE_SIZE passes (MI355X_MICROARCH.md "HBM": FETCH_SIZE reports half the
+the per-launch HBM traffic of the product's rowpass (H 256: rowpass_kx; H 64,
+suffix _h64: rowpass_dw2) from the FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md "HBM": FETCH_SIZE reports half the
 bytes of 16-B-per-lane reads on gfx950 -> x2; WRITE_SIZE exact; both in KB)."""
 import csv
 import json
@@ -45,67 +45,19 @@ def main():
     ks = os.path.join(d, "bench_configs1", "run_kernel_stats.csv")      # BASELINE configs[1]'s bench command
     if os.path.exists(ks):
         kernel_stats(ks, os.path.join(prof, f"{tag}_bench_configs1_kernel_stats.csv"))
-    fetch = os.path.join(d, "pmc_fetch", "run_counter_collection.csv")
-    write = os.path.join(d, "pmc_write", "run_counter_collection.csv")
-    if os.path.exists(fetch) and os.path.exists(write):
-        f_kb, nf = pmc_per_dispatch(fetch, "rowpass_kernel", "FETCH_SIZE")
-        w_kb, nw = pmc_per_dispatch(write, "rowpass_kernel", "WRITE_SIZE")
-        res = {"kernel": "rowpass_kernel<256, 16, 32, kx>", "hidden": 256, "minibatch": 4096,
-               "dispatches": [nf, nw], "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
-               "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
-               "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
-               "workload": "tools/rowpass_workload.py"}
-        with open(os.path.join(prof, f"{tag}_rowpass_pmc.json"), "w") as f:
-            json.dump(res, f, indent=1)
-        print(json.dumps(res))
-    mfma = os.path.join(d, "pmc_mfma", "run_counter_collection.csv")
-    if os.path.exists(mfma):
-        # MFMA utilisation of the rowpass: SQ_VALU_MFMA_BUSY_CYCLES sums each MFMA's
-        # busy cycles on its SIMD over the chip; GRBM_GUI_ACTIVE sums the busy
-        # cycles of the 8 XCDs (MI355X_MICROARCH.md), so one XCD's span is /8
-        busy, nb = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
-        grbm, ng = pmc_per_dispatch(mfma, "rowpass_kernel", "GRBM_GUI_ACTIVE")
-        sqb, ns = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_BUSY_CYCLES")
-        n_simd = 256 * 4
-        # per launch (256 workgroups x 16 waves): fc1 fwd + [dW1|db1] on v_mfma_f32_16x16x4f32
-        # (K padded to 32: 32 per wave, 131 072, 32 busy cycles each); fc2 fwd + dH1 as
-        # split-bf16 v_mfma_f32_16x16x32_bf16 (8 chunks x 2 row tiles x 6 products x 2
-        # phases = 192 per wave, 786 432, 16 busy cycles each)
-        n_f32, n_bf16 = 256 * 16 * 32, 256 * 16 * 192
-        n_mfma = n_f32 + n_bf16
-        busy_expected = 32 * n_f32 + 16 * n_bf16
-        res = {"kernel": "rowpass_kernel<256, 16, 32, kx>", "hidden": 256, "minibatch": 4096, "dispatches": [nb, ng, ns],
-               "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
-               "SQ_BUSY_CYCLES_median": sqb,
-               "xcd_cycles": grbm / 8.0 if grbm else None,
-               "mfma_busy_frac": busy / (grbm / 8.0 * n_simd) if busy and grbm else None,
-               "mfma_instructions_per_launch": n_mfma,
-               "mfma_f32_16x16x4_per_launch": n_f32, "mfma_bf16_16x16x32_per_launch": n_bf16,
-               "busy_cycles_expected": busy_expected,
-               "busy_over_expected": busy / busy_expected if busy else None,
-               "definition": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the "
-                             "fraction of SIMD-cycles of the dispatch window in which the matrix core was busy, at "
-                             "the clock the chip ran (roofline.frac prices against the 2.4 GHz peak instead). The "
-                             "window of a ~30 us dispatch under --pmc includes the profiler's per-dispatch set-up "
-                             "(MI355X_MICROARCH.md: GRBM quotients read high below ~0.3 ms), so this is a lower "
-                             "bound; busy_over_expected = 1 shows the counter equals the MFMAs' busy cycles (32 per f32 16x16x4, 16 per "
-                             "bf16 16x16x32)",
-               "workload": "tools/rowpass_workload.py"}
-        with open(os.path.join(prof, f"{tag}_rowpass_mfma_pmc.json"), "w") as f:
-            json.dump(res, f, indent=1)
-        print(json.dumps(res))
+    for sfx, H in (("", 256), ("_h64", 64)):
+        rowpass_summaries(d, tag, prof, sfx, H)
     sf = os.path.join(d, "pmc_step_fetch", "run_counter_collection.csv")
     sw = os.path.join(d, "pmc_step_write", "run_counter_collection.csv")
     sm = os.path.join(d, "pmc_step_mfma", "run_counter_collection.csv")
     if os.path.exists(sf) and os.path.exists(sw) and os.path.exists(sm):
         # the post-rowpass chain per launch: HBM bytes (FETCH x2 + WRITE) against
         # the algorithmic bytes, and matrix-core busy cycles (dW2 only has MFMA work)
-        # the product's dW2 at this shape: dw2_kx_kernel (k-packed bf16 planes, 8 splits;
-        # round 4) or the hipBLASLt GEMM ("Cijk", 4 splits; SATRL_DW2_KX=0)
-        kx = pmc_per_dispatch(sf, "dw2_kx_kernel", "FETCH_SIZE")[0] is not None
-        H, mb, S, nwg = 256, 4096, (8 if kx else 4), 128
+        # the product's dW2 at this shape: dw2_kx_kernel (k-packed bf16 planes, 8 splits)
+        kx = True
+        H, mb, S, nwg = 256, 4096, 8, 128
         tot = 2 * H * H + 2 * H * 20 + 6 * H + 12            # flat layout incl. pads (satrl_ppo_layout)
-        dw2 = "dw2_kx_kernel" if kx else "Cijk"
+        dw2 = "dw2_kx_kernel"
         alg = {dw2: (2 * 2 * 3 * mb * H * 2 if kx else 2 * 2 * mb * H * 4) + 2 * S * H * H * 4,
                "reduce_kernel": (2 * S * H * H + nwg * 2 * H * 20 + nwg * (6 * H + 12)) * 4 + tot * 4,
                "adam_kernel": 4 * tot * 4 + 3 * tot * 4 + 2 * H * H * (6 if kx else 4)}
@@ -124,36 +76,15 @@ def main():
         res = {"kernels": chain, "hidden": H, "minibatch": mb, "dw2_splits": S,
                "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
                "definition": "per-dispatch medians; dw2_kx_kernel = the split-bf16 dW2 on the rowpass's k-packed "
-                             "planes, Cijk = the hipBLASLt dW2 GEMM (1.07 GFLOP per launch, f32-equivalent); "
+                             "planes (1.07 GFLOP per launch, f32-equivalent); "
                              "mfma_busy_frac as in the rowpass summary, over the --pmc dispatch window (a lower "
                              "bound for short dispatches)",
                "workload": "tools/step_workload.py (eager minibatch steps)"}
         with open(os.path.join(prof, f"{tag}_chain_pmc.json"), "w") as f:
             json.dump(res, f, indent=1)
         print(json.dumps(res))
-    pol = os.path.join(d, "pmc_policy_mfma", "run_counter_collection.csv")
-    if os.path.exists(pol):
-        # the rollout's policy kernel (both agents' forward, 16384 rows each; 1024 workgroups
-        # of 8 waves, each wave 2 row tiles x 2 column tiles): fc1 (K padded to 32) on
-        # v_mfma_f32_16x16x4f32, 32 per wave; fc2 as split-bf16 v_mfma_f32_16x16x32_bf16,
-        # 8 chunks x 4 tiles x 6 = 192 per wave
-        busy, nb = pmc_per_dispatch(pol, "policy_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
-        grbm, ng = pmc_per_dispatch(pol, "policy_kernel", "GRBM_GUI_ACTIVE")
-        n_f32, n_bf16 = 1024 * 8 * 32, 1024 * 8 * 192
-        n_mfma = n_f32 + n_bf16
-        busy_expected = 32 * n_f32 + 16 * n_bf16
-        res = {"kernel": "policy_kernel<256, 8, 0>", "hidden": 256, "num_envs": 16384, "agents": 2,
-               "dispatches": [nb, ng], "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
-               "xcd_cycles": grbm / 8.0 if grbm else None,
-               "mfma_busy_frac": busy / (grbm / 8.0 * 1024) if busy and grbm else None,
-               "mfma_instructions_per_launch": n_mfma, "busy_cycles_expected": busy_expected,
-               "busy_over_expected": busy / busy_expected if busy else None,
-               "definition": "as in the rowpass summary: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 "
-                             "SIMDs) over the --pmc dispatch window",
-               "workload": "tools/policy_workload.py"}
-        with open(os.path.join(prof, f"{tag}_policy_mfma_pmc.json"), "w") as f:
-            json.dump(res, f, indent=1)
-        print(json.dumps(res))
+    for sfx, H, n in (("", 256, 16384), ("_h64", 64, 4096)):
+        policy_summary(d, tag, prof, sfx, H, n)
     fetch = os.path.join(d, "pmc_env_fetch", "run_counter_collection.csv")
     write = os.path.join(d, "pmc_env_write", "run_counter_collection.csv")
     if os.path.exists(fetch) and os.path.exists(write):
@@ -173,6 +104,96 @@ def main():
             json.dump(res, f, indent=1)
         print(json.dumps(res))
     env_extra(d, tag, prof)
+
+
+MFMA_DEF = ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the fraction of "
+            "SIMD-cycles of the dispatch window in which the matrix core was busy, at the clock the chip ran "
+            "(roofline.frac prices against the 2.4 GHz peak instead). The window of a ~10-30 us dispatch under "
+            "--pmc includes the profiler's per-dispatch set-up (MI355X_MICROARCH.md: GRBM quotients read high below "
+            "~0.3 ms), so this is a lower bound; busy_over_expected = 1 shows the counter equals the MFMAs' busy "
+            "cycles (32 per f32 16x16x4, 16 per bf16 16x16x32)")
+
+
+def rowpass_mfma_counts(H, mb):
+    """(f32 16x16x4, bf16 16x16x32) MFMA instructions of one product rowpass
+    launch over both nets.  H 256 (rowpass_kx, 32-row blocks of 16 waves, one
+    16-column tile each): fc1 fwd + [dW1|db1] 32 f32 per wave (K padded to 32),
+    fc2 fwd + dH1 as split-bf16 8 chunks x 2 row tiles x 6 products x 2 phases
+    = 192 per wave.  H 64 (rowpass_dw2, 32-row blocks of 4 waves): fc1 16, fc2
+    and dH1 2 chunks x 16 each, [dW1|db1] 16, the fused dW2 partial 8 x 4 =
+    32: 128 f32 per wave."""
+    wgs = 2 * ((mb + 31) // 32)
+    if H == 256:
+        return wgs * 16 * 32, wgs * 16 * 192
+    return wgs * 4 * 128, 0
+
+
+def rowpass_summaries(d, tag, prof, sfx, H):
+    mb = 4096
+    kernel = "rowpass_kernel<256, 16, 32, kx>" if H == 256 else "rowpass_kernel<64, 4, 32, fused dW2>"
+    fetch = os.path.join(d, "pmc_fetch" + sfx, "run_counter_collection.csv")
+    write = os.path.join(d, "pmc_write" + sfx, "run_counter_collection.csv")
+    if os.path.exists(fetch) and os.path.exists(write):
+        f_kb, nf = pmc_per_dispatch(fetch, "rowpass_kernel", "FETCH_SIZE")
+        w_kb, nw = pmc_per_dispatch(write, "rowpass_kernel", "WRITE_SIZE")
+        res = {"kernel": kernel, "hidden": H, "minibatch": mb,
+               "dispatches": [nf, nw], "FETCH_SIZE_kB_median": f_kb, "WRITE_SIZE_kB_median": w_kb,
+               "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
+               "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
+               "workload": f"tools/rowpass_workload.py 40 {H} {mb}"}
+        with open(os.path.join(prof, f"{tag}_rowpass{sfx}_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
+    mfma = os.path.join(d, "pmc_mfma" + sfx, "run_counter_collection.csv")
+    if os.path.exists(mfma):
+        # SQ_VALU_MFMA_BUSY_CYCLES sums each MFMA's busy cycles on its SIMD over the
+        # chip; GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs (MI355X_MICROARCH.md),
+        # so one XCD's span is /8
+        busy, nb = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
+        grbm, ng = pmc_per_dispatch(mfma, "rowpass_kernel", "GRBM_GUI_ACTIVE")
+        sqb, ns = pmc_per_dispatch(mfma, "rowpass_kernel", "SQ_BUSY_CYCLES")
+        n_f32, n_bf16 = rowpass_mfma_counts(H, mb)
+        busy_expected = 32 * n_f32 + 16 * n_bf16
+        res = {"kernel": kernel, "hidden": H, "minibatch": mb, "dispatches": [nb, ng, ns],
+               "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
+               "SQ_BUSY_CYCLES_median": sqb,
+               "xcd_cycles": grbm / 8.0 if grbm else None,
+               "mfma_busy_frac": busy / (grbm / 8.0 * 1024) if busy and grbm else None,
+               "mfma_instructions_per_launch": n_f32 + n_bf16,
+               "mfma_f32_16x16x4_per_launch": n_f32, "mfma_bf16_16x16x32_per_launch": n_bf16,
+               "busy_cycles_expected": busy_expected,
+               "busy_over_expected": busy / busy_expected if busy else None,
+               "definition": MFMA_DEF, "workload": f"tools/rowpass_workload.py 40 {H} {mb}"}
+        with open(os.path.join(prof, f"{tag}_rowpass{sfx}_mfma_pmc.json"), "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res))
+
+
+def policy_summary(d, tag, prof, sfx, H, n):
+    """The rollout's policy kernel (both agents' forward, n rows each; 32-row
+    workgroups).  H 256: 8 waves, each 2 row tiles x 2 column tiles: fc1 (K
+    padded to 32) 32 f32 per wave, fc2 as split-bf16 8 chunks x 4 tiles x 6 =
+    192 per wave.  H 64: 4 waves, one column tile each: fc1 16, fc2 2 chunks x
+    16 = 48 f32 per wave."""
+    pol = os.path.join(d, "pmc_policy_mfma" + sfx, "run_counter_collection.csv")
+    if not os.path.exists(pol):
+        return
+    busy, nb = pmc_per_dispatch(pol, "policy_kernel", "SQ_VALU_MFMA_BUSY_CYCLES")
+    grbm, ng = pmc_per_dispatch(pol, "policy_kernel", "GRBM_GUI_ACTIVE")
+    wgs = 2 * (n // 32)
+    n_f32, n_bf16 = (wgs * 8 * 32, wgs * 8 * 192) if H == 256 else (wgs * 4 * 48, 0)
+    busy_expected = 32 * n_f32 + 16 * n_bf16
+    nw = 8 if H == 256 else H // 16
+    res = {"kernel": f"policy_kernel<{H}, {nw}, 0>", "hidden": H, "num_envs": n, "agents": 2,
+           "dispatches": [nb, ng], "SQ_VALU_MFMA_BUSY_CYCLES_median": busy, "GRBM_GUI_ACTIVE_median": grbm,
+           "xcd_cycles": grbm / 8.0 if grbm else None,
+           "mfma_busy_frac": busy / (grbm / 8.0 * 1024) if busy and grbm else None,
+           "mfma_instructions_per_launch": n_f32 + n_bf16, "busy_cycles_expected": busy_expected,
+           "busy_over_expected": busy / busy_expected if busy else None,
+           "definition": MFMA_DEF, "workload": f"tools/policy_workload.py 40 {H} {n}"}
+    with open(os.path.join(prof, f"{tag}_policy{sfx}_mfma_pmc.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
 
 
 def env_extra(d, tag, prof):
