@@ -3,7 +3,8 @@
 minibatch step for FusedMinibatch variants side by side (constructor
 keywords), replaying the update's graphs over a 16-minibatch epoch.
 Usage: python tools/step_ab.py H mb variant[,variant...] [reps]
-  variants: "product" (defaults), or key=value pairs joined by '+', e.g. kx=0"""
+  variants: "product" (defaults), or key=value pairs joined by '+': FusedMinibatch
+  keywords (e.g. split_chains=1), or S=<n> to run the dW2 split-K n ways"""
 import os
 import sys
 
@@ -28,7 +29,10 @@ def time_variant(H, mb, kw, n=20):
     g = torch.Generator(device="cuda").manual_seed(0)
     src = torch.randn((B, 32), device="cuda", generator=g)
     src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+    S = kw.pop("S", None)
     st = FusedMinibatch(L, mb, 16, **kw)
+    if S is not None:                       # (a valid split count: no empty split, <= the slab capacity)
+        st.S = S
     perm = torch.randperm(B, device="cuda", generator=g)
     L.sync_w2t()
     for _ in range(3):
