@@ -1307,9 +1307,13 @@ int dw2_splits(int H, int mb, int net) {
 // A chunk sums slabs c, c+CH, ... in that order, every load issued before the
 // first add (one latency round), then chunk 0 adds the CH partials in order.
 // ---------------------------------------------------------------------------
-struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net; };   // net: -1 both, 0 actor, 1 critic
+struct RedGeom { int nb2, nb1, nbt, S, nw1, nwg, net, ch2; };   // net: -1 both, 0 actor, 1 critic
 __host__ __device__ inline int n_blocks_dev(const RedGeom& g) { return g.nb2 + g.nb1 + g.nbt; }
-constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4;   // chunks per column: W1, tail, W2 regions
+// chunks per column: W1, tail, W2 regions; the W2 region at H = 64 takes
+// kRedCH2x chunks (its 128 one-block dW2 slabs per minibatch: 8 per thread,
+// one load round, 16 float4 columns per block, 4x the blocks)
+constexpr int kRedCH1 = 8, kRedCHt = 32, kRedCH2 = 4, kRedCH2x = 16;
+__host__ __device__ inline int red_ch2(int H) { return H == 64 ? kRedCH2x : kRedCH2; }
 
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -1480,14 +1484,15 @@ __device__ __forceinline__ void reduce_block(int H, const Layout& L, const RedGe
   const int t = threadIdx.x;
   const int64_t HH4 = (int64_t)H * H / 4;
   if (b < g.nb2) {                                                // W2: [2][S] split-K slabs of H*H
-    constexpr int EB = 256 / kRedCH2;
+    const int EB = 256 / g.ch2;
     const int64_t col = (g.net > 0 ? HH4 : 0) + (int64_t)b * EB + (t % EB);
     const bool valid = col < (g.net < 0 ? 2 : g.net + 1) * HH4, lead = t < EB;
     const int net = col >= HH4;                                   // EB divides HH4: one net per block
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mode & 1) {
-      v = chunk_sum4<kRedCH2>(reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4, HH4, g.S,
-                              col - net * HH4, valid, red);
+      const float4* p2n = reinterpret_cast<const float4*>(p2) + (int64_t)net * g.S * HH4;
+      v = g.ch2 == kRedCH2x ? chunk_sum4<kRedCH2x>(p2n, HH4, g.S, col - net * HH4, valid, red)
+                            : chunk_sum4<kRedCH2>(p2n, HH4, g.S, col - net * HH4, valid, red);
       if (lead && valid) G4[col] = v;
     } else if (lead && valid) {
       v = G4[col];
@@ -1714,7 +1719,8 @@ RedGeom geom(int H, int mb, int S, int net = -1) {
   const Layout L = layout(H);
   const int nn = net < 0 ? 2 : 1;                                  // nets covered
   RedGeom g;
-  g.nb2 = (int)((nn * (int64_t)H * H / 4 + (256 / kRedCH2) - 1) / (256 / kRedCH2));
+  g.ch2 = red_ch2(H);
+  g.nb2 = (int)((nn * (int64_t)H * H / 4 + (256 / g.ch2) - 1) / (256 / g.ch2));
   g.nb1 = (int)((nn * (int64_t)H * 20 / 4 + (256 / kRedCH1) - 1) / (256 / kRedCH1));
   g.nbt = (int)((L.tail / 4 + (256 / kRedCHt) - 1) / (256 / kRedCHt));
   g.S = S;
@@ -1799,7 +1805,7 @@ __device__ __forceinline__ float peer_pull(const unsigned long long* base, int64
 
 // the float4 of G reduce_dp's block rb hands thread t (its lead threads), or -1
 __device__ __forceinline__ int64_t peer_col(const Layout& L, const RedGeom& g, int H, int rb, int t) {
-  if (rb < g.nb2) return t < 256 / kRedCH2 ? (int64_t)rb * (256 / kRedCH2) + t : -1;
+  if (rb < g.nb2) return t < 256 / g.ch2 ? (int64_t)rb * (256 / g.ch2) + t : -1;
   if (rb < g.nb2 + g.nb1) {
     const int64_t c = (int64_t)(rb - g.nb2) * (256 / kRedCH1) + t;
     return t < 256 / kRedCH1 && c < 2LL * H * 20 / 4 ? L.W1 / 4 + c : -1;
