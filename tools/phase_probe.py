@@ -111,10 +111,9 @@ def t(fn, n=200):
 
 
 nsq = st.nsq[0]
-print("dW2 solution index", st.dw2_algo if st.lib_gemm else "dw2_kernel")
 res = {
-    "rowpass": t(lambda: st.rowpass(src, None)),
-    "dw2": t(lambda: st._dw2(H1, dZ2, mb, S, -1)),
+    "rowpass": t(lambda: st.rowpass_kx(src, None) if st.kx(mb) else st.rowpass(src, None)),
+    "dw2": t(lambda: st.dw2_kx(mb, S) if st.kx(mb) else st._dw2(H1, dZ2, mb, S, -1)),
     "reduce": t(lambda: lib.satrl_ppo_reduce(H, mb, -1, S, 3, _L.ptr(st.p2), _L.ptr(st.pw1), _L.ptr(st.ptail),
                                              _L.ptr(L.G), _L.ptr(nsq), _L.ptr(L.steps), sp)),
     "adam": t(lambda: lib.satrl_ppo_adam(H, mb, -1, _L.ptr(nsq), _L.ptr(L.steps), _L.ptr(L.bct), L.bct.shape[0],
