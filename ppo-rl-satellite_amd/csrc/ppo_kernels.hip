@@ -319,7 +319,7 @@ __device__ __forceinline__ void mfma_rows(const float* __restrict__ A, const flo
 // / sum|a*b| max 2.2e-7, mean 1.3e-8 against 2.9e-7 / 1.7e-8 for the f32
 // MFMA chain.  The A operand (activations, written once per row block) goes
 // to LDS as three bf16 planes; the B operand (fc2.weight / its transpose,
-// read once per workgroup from L2) stays f32 and is split in registers, 44
+// read once per workgroup from L2) stays f32 and is split in registers, 36
 // VALU per 32-wide k chunk beside its 12 MFMAs.  The 16x16x32 operand layout
 // (lane l: row / column l & 15, k = 8 (l >> 4) + j) is the f32 path's k
 // mapping, and its accumulator layout the 16x16x4's, so nothing else changes.
@@ -346,12 +346,29 @@ __device__ __forceinline__ unsigned pk_bf16(f2v x) { return __builtin_bit_cast(u
 __device__ __forceinline__ f2v unpk_bf16(unsigned p) {
   return f2v{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
 }
-// split3 on a pair, packed: 9 VALU per pair (the residuals as packed f32 subtractions)
+// x - (the bf16 pair p, widened), per lane half, as one v_dot2c_f32_bf16 each
+// (p . (-1, 0) + x.x and p . (0, -1) + x.y): the difference is exact in f32
+// (p is x rounded to bf16), so the dot's single rounding returns it unchanged
+// -- two VALU where widening p and a packed subtraction take three
+// The (-1, 0) / (0, -1) operands go through SGPRs: the compiler encodes
+// (-1, 0) as the inline constant -1.0, which the instruction reads as the f32
+// pattern (0, -1) -- the wrong half (tools/_probe/dot2/dot2_exact.hip).
+__device__ __forceinline__ bf2v sgpr_bf16x2(unsigned bits) {
+  unsigned r;
+  asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(bits));
+  return __builtin_bit_cast(bf2v, r);
+}
+__device__ __forceinline__ f2v resid_bf16(f2v x, unsigned p) {
+  const bf2v pv = __builtin_bit_cast(bf2v, p);
+  return f2v{__builtin_amdgcn_fdot2_f32_bf16(pv, sgpr_bf16x2(0x0000bf80u), x.x, false),
+             __builtin_amdgcn_fdot2_f32_bf16(pv, sgpr_bf16x2(0xbf800000u), x.y, false)};
+}
+// split3 on a pair, packed: 7 VALU per pair (3 v_cvt_pk_bf16_f32, 4 v_dot2c_f32_bf16)
 __device__ __forceinline__ void split3x2(f2v x, unsigned& h, unsigned& m, unsigned& l) {
   h = pk_bf16(x);
-  const f2v r = x - unpk_bf16(h);
+  const f2v r = resid_bf16(x, h);
   m = pk_bf16(r);
-  const f2v q = r - unpk_bf16(m);
+  const f2v q = resid_bf16(r, m);
   l = pk_bf16(q);
 }
 __device__ __forceinline__ void split3x8(const float4 (&x)[2], s8v (&o)[3]) {
