@@ -352,7 +352,7 @@ __device__ __forceinline__ f2v unpk_bf16(unsigned p) {
 // -- two VALU where widening p and a packed subtraction take three
 // The (-1, 0) / (0, -1) operands go through SGPRs: the compiler encodes
 // (-1, 0) as the inline constant -1.0, which the instruction reads as the f32
-// pattern (0, -1) -- the wrong half (tools/_probe/dot2/dot2_exact.hip).
+// pattern (0, -1) -- the wrong half (tools/dot2_exact.hip).
 __device__ __forceinline__ bf2v sgpr_bf16x2(unsigned bits) {
   unsigned r;
   asm("s_mov_b32 %0, %1" : "=s"(r) : "i"(bits));
