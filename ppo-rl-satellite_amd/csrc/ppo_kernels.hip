@@ -546,7 +546,13 @@ template <int H, int NW, int RR = kRows>
 struct MlpSmem {
   static constexpr bool BF3 = kBf3<H>;
   static constexpr int R = RR, LDA = H + 4, LDS_S = 36;
-  static constexpr int LDP = H + 8, PS = R * LDP;     // bf16 planes: rows padded by 16 B
+  // bf16 planes: rows padded by 32 B, a row stride of 8 banks (mod 64): the
+  // 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...) of an
+  // MFMA operand read (row i, 16-B column run g) then land on 16 distinct
+  // 4-bank slots (8i + 4g mod 64).  A 16-B pad (4 banks) put two lanes of
+  // every group on one slot: SQ_LDS_BANK_CONFLICT 1.67 M -> 0.49 M per
+  // rowpass (tools/lds_conflict_ab.sh), bitwise the same, no faster
+  static constexpr int LDP = H + 16, PS = R * LDP;
   float h1s[BF3 ? 0 : R][LDA] __attribute__((aligned(16)));                // tanh(fc1)
   unsigned short h1p[BF3 ? 3 * PS : 0] __attribute__((aligned(16)));      // (BF3) its three bf16 planes
   float S[R][LDS_S] __attribute__((aligned(16)));     // [s(18) | 1 | 0...] per row
@@ -737,7 +743,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
   constexpr bool BF3 = kBf3<H>;
-  constexpr int LDP = H + 8, PS = R * LDP;
+  constexpr int LDP = MlpSmem<H, NW, R>::LDP, PS = MlpSmem<H, NW, R>::PS;
   __shared__ __attribute__((aligned(16))) float dzs[BF3 ? 1 : R][BF3 ? 4 : LDA];   // dZ2
   __shared__ __attribute__((aligned(16))) unsigned short dzp[BF3 ? 3 * PS : 8];    // (BF3) its bf16 planes
   __shared__ float ax[R][8];
