@@ -83,13 +83,6 @@ int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* step
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
                    float* P, float* M, float* V, void* W2X /* nullable: also refresh the fc2 operand image */,
                    void* stream);
-/* The same step reading the state from Pin / Min / Vin and writing it to P /
- * M / V (either the same buffers, as satrl_ppo_adam, or other ones: the end
- * of a folded-Adam group, satrl_ppo_rowpass_dw2_adam below).               */
-int satrl_ppo_adam_to(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
-                      const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip,
-                      const float* G, const float* Pin, const float* Min, const float* Vin, float* P, float* M,
-                      float* V, void* W2X, void* stream);
 
 /* The fc2 operand image W2X the rowpass reads for its two H x H products
  * (and satrl_ppo_adam keeps current), satrl_ppo_w2x_floats(H) floats: the
@@ -134,25 +127,6 @@ int satrl_ppo_row_blocks(int H, int mb);
 int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
                           const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
                           float* pw1, void* stream);
-
-/* H = 64: satrl_ppo_rowpass_dw2 with the PREVIOUS minibatch's Adam step
- * (satrl_ppo_adam's arguments; its minibatch had mb_prev rows) folded into
- * the launch.  Every workgroup computes its net's whole update in its own
- * LDS (the same instructions on the same inputs as satrl_ppo_adam: the
- * same bits), runs the step on it, and writes its share of the new state
- * to Pout / Mout / Vout -- buffers other than Pin / Min / Vin, which other
- * workgroups of the launch still read.  A run of minibatches is then
- * rowpass_dw2, reduce, {rowpass_dw2_adam, reduce} ..., satrl_ppo_adam_to
- * (state alternating between two buffer sets): two launches per step
- * instead of three.  The fc2 operand image is not read (the step builds
- * its own from the updated weights) and not written (satrl_ppo_adam_to at
- * the end of the run refreshes it).                                         */
-int satrl_ppo_rowpass_dw2_adam(int H, int mb, int net, const float* src, const int64_t* idx, float epsilon,
-                               float ent_coef, float max_action, float* p2, float* ptail, float* pw1, int mb_prev,
-                               const double* nsq, const double* steps, const double* bct, int bct_len,
-                               const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip,
-                               const float* G, const float* Pin, const float* Min, const float* Vin, float* Pout,
-                               float* Mout, float* Vout, void* stream);
 
 /* H = 256, every minibatch (32-row workgroups above 1024 rows, 16-row ones
  * up to it): the rowpass with H1 and dZ2 written as k-packed bf16 planes (each element split hi + mid +

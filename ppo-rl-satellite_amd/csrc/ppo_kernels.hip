@@ -565,20 +565,15 @@ struct MlpSmem {
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
 // tanh(fc1) goes to h1out[r * H + n].
-// The parameters: Q[o - L.W1] is the flat layout's element o >= L.W1 (W1,
-// the fc2 bias, the output layers) and W2 this net's fc2.weight rows (row
-// stride LDW).  LATE: they are read after the gather's barrier (an LDS image
-// that gather() itself writes: the folded Adam step, rowpass_kernel ADAM).
-template <int H, int NW, int R, bool APRE, int LDW = H, bool LATE = false, class Gather>
-__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ Q,
-                                            const float* __restrict__ W2, int net, int nvalid,
+template <int H, int NW, int R, bool APRE, class Gather>
+__device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P,
+                                            int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
                                             f4 (&acc)[R / 16][H / 16 / NW],
                                             float (&h1)[R / 16][H / 16 / NW][4],
                                             float (&w3)[H / 16 / NW][3]) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
   static_assert(CT >= 1 && H % (16 * NW) == 0, "tile split");
-  static_assert(LDW == H || !kBf3<H>, "the split-bf16 fc2 streams W2 at stride H");
   const Layout L = layout(H);
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
   const int n0 = w * (H / NW);
@@ -594,8 +589,8 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   // issued after the gather would hold up the barrier below
   float4 w1raw[CT][2];
   float b2v[CT], w3raw[CT][3];
-  auto load_w = [&] {
-    const float* W1 = Q + (int64_t)net * H * 20;
+  {
+    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
     const int o0 = lg < 2 ? 8 * lg : 16, o1 = lg < 2 ? 8 * lg + 4 : 16;
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
@@ -603,13 +598,12 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
       const float* bp = W1 + (int64_t)n * 20;
       w1raw[t][0] = *reinterpret_cast<const float4*>(bp + o0);
       w1raw[t][1] = *reinterpret_cast<const float4*>(bp + o1);
-      b2v[t] = Q[L.b2 - L.W1 + net * H + n];
-      w3raw[t][0] = Q[(net == 0 ? L.W3a : L.W3c) - L.W1 + n];
-      w3raw[t][1] = Q[L.W3a - L.W1 + H + n];
-      w3raw[t][2] = Q[L.W3a - L.W1 + 2 * H + n];
+      b2v[t] = P[L.b2 + net * H + n];
+      w3raw[t][0] = P[(net == 0 ? L.W3a : L.W3c) + n];
+      w3raw[t][1] = P[L.W3a + H + n];
+      w3raw[t][2] = P[L.W3a + 2 * H + n];
     }
-  };
-  if constexpr (!LATE) load_w();
+  }
   gather(tid, NT);
   for (int q = tid; q < R * (LDS_S - 18); q += NT) {
     const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
@@ -618,11 +612,10 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
   PHASE_PROBE(8);
   rp_barrier();
   PHASE_PROBE(9);
-  if constexpr (LATE) load_w();
   // (split-bf16 fc2) phase B's first weight chunks go out now, under fc1 (an
   // LDS-only barrier below, leaving them in flight, measured no faster)
   WPre<CT> preB;
-  if constexpr (kBf3<H>) mfma_rows_pre<H, CT>(W2, n0, preB);
+  if constexpr (kBf3<H>) mfma_rows_pre<H, CT>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   float4 bw1[CT][2];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -661,9 +654,10 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 
   // ---- B: Z2 = H1 W2^T -------------------------------------------------------
   if constexpr (kBf3<H>)
-    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, true>(sm.h1p, W2, n0, acc, &preB);
+    mfma_rows3<H, MlpSmem<H, NW, R>::LDP, MlpSmem<H, NW, R>::PS, H, RT, CT, true>(
+        sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   else
-    mfma_rows<H, LDA, LDW, RT, CT, APRE>(&sm.h1s[0][0], W2, n0, acc);
+    mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -731,33 +725,16 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
   return od;
 }
 
-// The previous minibatch's Adam step folded into a rowpass launch (ADAM;
-// satrl_ppo_rowpass_dw2_adam): adam_kernel's inputs, with the parameter
-// state read from Pin / Min / Vin and written to Pout / Mout / Vout (two
-// buffers: other workgroups of the launch still read the old state)
-struct AdamIn {
-  const float *G, *Pin, *Min, *Vin;
-  float *Pout, *Mout, *Vout;
-  const double *nsq, *steps, *bct;
-  const float* lr;
-  int nblk, bct_len, use_clip;
-  float beta1, beta2, eps, max_norm;
-};
-template <int H, int LDW>
-__device__ void rp_adam(const AdamIn& ad, int net, int rb, int nrb, float (*w2s)[LDW], float (*w2ts)[LDW],
-                        float* qs, float* hb3s, float (*hcs)[3], double* sh);
-
-template <int H, int NW, int R = kRows, bool FDW2 = false, bool KX = false, bool ADAM = false>
+template <int H, int NW, int R = kRows, bool FDW2 = false, bool KX = false>
 __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const void* __restrict__ W2X, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1, int net_sel, float* __restrict__ p2,
-                                                      int S2, float* __restrict__ ratio_out, AdamIn ad) {
+                                                      int S2, float* __restrict__ ratio_out) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
-  static_assert(!ADAM || (H == 64 && NT == 256 && FDW2), "the folded Adam step: H = 64's rowpass_dw2");
   // KX: H1 / dZ2 go out as k-packed bf16 planes (store_kx; H1g / dZ2g point at
   // u16 [2][3][kx_rows(mb)][H]) for satrl_ppo_dw2_kx, whole 32-row chunks (a
   // 16-row kernel's last block zero-fills the chunk's other half)
@@ -771,13 +748,6 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   __shared__ __attribute__((aligned(16))) unsigned short dzp[BF3 ? 3 * PS : 8];    // (BF3) its bf16 planes
   __shared__ float ax[R][8];
   __shared__ float dz3s[R][4];
-  // (ADAM) this net's updated parameters: fc2.weight and its transpose (rows
-  // padded by 16 B) and the flat layout from W1 on (Q of mlp_forward)
-  constexpr int LDW = ADAM ? H + 4 : H;
-  __shared__ __attribute__((aligned(16))) float w2s[ADAM ? H : 1][LDW];
-  __shared__ __attribute__((aligned(16))) float w2ts[ADAM ? H : 1][LDW];
-  __shared__ __attribute__((aligned(16))) float qs[ADAM ? 46 * H + 12 : 4];   // layout(H).total - .W1
-  __shared__ double ash[8];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
   // net_sel < 0: both nets, blockIdx = (row block, net); else that net only
   const int net = net_sel < 0 ? (int)(blockIdx.x & 1) : net_sel;
@@ -803,7 +773,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   __shared__ float hb3s[4];                                        // b3a[0..2], b3c
   const int hd = tid - (NT - 64);                                  // head-scalar lane of the last wave
   float hls_d = 0.0f, hb3_d = 0.0f;
-  if (!ADAM && hd >= 0 && hd < 4) {
+  if (hd >= 0 && hd < 4) {
     hb3_d = P[hd < 3 ? L.b3a + hd : L.b3c];
     hls_d = P[L.ls + (hd < 3 ? hd : 0)];
   }
@@ -813,10 +783,6 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   float w3[CT][3];
   auto gather = [&](int t0, int nt) {
     auto head_consts = [&] {
-      if constexpr (ADAM) {                      // (rp_adam computes them from the updated values)
-        rp_adam<H, LDW>(ad, net, rb, S2, w2s, w2ts, qs, hb3s, hcs, ash);
-        return;
-      }
       // (opaque to the compiler and ordered after the row loads: otherwise it
       // hoists this arithmetic next to its loads at the top of the kernel,
       // and the whole wave waits for them before issuing any row load)
@@ -864,10 +830,8 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   const float* W2T = static_cast<const float*>(W2X);
   // (H = 256: the H1 store after phase B, not between fc1 and B: 8 fewer VGPRs
   // live through B, so the 32-row kernel stays at <= 104)
-  const float* Qp = ADAM ? qs : P + L.W1;
-  const float* W2p = ADAM ? &w2s[0][0] : P + L.W2 + (int64_t)net * H * H;
-  mlp_forward<H, NW, R, true, LDW, ADAM>(sm, Qp, W2p, net, mb - r0, gather,
-                                         FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather,
+                                   FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   if constexpr (KX) {
     store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
@@ -879,9 +843,8 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   }
   else if constexpr (BF3 && !FDW2) store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, h1);
   // phase D's first W2T chunks go out now, under the loss head and the tail
-  const float* W2Tp = ADAM ? &w2ts[0][0] : W2T + (int64_t)net * H * H;
   WPre<CT> preD;
-  mfma_rows_pre<LDW, CT>(W2Tp, n0, preD);
+  mfma_rows_pre<H, CT>(W2T + (int64_t)net * H * H, n0, preD);
 
   // ---- C: the net's loss and its gradient, dZ2 ---------------------------------
   if (tid < R) {
@@ -1024,7 +987,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   if constexpr (BF3)
     mfma_rows3<H, LDP, PS, H, RT, CT, true>(dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
   else
-    mfma_rows<H, LDA, LDW, RT, CT, true, true>(&dzs[0][0], W2Tp, n0, acc, &preD);
+    mfma_rows<H, LDA, H, RT, CT, true, true>(&dzs[0][0], W2T + (int64_t)net * H * H, n0, acc, &preD);
   PHASE_PROBE(6);
 
   // ---- E: dZ1 = dH1 (1 - H1^2); [dW1 | db1][n][k'] = sum_r dZ1[r][n] S[r][k'] ----
@@ -1142,8 +1105,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW, R, false>(sm, P + L.W1, P + L.W2 + (int64_t)(MODE == 0 ? 0 : 1) * H * H, MODE == 0 ? 0 : 1,
-                               nvalid, gather, nullptr, acc, h1, w3);
+  mlp_forward<H, NW, R, false>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
@@ -1640,161 +1602,14 @@ __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p,
   const float denom = sqrtf(v) / bc2s + eps;
   return p + (-step_size) * (m / denom);                           // addcdiv_(m, denom, -step_size)
 }
-__device__ __forceinline__ float4 adam4(float4 g, float4& m, float4& v, float4 p, float coef, float ss, float b2s,
-                                        float w1, float w2, float beta2, float eps, int use_clip) {
-  float4 pn;
-  pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  pn.z = adam_elem(g.z, m.z, v.z, p.z, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  pn.w = adam_elem(g.w, m.w, v.w, p.w, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  return pn;
-}
-// the per-block squared norms (nblk pairs {actor, critic}), loads first ...
-__device__ __forceinline__ void norm_loads(const double* __restrict__ nsq, int nblk, double2 (&pn2)[4]) {
-  const double2* nsq2 = reinterpret_cast<const double2*>(nsq);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) pn2[i] = nsq2[min((int)threadIdx.x + 256 * i, nblk - 1)];
-}
-// ... then folded, k = t, t + 256, ... in order and the block sum: the same
-// bits in every thread of every block
-__device__ __forceinline__ void norm_fold(const double* __restrict__ nsq, int nblk, const double2 (&pn2)[4],
-                                          double& a, double& c, double* sh) {
-  const int t = threadIdx.x;
-  a = 0.0; c = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {                                    // k = t, t+256, ... in order, as the loop
-    // x * 1.0 == x, x * 0.0 + a == a for these non-negative sums: bitwise the
-    // loop's skip, without a branch the compiler would sink the load into
-    const double in = t + 256 * i < nblk ? 1.0 : 0.0;
-    a += pn2[i].x * in;
-    c += pn2[i].y * in;
-  }
-  if (nblk > 1024) {                                               // (not at the sizes in use)
-    for (int k = t + 1024; k < nblk; k += 256) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
-  }
-  block_sum2(a, c, sh);
-}
-// one net's clip coefficient, step size and sqrt bias correction from its
-// squared norm nn, step count st and bias-correction row bc
-__device__ __forceinline__ void adam_consts(double nn, int st, double2 bc, int bct_len, float lrv, float max_norm,
-                                            int use_clip, float& coef, float& ss, float& b2s) {
-  const float nrm = (float)sqrt(nn);
-  coef = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
-  // bct[2*step] = 1 - beta1**step, bct[2*step+1] = sqrt(1 - beta2**step) (python float
-  // math, as torch.optim.Adam computes them); constant 1.0 past the table
-  const double bc1 = st < bct_len ? bc.x : 1.0;
-  const double bc2s = st < bct_len ? bc.y : 1.0;
-  ss = (float)((double)lrv / bc1);
-  b2s = (float)bc2s;
-}
-// (sqrtf / 1.0f / expf / logf as adam_kernel and the rowpass head constants)
-
-// rp_adam: the folded Adam step of one rowpass workgroup (rowpass_kernel
-// ADAM, H = 64, 256 threads).  Every workgroup of the net computes the whole
-// net's update -- the same instructions on the same inputs as adam_kernel,
-// so the same bits -- into its LDS images (fc2.weight, its transpose, the
-// flat layout from W1 on, the head's constants), and writes its share of
-// Pout / Mout / Vout (the net's float4s u with u % nrb == rb).  Every thread
-// of the workgroup calls it (one barrier, in the norm fold).
-template <int H, int LDW>
-__device__ void rp_adam(const AdamIn& ad, int net, int rb, int nrb, float (*w2s)[LDW], float (*w2ts)[LDW],
-                        float* qs, float* hb3s, float (*hcs)[3], double* sh) {
-  constexpr int NT = 256, N2 = H * H / 4, N1 = H * 20 / 4;
-  constexpr int S2 = N2 / NT, S1 = (N1 + NT - 1) / NT;             // float4 slots per thread: fc2, W1
-  static_assert(N2 % NT == 0, "fc2 float4s per thread");
-  constexpr int NS = S2 + S1 + 1;                                  // + one slot of the tail region
-  const Layout L = layout(H);
-  const int t = threadIdx.x;
-  static_assert((6 * H + 12) / 4 <= NT, "one tail float4 per thread (layout(H).tail = 6H + 12)");
-  double2 pn2[4];
-  norm_loads(ad.nsq, ad.nblk, pn2);
-  int64_t e4[NS];
-  int u[NS];
-  bool ok[NS];
-#pragma unroll
-  for (int i = 0; i < S2; ++i) {
-    u[i] = t + NT * i;
-    e4[i] = (int64_t)net * N2 + u[i];
-    ok[i] = true;
-  }
-#pragma unroll
-  for (int i = 0; i < S1; ++i) {
-    const int j = t + NT * i;
-    u[S2 + i] = N2 + j;
-    ok[S2 + i] = j < N1;
-    e4[S2 + i] = L.W1 / 4 + (int64_t)net * N1 + (j < N1 ? j : 0);
-  }
-  {
-    const int64_t e = L.b2 / 4 + t;
-    ok[NS - 1] = t < L.tail / 4 && net_of(L, e * 4, H) == net;
-    u[NS - 1] = N2 + N1 + t;
-    e4[NS - 1] = ok[NS - 1] ? e : L.b2 / 4;
-  }
-  const float4* G4 = reinterpret_cast<const float4*>(ad.G);
-  const float4* Pi4 = reinterpret_cast<const float4*>(ad.Pin);
-  const float4* Mi4 = reinterpret_cast<const float4*>(ad.Min);
-  const float4* Vi4 = reinterpret_cast<const float4*>(ad.Vin);
-  float4 g[NS], m[NS], v[NS], p[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    g[i] = G4[e4[i]];
-    m[i] = Mi4[e4[i]];
-    v[i] = Vi4[e4[i]];
-    p[i] = Pi4[e4[i]];
-  }
-  const double st = ad.steps[net];
-  const float lrv = ad.lr[net];
-  const int k = (int)st;
-  const double2 bc = reinterpret_cast<const double2*>(ad.bct)[k < ad.bct_len ? k : ad.bct_len - 1];
-  double a, c;
-  norm_fold(ad.nsq, ad.nblk, pn2, a, c, sh);
-  float coef, ss, b2s;
-  adam_consts(net == 0 ? a : c, k, bc, ad.bct_len, lrv, ad.max_norm, ad.use_clip, coef, ss, b2s);
-  const float w1 = (float)(1.0 - (double)ad.beta1);                // lerp weight 1 - beta1
-  const float w2 = (float)(1.0 - (double)ad.beta2);
-  float4* Po4 = reinterpret_cast<float4*>(ad.Pout);
-  float4* Mo4 = reinterpret_cast<float4*>(ad.Mout);
-  float4* Vo4 = reinterpret_cast<float4*>(ad.Vout);
-#pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    if (!ok[i]) continue;
-    const float4 pn = adam4(g[i], m[i], v[i], p[i], coef, ss, b2s, w1, w2, ad.beta2, ad.eps, ad.use_clip);
-    if (u[i] % nrb == rb) {
-      Po4[e4[i]] = pn;
-      Mo4[e4[i]] = m[i];
-      Vo4[e4[i]] = v[i];
-    }
-    if (i < S2) {                                                  // fc2.weight (n, k..k+3) and transposed
-      const int f = 4 * u[i], n = f / H, kk = f % H;
-      *reinterpret_cast<float4*>(&w2s[n][kk]) = pn;
-      w2ts[kk][n] = pn.x; w2ts[kk + 1][n] = pn.y; w2ts[kk + 2][n] = pn.z; w2ts[kk + 3][n] = pn.w;
-    } else {
-      const int64_t o = e4[i] * 4;
-      *reinterpret_cast<float4*>(qs + (o - L.W1)) = pn;
-      // the head's constants, as the rowpass's head_consts computes them from P
-      if (o == L.b3a) { hb3s[0] = pn.x; hb3s[1] = pn.y; hb3s[2] = pn.z; }
-      if (o == L.b3c) hb3s[3] = pn.x;
-      if (o == L.ls) {
-        const float ls3[3] = {pn.x, pn.y, pn.z};
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const float sd = expf(ls3[d]), var = sd * sd;
-          hcs[0][d] = var;
-          hcs[1][d] = logf(sd);
-          hcs[2][d] = 1.0f / var;
-        }
-      }
-    }
-  }
-}
 
 __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double* __restrict__ nsq,
                                                    const double* __restrict__ steps, const double* __restrict__ bct,
                                                    int bct_len, const float* __restrict__ lr, float beta1,
                                                    float beta2, float eps, float max_norm, int use_clip,
-                                                   const float* __restrict__ G, const float* Pin,
-                                                   const float* Min, const float* Vin, float* Pout, float* Mout,
-                                                   float* Vout, void* __restrict__ W2X, int net_sel) {
+                                                   const float* __restrict__ G, float* __restrict__ P,
+                                                   float* __restrict__ M, float* __restrict__ V,
+                                                   void* __restrict__ W2X, int net_sel) {
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float tile[32][33];
@@ -1819,20 +1634,18 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   // behind them: the fold below waits only for the partials (vmcnt is in
   // order), so the operand latency overlaps the fold
   // (all loads unconditional on clamped indices, so none becomes a branch)
+  const double2* nsq2 = reinterpret_cast<const double2*>(nsq);
   double2 pn2[4];
-  norm_loads(nsq, nblk, pn2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pn2[i] = nsq2[min(t + 256 * i, nblk - 1)];
   const float4* G4 = reinterpret_cast<const float4*>(G);
-  // (in place, or from the shadow state of a folded-Adam group: Pin != Pout)
-  const float4* Pi4 = reinterpret_cast<const float4*>(Pin);
-  const float4* Mi4 = reinterpret_cast<const float4*>(Min);
-  const float4* Vi4 = reinterpret_cast<const float4*>(Vin);
-  float4* Po4 = reinterpret_cast<float4*>(Pout);
-  float4* Mo4 = reinterpret_cast<float4*>(Mout);
-  float4* Vo4 = reinterpret_cast<float4*>(Vout);
+  float4* P4 = reinterpret_cast<float4*>(P);
+  float4* M4 = reinterpret_cast<float4*>(M);
+  float4* V4 = reinterpret_cast<float4*>(V);
   const int64_t el = live ? e4 : 0;
   const float4 g = G4[el];
-  float4 m = Mi4[el], v = Vi4[el];
-  const float4 p = Pi4[el];
+  float4 m = M4[el], v = V4[el];
+  const float4 p = P4[el];
   // both nets' step counts, learning rates and bias-correction rows, issued
   // here too: after the fold (a barrier the compiler does not hoist loads
   // over) they were two dependent load round trips on the kernel's path
@@ -1841,20 +1654,46 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   const int ka = (int)st_a, kc = (int)st_c;
   const double2* bct2 = reinterpret_cast<const double2*>(bct);
   const double2 bca = bct2[ka < bct_len ? ka : bct_len - 1], bcc = bct2[kc < bct_len ? kc : bct_len - 1];
-  double a, c;
-  norm_fold(nsq, nblk, pn2, a, c, sh);
+  double a = 0.0, c = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {                                    // k = t, t+256, ... in order, as the loop
+    // x * 1.0 == x, x * 0.0 + a == a for these non-negative sums: bitwise the
+    // loop's skip, without a branch the compiler would sink the load into
+    const double in = t + 256 * i < nblk ? 1.0 : 0.0;
+    a += pn2[i].x * in;
+    c += pn2[i].y * in;
+  }
+  if (nblk > 1024) {                                               // (not at the sizes in use)
+    for (int k = t + 1024; k < nblk; k += 256) { a += nsq[2 * k]; c += nsq[2 * k + 1]; }
+  }
+  block_sum2(a, c, sh);
   // every thread folds the same partials in the same order, so each derives
   // its own net's constants (no second barrier)
   float coef, ss, b2s;
-  adam_consts(net == 0 ? a : c, net == 0 ? ka : kc, net == 0 ? bca : bcc, bct_len, net == 0 ? lr_a : lr_c, max_norm,
-              use_clip, coef, ss, b2s);
+  {
+    const double nn = net == 0 ? a : c;
+    const float nrm = (float)sqrt(nn);
+    coef = use_clip ? fminf(max_norm / (nrm + 1e-6f), 1.0f) : 1.0f;
+    // bct[2*step] = 1 - beta1**step, bct[2*step+1] = sqrt(1 - beta2**step) (python float
+    // math, as torch.optim.Adam computes them); constant 1.0 past the table
+    const int st = net == 0 ? ka : kc;
+    const double2 bc = net == 0 ? bca : bcc;
+    const double bc1 = st < bct_len ? bc.x : 1.0;
+    const double bc2s = st < bct_len ? bc.y : 1.0;
+    ss = (float)((double)(net == 0 ? lr_a : lr_c) / bc1);
+    b2s = (float)bc2s;
+  }
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
   if (!live) return;                                               // (W1.. tail blocks only: no barrier follows)
-  const float4 pn = adam4(g, m, v, p, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
-  Po4[e4] = pn;
-  Mo4[e4] = m;
-  Vo4[e4] = v;
+  float4 pn;
+  pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  pn.z = adam_elem(g.z, m.z, v.z, p.z, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  pn.w = adam_elem(g.w, m.w, v.w, p.w, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
+  P4[e4] = pn;
+  M4[e4] = m;
+  V4[e4] = v;
   if ((int)blockIdx.x < nbw && W2X != nullptr)                     // keep the fc2 operand image current
     w2x_tile(H, net, blockIdx.x % (ntc * ntc), pn, W2X, tile);
 }
@@ -2107,16 +1946,13 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
 static int launch_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
                           const void* W2X, float epsilon, float ent_coef, float max_action, float* H1, float* dZ2,
                           float* ptail, float* pw1, float* p2, float* ratio, bool fdw2, void* stream,
-                          bool kx = false, const AdamIn* ad = nullptr) {
+                          bool kx = false) {
   const int R = rows_per_wg(H, mb), nrb = n_head_wg(H, mb);
   dim3 g((net < 0 ? 2 : 1) * nrb);   // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
-  const AdamIn adi = ad ? *ad : AdamIn{};
-#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio, adi
-  if (H == 64 && fdw2 && ad)
-    hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true, false, true>), g, dim3(256), 0, s, RP_ARGS);
-  else if (H == 64 && fdw2)
+#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio
+  if (H == 64 && fdw2)
     hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true>), g, dim3(256), 0, s, RP_ARGS);
   else if (H == 64)
     hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, RP_ARGS);
@@ -2168,30 +2004,6 @@ int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_
     return -1;
   return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
                         nullptr, true, stream);
-}
-
-int satrl_ppo_rowpass_dw2_adam(int H, int mb, int net, const float* src, const int64_t* idx, float epsilon,
-                               float ent_coef, float max_action, float* p2, float* ptail, float* pw1, int mb_prev,
-                               const double* nsq, const double* steps, const double* bct, int bct_len,
-                               const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip,
-                               const float* G, const float* Pin, const float* Min, const float* Vin, float* Pout,
-                               float* Mout, float* Vout, void* stream) {
-  if (H != 64 || mb <= 0 || mb_prev <= 0 || net < -1 || net > 1 || !src || !p2 || !ptail || !pw1 || !nsq ||
-      !steps || !bct || bct_len < 1 || !lr || !G || !Pin || !Min || !Vin || !Pout || !Mout || !Vout)
-    return -1;
-  if (Pout == Pin || Mout == Min || Vout == Vin) {
-    g_err = "satrl_ppo_rowpass_dw2_adam: the state must go to other buffers (workgroups still read the old one)";
-    return -1;
-  }
-  AdamIn ad{};
-  ad.G = G; ad.Pin = Pin; ad.Min = Min; ad.Vin = Vin; ad.Pout = Pout; ad.Mout = Mout; ad.Vout = Vout;
-  ad.nsq = nsq; ad.steps = steps; ad.bct = bct; ad.lr = lr;
-  ad.nblk = n_blocks(geom(H, mb_prev, 1, net)); ad.bct_len = bct_len; ad.use_clip = use_clip;
-  ad.beta1 = beta1; ad.beta2 = beta2; ad.eps = eps; ad.max_norm = max_norm;
-  // (P and the fc2 operand image are this launch's LDS images: any non-null
-  // pointer satisfies launch_rowpass, nothing reads them)
-  return launch_rowpass(H, mb, net, src, idx, Pin, Pin, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1,
-                        p2, nullptr, true, stream, false, &ad);
 }
 
 int64_t satrl_ppo_kx_elems(int H, int mb) {
@@ -2369,26 +2181,17 @@ int satrl_ppo_allreduce_peer(int H, int mb, int world, int rank, void* const* bu
   return 0;
 }
 
-int satrl_ppo_adam_to(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
-                      const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip,
-                      const float* G, const float* Pin, const float* Min, const float* Vin, float* P, float* M,
-                      float* V, void* W2X, void* stream) {
-  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !Pin ||
-      !Min || !Vin || !P || !M || !V)
-    return -1;
-  const int nblk = n_blocks(geom(H, mb, 1, net));
-  hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq,
-                     steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, Pin, Min, Vin, P, M, V, W2X,
-                     net);
-  LAUNCH_CHECK();
-  return 0;
-}
-
 int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* steps, const double* bct, int bct_len,
                    const float* lr, float beta1, float beta2, float eps, float max_norm, int use_clip, const float* G,
                    float* P, float* M, float* V, void* W2X, void* stream) {
-  return satrl_ppo_adam_to(H, mb, net, nsq, steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M,
-                           V, P, M, V, W2X, stream);
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || !nsq || !steps || !bct || bct_len < 1 || !lr || !G || !P ||
+      !M || !V)
+    return -1;
+  const int nblk = n_blocks(geom(H, mb, 1, net));
+  hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq,
+                     steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2X, net);
+  LAUNCH_CHECK();
+  return 0;
 }
 
 int64_t satrl_ppo_w2x_floats(int H) { return valid_h(H) ? w2x_floats(H) : -1; }

@@ -112,11 +112,6 @@ _SIGS = {
     "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
                         C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_adam_to": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
-                           C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_rowpass_dw2_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp,
-                                    _vp, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
-                                    C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp, _vp,
                            _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass_ratio": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,

@@ -200,9 +200,7 @@ class FusedMinibatch:
     """One PPO minibatch step for actor + critic on shared rows:
     satrl_ppo_rowpass (gather, MLP forward/backward on f32 MFMA, losses),
     satrl_ppo_dw2 (the dW2 weight gradient, split-K), satrl_ppo_reduce and
-    satrl_ppo_adam, both nets per launch (H = 64: the dW2 product inside the
-    rowpass, and every Adam step of a run but the last folded into the next
-    rowpass -- satrl_ppo_rowpass_dw2_adam).  The actor and
+    satrl_ppo_adam, both nets per launch.  The actor and
     critic steps share nothing but the rows (ppo_continuous.py:216-239 runs
     two independent optimisers); with ``split_chains`` they run as two
     per-net chains on two streams (the critic on a side stream, fork/join per
@@ -210,7 +208,7 @@ class FusedMinibatch:
     all-reduce.  Groups of ``group`` minibatches are captured into a hipGraph
     and replayed over [group, mb] blocks of a device permutation."""
 
-    def __init__(self, learner, mb, group, use_graph=True, split_chains=False, fold_adam=True):
+    def __init__(self, learner, mb, group, use_graph=True, split_chains=False):
         self.L = learner
         self.mb = int(mb)
         self.group = int(group)
@@ -227,14 +225,6 @@ class FusedMinibatch:
         self.fused_dw2 = learner.H == 64
         self.kx_on = learner.H == 256
         self.kx_elems = 0
-        # H = 64: each run of minibatches (a graph group, an eager group) folds
-        # every Adam step but the last into the next minibatch's rowpass
-        # (satrl_ppo_rowpass_dw2_adam): two launches per step instead of
-        # three, the same bits.  The state alternates between the learner's
-        # P / M / V and a shadow set; the run's last step writes it back.
-        self.fold = bool(fold_adam) and self.fused_dw2
-        if self.fold:
-            self.shadow = tuple(torch.empty_like(t) for t in (learner.P, learner.M, learner.V))
         # two concurrent per-net chains: measured no faster than one fused chain at
         # H = 256 / 64, mb = 4096 on MI355X (the chains run in lockstep), so off by default
         self.split = bool(split_chains) and learner.pg is None
@@ -386,27 +376,10 @@ class FusedMinibatch:
         check(_lib.lib().satrl_ppo_dw2(self.L.H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), stream_ptr()),
               "satrl_ppo_dw2")
 
-    def _run(self, k, n):
-        """The run position of step k of n (folded Adam), else None."""
-        return (k, k == n - 1) if self.fold else None
-
-    def _state(self, k):
-        """(P, M, V) buffer set k % 2 of a folded-Adam run (0: the learner's)."""
-        L = self.L
-        return (L.P, L.M, L.V) if k % 2 == 0 else self.shadow
-
-    def _adam_args(self):
-        L = self.L
-        return (ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr), float(L.beta1), float(L.beta2), float(L.adam_eps),
-                0.5, int(bool(L.use_grad_clip)))
-
-    def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False, run=None):
-        """One minibatch step of one chain.  run = (k, last): step k of a
-        folded-Adam run (self.fold) -- k > 0 folds step k-1's Adam into this
-        rowpass, and only the last step launches one.  Bench-only knobs:
-        `events` (a pair of torch.cuda.Event) recorded around the rowpass
-        launch; skip_rowpass runs the rest of the chain on the last
-        H1/dZ2/slabs (timing only)."""
+    def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False):
+        """One minibatch step of one chain.  Bench-only knobs: `events` (a pair
+        of torch.cuda.Event) recorded around the rowpass launch; skip_rowpass
+        runs the rest of the chain on the last H1/dZ2/slabs (timing only)."""
         L = self.L
         H = L.H
         S = self.S if mb == self.mb else self.splits(H, mb)
@@ -422,16 +395,6 @@ class FusedMinibatch:
             H1, dZ2 = self.H1[:n], self.dZ2[:n]
         elif kx:
             self.rowpass_kx(src, idx, mb, net)
-            H1 = dZ2 = None
-        elif self.fused_dw2 and run is not None and run[0] > 0:
-            Pin, Min, Vin = self._state(run[0] - 1)
-            Po, Mo, Vo = self._state(run[0])
-            st, bct, nbct, lr, b1, b2, eps, mx, clip = self._adam_args()
-            check(lib.satrl_ppo_rowpass_dw2_adam(H, mb, int(net), ptr(src), None if idx is None else ptr(idx),
-                                                 float(L.epsilon), float(L.entropy_coef), float(L.max_action),
-                                                 ptr(self.p2), ptr(self.ptail), ptr(self.pw1), mb, ptr(nsq), st, bct,
-                                                 nbct, lr, b1, b2, eps, mx, clip, ptr(L.G), ptr(Pin), ptr(Min),
-                                                 ptr(Vin), ptr(Po), ptr(Mo), ptr(Vo), sp), "satrl_ppo_rowpass_dw2_adam")
             H1 = dZ2 = None
         elif self.fused_dw2:
             self.rowpass_dw2(src, idx, mb, net)
@@ -464,11 +427,9 @@ class FusedMinibatch:
             if L.peer is None or net >= 0:
                 check(lib.satrl_ppo_reduce_dp(H, mb, net, _dist.world_size(L.pg), ptr(L.G), ptr(nsq), ptr(L.steps),
                                               sp), "satrl_ppo_reduce_dp")
-        if run is not None and not run[1]:
-            return                                  # (folded into the next step's rowpass)
-        Pin, Min, Vin = self._state(run[0]) if run is not None else (L.P, L.M, L.V)
-        check(lib.satrl_ppo_adam_to(H, mb, net, ptr(nsq), *self._adam_args(), ptr(L.G), ptr(Pin), ptr(Min),
-                                    ptr(Vin), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam_to")
+        check(lib.satrl_ppo_adam(H, mb, net, ptr(nsq), ptr(L.steps), ptr(L.bct), L.bct.shape[0], ptr(L.lr),
+                                 float(L.beta1), float(L.beta2), float(L.adam_eps), 0.5, int(bool(L.use_grad_clip)),
+                                 ptr(L.G), ptr(L.P), ptr(L.M), ptr(L.V), ptr(L.W2T), sp), "satrl_ppo_adam")
 
     def _chains(self, fn):
         """fn(net) for the actor on the current stream and the critic on the
@@ -498,7 +459,7 @@ class FusedMinibatch:
 
         def chain(net):
             for k in range(ng):
-                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net, run=self._run(k, ng))
+                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
         self._chains(chain)
 
     def _group_dev(self, src):
@@ -510,7 +471,7 @@ class FusedMinibatch:
 
         def chain(net):
             for k in range(G):
-                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net, run=self._run(k, G))
+                self._net_step(self.stage[k * mb:(k + 1) * mb], None, mb, net)
         self._chains(chain)
         check(_lib.lib().satrl_ppo_group_advance(ptr(self.grp), stream_ptr()), "satrl_ppo_group_advance")
 
@@ -599,7 +560,7 @@ class PPOLearner:
     parameters are views into ``P`` so every forward pass (rollout, values,
     evaluate) reads the weights the fused update writes."""
 
-    def __init__(self, args, agent_idx, device=None, pg=None, graph_group=16, use_graph=True, fold_adam=True):
+    def __init__(self, args, agent_idx, device=None, pg=None, graph_group=16, use_graph=True):
         self.device = torch.device("cuda") if device is None else torch.device(device)
         self.args = args
         self.H = int(args.hidden_width)
@@ -633,7 +594,6 @@ class PPOLearner:
             self.peer = PeerComm(pg, ppo_layout(int(args.hidden_width))["total"], self.device, int(args.hidden_width))
         self.graph_group = graph_group
         self.use_graph = use_graph
-        self.fold_adam = fold_adam                          # (FusedMinibatch: H = 64's folded Adam steps)
         # CPU init with the reference's RNG consumption order (actor, then critic)
         actor = Actor_Gaussian(args, agent_idx)
         critic = Critic(args, agent_idx)
@@ -728,8 +688,7 @@ class PPOLearner:
 
     def stepper(self, mb):
         if mb not in self._steppers:
-            self._steppers[mb] = FusedMinibatch(self, mb, self.graph_group, use_graph=self.use_graph,
-                                                fold_adam=self.fold_adam)
+            self._steppers[mb] = FusedMinibatch(self, mb, self.graph_group, use_graph=self.use_graph)
         return self._steppers[mb]
 
     def normalize_adv(self, adv):

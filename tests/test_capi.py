@@ -106,18 +106,6 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, fake, None) == -1     # S < 1
     assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, fake, None) == -1       # an empty split (2 chunks)
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, fake, None) == -1     # null H1x
-    # the folded Adam step (H = 64 only; the new state must not overwrite the one other workgroups read)
-    f2, f3 = C.c_void_p(32), C.c_void_p(48)
-    fa = [fake, None, 0.1, 0.01, 1.6, fake, fake, fake, 4096, fake, fake, fake, 8, fake, 0.9, 0.999, 1e-5, 0.5, 1,
-          fake]
-    assert lib.satrl_ppo_rowpass_dw2_adam(256, 4096, -1, *fa, fake, fake, fake, f2, f2, f2, None) == -1   # H 64 only
-    assert lib.satrl_ppo_rowpass_dw2_adam(64, 4096, -1, *fa, fake, fake, fake, fake, f2, f2, None) == -1  # Pout == Pin
-    assert b"other buffers" in lib.satrl_ppo_last_error()
-    fa0 = list(fa)
-    fa0[8] = 0                                                                  # mb_prev 0
-    assert lib.satrl_ppo_rowpass_dw2_adam(64, 4096, -1, *fa0, f3, f3, f3, f2, f2, f2, None) == -1
-    assert lib.satrl_ppo_adam_to(64, 4096, -1, fake, fake, fake, 8, fake, 0.9, 0.999, 1e-5, 0.5, 1, fake, None, fake,
-                                 fake, fake, fake, fake, None, None) == -1       # null Pin
     # the peer all-reduce: grid, deadline, buffers
     bufs = (C.c_void_p * 2)(16, 16)
     pa = [C.cast(bufs, C.c_void_p), fake, fake, fake]

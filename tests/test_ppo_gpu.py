@@ -450,39 +450,6 @@ def test_update_graph_groups_equal_eager():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mb,use_graph,split", [(4096, True, False), (512, False, False), (512, True, True)])
-def test_folded_adam_equals_three_launches(mb, use_graph, split):
-    """H = 64: runs whose Adam steps are folded into the next minibatch's
-    rowpass (satrl_ppo_rowpass_dw2_adam: every workgroup updates its net in
-    LDS, the state alternating with a shadow set, satrl_ppo_adam_to at the
-    run's end) == the three-launch steps bit for bit: parameters, Adam
-    moments, step counters and the fc2 operand image, over two epochs of
-    graph groups (even runs), an eager remainder (an odd run) and a ragged
-    tail; one or two (split) chains."""
-    from satrl.ppo import FusedMinibatch, PPOLearner
-    G = 4
-    B = (2 * G + 3) * mb + 17
-    res = []
-    for fold in (True, False):
-        torch.manual_seed(11)
-        args = _args(hidden_width=64, mini_batch_size=mb, batch_size=B)
-        L = PPOLearner(args, "pursuer", graph_group=G, use_graph=use_graph, fold_adam=fold)
-        g = torch.Generator(device="cuda").manual_seed(2)
-        src = torch.randn((B, 32), device="cuda", generator=g)
-        src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
-        perms = [torch.randperm(B, device="cuda", generator=g) for _ in range(2)]
-        L.sync_w2t()
-        st = FusedMinibatch(L, mb, G, use_graph=use_graph, split_chains=split, fold_adam=fold)
-        assert st.fold == fold
-        for p in perms:
-            st.run(src, p)
-        torch.cuda.synchronize()
-        res.append((L.P.clone(), L.M.clone(), L.V.clone(), L.steps.clone(), L.W2T.clone()))
-    assert res[0][3].tolist() == [2.0 * (2 * G + 4)] * 2
-    for k, (a, b) in enumerate(zip(*res)):
-        assert torch.equal(a, b), ("P", "M", "V", "steps", "W2T")[k]
-
-
 @pytest.mark.parametrize("H,N", [(256, 1000), (256, 65536), (64, 4096), (64, 65536)])
 def test_policy_act_and_value_kernels(H, N):
     """satrl_policy_act / satrl_policy_value vs the torch modules + satrl_gaussian_sample

@@ -4,8 +4,7 @@ minibatch step for FusedMinibatch variants side by side (constructor
 keywords), replaying the update's graphs over a 16-minibatch epoch.
 Usage: python tools/step_ab.py H mb variant[,variant...] [reps]
   variants: "product" (defaults), or key=value pairs joined by '+': FusedMinibatch
-  keywords (e.g. split_chains=1), or S=<n> to run the dW2 split-K n ways,
-  noadam=1 / noreduce=1 to leave that launch out (timing-only upper bounds)"""
+  keywords (e.g. split_chains=1), or S=<n> to run the dW2 split-K n ways"""
 import os
 import sys
 
@@ -15,7 +14,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ppo-rl-satellite_amd"))
 from satrl.ppo import FusedMinibatch, PPOLearner  # noqa: E402
 from satrl.trainer import args_param  # noqa: E402
-from satrl import _lib  # noqa: E402
 
 
 def parse(v):
@@ -32,11 +30,6 @@ def time_variant(H, mb, kw, n=20):
     src = torch.randn((B, 32), device="cuda", generator=g)
     src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
     S = kw.pop("S", None)
-    skip = [k for k in ("noadam", "noreduce") if kw.pop(k, 0)]   # (timing-only upper bounds: launches left out)
-    lib = _lib.lib()
-    saved = {n: getattr(lib, n) for n in ("satrl_ppo_adam_to", "satrl_ppo_reduce")}
-    for k in skip:
-        setattr(lib, "satrl_ppo_adam_to" if k == "noadam" else "satrl_ppo_reduce", lambda *a: 0)
     st = FusedMinibatch(L, mb, 16, **kw)
     if S is not None:                       # (a valid split count: no empty split, <= the slab capacity)
         st.S = S
@@ -51,8 +44,6 @@ def time_variant(H, mb, kw, n=20):
         st.run(src, perm)
     e1.record()
     torch.cuda.synchronize()
-    for n_, f in saved.items():
-        setattr(lib, n_, f)
     return e0.elapsed_time(e1) * 1e3 / (n * 16)
 
 
