@@ -3,10 +3,10 @@
 # (the last commit's ppo_kernels.hip: make variant VNAME=head VSRC=...):
 # bitwise identity of whole updates + rollout passes (when BITS=1), then the
 # in-graph minibatch step at H 256 (mb 512, 4096) and the policy launch, twice
-# usage: TAG=name BITS=1 bash tools/ab_head.sh
+# usage: TAG=name BITS=1 [VNAME=head] bash tools/ab_head.sh  (VNAME: another tools/_probe/libsatrl_<VNAME>.so)
 set -o pipefail
 mkdir -p gpurun_out
-V=$GRAFT_REPO_ROOT/tools/_probe/libsatrl_head.so
+V=$GRAFT_REPO_ROOT/tools/_probe/libsatrl_${VNAME:-head}.so
 L=gpurun_out/${TAG}_ab.log
 if [ "${BITS:-0}" = 1 ]; then
   timeout -k 10 300 python -u tools/bitwise_dump.py gpurun_out/${TAG}_new.npz > $L 2>&1 &&
