@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Capture seeded PPO_continuous.update() runs of the reference at the
-product's hidden width (H = 256), build container ONLY.
+product's hidden widths, build container ONLY.
 
 Imports qiaobeibei/PPO-RL-Satellite from /root/reference (read-only, the
-gym stub of capture_golden.py) and records ``update_h256.npz`` next to this
-script: data only, the reference never travels.
+gym stub of capture_golden.py) and records ``update_h256.npz`` (H = 256,
+configs[2] / configs[3]) and ``update_h64.npz`` (H = 64, configs[1]) next
+to this script: data only, the reference never travels.
 
 The minibatch shapes are the ones the product's kernels are chosen by
 (satrl/ppo.py FusedMinibatch):
@@ -14,6 +15,11 @@ The minibatch shapes are the ones the product's kernels are chosen by
                                  rowpass; 4096 / 8 ranks)
   ragged  B 4873, mb 4096, K 2   one kx minibatch + a 777-row ragged tail
                                  (BatchSampler drop_last=False)
+and at H = 64 (every minibatch: the rowpass with the dW2 product fused in,
+satrl_ppo_rowpass_dw2, then reduce and Adam):
+  cfg1    B 8192, mb 4096, K 2   configs[1]'s minibatch (4096 envs)
+  short   B 2048, mb  512, K 2
+  ragged  B 4873, mb 4096, K 2
 
 Per case: the ReplayBuffer contents, the K epochs' SubsetRandomSampler
 permutations (drawn from the same torch generator state update() starts
@@ -22,7 +28,7 @@ after the decay.  The buffer is synthetic (reference choose_action for a
 and logp on N(0, 4) states), the networks the reference's own orthogonal
 init.
 
-Run:  python tests/golden/capture_update_h256.py      (~1 minute)
+Run:  python tests/golden/capture_update_h256.py [256] [64]   (~1 minute each)
 """
 import contextlib
 import io
@@ -35,14 +41,15 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from capture_golden import OUT, REF, _setup  # noqa: E402
 
 CASES = [("kx", 8192, 4096, 2, 1001), ("short", 2048, 512, 2, 1002), ("ragged", 4873, 4096, 2, 1003)]
+CASES_H64 = [("cfg1", 8192, 4096, 2, 2001), ("short", 2048, 512, 2, 2002), ("ragged", 4873, 4096, 2, 2003)]
 
 
-def capture_case(name, B, mb, K, seed, CPPO_main, ppo_continuous, replaybuffer):
+def capture_case(name, B, mb, K, seed, CPPO_main, ppo_continuous, replaybuffer, H=256):
     import torch
     from torch.utils.data.sampler import BatchSampler, SubsetRandomSampler
     torch.manual_seed(seed)
     np.random.seed(seed)
-    a = CPPO_main.args_param(batch_size=B, mini_batch_size=mb, hidden_width=256, K_epochs=K,
+    a = CPPO_main.args_param(batch_size=B, mini_batch_size=mb, hidden_width=H, K_epochs=K,
                              max_train_steps=5000, chkpt_dir="/nonexistent")
     a.state_dim, a.action_dim, a.max_action = 18, 3, 1.6
     with contextlib.redirect_stdout(io.StringIO()):
@@ -78,7 +85,7 @@ def capture_case(name, B, mb, K, seed, CPPO_main, ppo_continuous, replaybuffer):
     out = {"s": f32(buf.s), "a": f32(buf.a), "logp": f32(buf.a_logprob), "r": f32(buf.r), "s_": f32(buf.s_),
            "dw": f32(buf.dw), "done": f32(buf.done),
            "perms": np.stack(perms), "total_steps": np.array(total_steps),
-           "hp": np.array([B, mb, 256, K, a.max_train_steps, a.lr_a, a.lr_c, a.gamma, a.lamda, a.epsilon,
+           "hp": np.array([B, mb, H, K, a.max_train_steps, a.lr_a, a.lr_c, a.gamma, a.lamda, a.epsilon,
                            a.entropy_coef]),
            "lr_after": np.array([agent.optimizer_actor.param_groups[0]["lr"],
                                  agent.optimizer_critic.param_groups[0]["lr"]])}
@@ -87,7 +94,7 @@ def capture_case(name, B, mb, K, seed, CPPO_main, ppo_continuous, replaybuffer):
     for k, v in p1.items():
         out["p1." + k] = v
     move = max(float(np.abs(p1[k] - p0[k]).max()) for k in p0)
-    print(f"{name}: B {B} mb {mb} K {K}: max parameter movement {move:.3e}")
+    print(f"H {H} {name}: B {B} mb {mb} K {K}: max parameter movement {move:.3e}")
     return {f"{name}.{k}": v for k, v in out.items()}
 
 
@@ -98,10 +105,14 @@ def main():
     import CPPO_main
     import ppo_continuous
     import replaybuffer
-    fx = {}
-    for case in CASES:
-        fx.update(capture_case(*case, CPPO_main, ppo_continuous, replaybuffer))
-    np.savez_compressed(os.path.join(OUT, "update_h256.npz"), **fx)
+    which = sys.argv[1:] or ["256", "64"]
+    for H, cases, fname in ((256, CASES, "update_h256.npz"), (64, CASES_H64, "update_h64.npz")):
+        if str(H) not in which:
+            continue
+        fx = {}
+        for case in cases:
+            fx.update(capture_case(*case, CPPO_main, ppo_continuous, replaybuffer, H=H))
+        np.savez_compressed(os.path.join(OUT, fname), **fx)
 
 
 if __name__ == "__main__":

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from conftest import golden
-from update_replay import h256_case, run_reference_update
+from update_replay import h64_case, h256_case, run_reference_update
 
 pytestmark = pytest.mark.gpu
 
@@ -167,6 +167,18 @@ def test_update_matches_reference_h256(case):
     MI355X; the f32 sums in another order than torch's CPU ones -- on the CPU
     the same cases move by <= 8e-8 when fc1 is summed in f64 instead)."""
     run_reference_update(h256_case(case), atol=1e-6)
+
+
+@pytest.mark.parametrize("case", ["cfg1", "short", "ragged"])
+def test_update_matches_reference_h64_configs1(case):
+    """The reference's own update() at H = 64 (tests/golden/capture_update_h256.py,
+    update_h64.npz): "cfg1" B 8192 / mb 4096 (configs[1]'s minibatch: the
+    rowpass with the dW2 product fused in, reduce, Adam), "short" mb 512,
+    "ragged" B 4873 (a 777-row tail), two epochs each, through the drop-in
+    PPO_continuous with the captured minibatch orders.  Bar 1e-6 absolute
+    on every parameter after the update (f32 MFMA chains against the
+    reference's CPU f32 GEMMs)."""
+    run_reference_update(h64_case(case), atol=1e-6)
 
 
 @pytest.mark.parametrize("H,split,mb", [(64, False, 512), (256, False, 512), (256, True, 512),

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from conftest import golden
-from update_replay import h256_case, run_reference_update
+from update_replay import h64_case, h256_case, run_reference_update
 
 
 @pytest.fixture
@@ -28,3 +28,10 @@ def test_host_update_matches_reference_h64(one_thread):
 @pytest.mark.parametrize("case", ["kx", "short", "ragged"])
 def test_host_update_matches_reference_h256(one_thread, case):
     assert run_reference_update(h256_case(case), device="cpu", atol=0.0) == 0.0
+
+
+@pytest.mark.parametrize("case", ["cfg1", "short", "ragged"])
+def test_host_update_matches_reference_h64_configs1(one_thread, case):
+    """H = 64 at configs[1]'s minibatch (4096 rows), a short one and a ragged
+    tail (update_h64.npz)."""
+    assert run_reference_update(h64_case(case), device="cpu", atol=0.0) == 0.0

@@ -14,10 +14,19 @@ def _args(**kw):
     return a
 
 
-def h256_case(name):
-    """One case of update_h256.npz as {key: array}."""
-    u = golden("update_h256")
+def width_case(H, name):
+    """One case of update_h<H>.npz (tests/golden/capture_update_h256.py) as
+    {key: array}."""
+    u = golden(f"update_h{H}")
     return {k[len(name) + 1:]: u[k] for k in u.files if k.startswith(name + ".")}
+
+
+def h256_case(name):
+    return width_case(256, name)
+
+
+def h64_case(name):
+    return width_case(64, name)
 
 
 def run_reference_update(u, device=None, atol=5e-5):
