@@ -15,11 +15,13 @@ The minibatch shapes are the ones the product's kernels are chosen by
                                  rowpass; 4096 / 8 ranks)
   ragged  B 4873, mb 4096, K 2   one kx minibatch + a 777-row ragged tail
                                  (BatchSampler drop_last=False)
+  k10     B 8192, mb 4096, K 10  the bench's epoch count: 20 Adam steps
 and at H = 64 (every minibatch: the rowpass with the dW2 product fused in,
 satrl_ppo_rowpass_dw2, then reduce and Adam):
   cfg1    B 8192, mb 4096, K 2   configs[1]'s minibatch (4096 envs)
   short   B 2048, mb  512, K 2
   ragged  B 4873, mb 4096, K 2
+  k10     B 8192, mb 4096, K 10
 
 Per case: the ReplayBuffer contents, the K epochs' SubsetRandomSampler
 permutations (drawn from the same torch generator state update() starts
@@ -40,8 +42,10 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from capture_golden import OUT, REF, _setup  # noqa: E402
 
-CASES = [("kx", 8192, 4096, 2, 1001), ("short", 2048, 512, 2, 1002), ("ragged", 4873, 4096, 2, 1003)]
-CASES_H64 = [("cfg1", 8192, 4096, 2, 2001), ("short", 2048, 512, 2, 2002), ("ragged", 4873, 4096, 2, 2003)]
+CASES = [("kx", 8192, 4096, 2, 1001), ("short", 2048, 512, 2, 1002), ("ragged", 4873, 4096, 2, 1003),
+         ("k10", 8192, 4096, 10, 1004)]
+CASES_H64 = [("cfg1", 8192, 4096, 2, 2001), ("short", 2048, 512, 2, 2002), ("ragged", 4873, 4096, 2, 2003),
+             ("k10", 8192, 4096, 10, 2004)]
 
 
 def capture_case(name, B, mb, K, seed, CPPO_main, ppo_continuous, replaybuffer, H=256):

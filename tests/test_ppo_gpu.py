@@ -155,7 +155,7 @@ def test_update_matches_reference():
     run_reference_update({k: u[k] for k in u.files})
 
 
-@pytest.mark.parametrize("case", ["kx", "short", "ragged"])
+@pytest.mark.parametrize("case", ["kx", "short", "ragged", "k10"])
 def test_update_matches_reference_h256(case):
     """The product's own update kernels pinned to the reference's update() at
     H = 256 (tests/golden/capture_update_h256.py): "kx" B 8192 / mb 4096 (the
@@ -169,7 +169,7 @@ def test_update_matches_reference_h256(case):
     run_reference_update(h256_case(case), atol=1e-6)
 
 
-@pytest.mark.parametrize("case", ["cfg1", "short", "ragged"])
+@pytest.mark.parametrize("case", ["cfg1", "short", "ragged", "k10"])
 def test_update_matches_reference_h64_configs1(case):
     """The reference's own update() at H = 64 (tests/golden/capture_update_h256.py,
     update_h64.npz): "cfg1" B 8192 / mb 4096 (configs[1]'s minibatch: the

@@ -25,12 +25,12 @@ def test_host_update_matches_reference_h64(one_thread):
     assert run_reference_update({k: u[k] for k in u.files}, device="cpu", atol=0.0) == 0.0
 
 
-@pytest.mark.parametrize("case", ["kx", "short", "ragged"])
+@pytest.mark.parametrize("case", ["kx", "short", "ragged", "k10"])
 def test_host_update_matches_reference_h256(one_thread, case):
     assert run_reference_update(h256_case(case), device="cpu", atol=0.0) == 0.0
 
 
-@pytest.mark.parametrize("case", ["cfg1", "short", "ragged"])
+@pytest.mark.parametrize("case", ["cfg1", "short", "ragged", "k10"])
 def test_host_update_matches_reference_h64_configs1(one_thread, case):
     """H = 64 at configs[1]'s minibatch (4096 rows), a short one and a ragged
     tail (update_h64.npz)."""
