@@ -150,7 +150,12 @@ def test_update_matches_reference():
     minibatch permutations (captured), through the drop-in PPO_continuous.
     5e-5 absolute: about 1 % of the movement 24 Adam steps at lr 2e-4 can
     make (lr * nsteps = 4.8e-3), 2.8x the measured worst (1.8e-5, the f32
-    gradient sums adding in another order than torch's)."""
+    gradient sums adding in another order than torch's).  The buffer is a
+    real env rollout, states at the env's raw metre scale (~1e5): fc1's
+    pre-activations are sums of large terms cancelling to O(1), so any f32
+    summation order moves tanh' and dW1 visibly -- the well-conditioned
+    captures at the product's shapes (update_h64.npz / update_h256.npz,
+    below) hold every width to 1e-6."""
     u = golden("update_case")
     run_reference_update({k: u[k] for k in u.files})
 
