@@ -732,7 +732,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1, int net_sel, float* __restrict__ p2,
-                                                      int S2, float* __restrict__ ratio_out) {
+                                                      int S2, float* __restrict__ ratio_out, float inv_mb) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
   // KX: H1 / dZ2 go out as k-packed bf16 planes (store_kx; H1g / dZ2g point at
@@ -833,13 +833,18 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather,
                                    FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
-  if constexpr (KX) {
+  // (KX) the H1 planes: wave 0, which runs the loss head next, stores its
+  // share after the head, off the head's path; the other waves now
+  auto h1_kx = [&] {
     store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
     if (R < 32 && r0 + R < kx_rows(mb) && r0 + R >= mb) {            // (uniform) the padded chunk's rows past this block
       const float z[R / 16][CT][4] = {};
       store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0 + R, n0, z);
       store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(dZ2g) + net * 3 * PLX, PLX, r0 + R, n0, z);
     }
+  };
+  if constexpr (KX) {
+    if (w != 0) h1_kx();
   }
   else if constexpr (BF3 && !FDW2) store_rows<R, CT>(H1g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, h1);
   // phase D's first W2T chunks go out now, under the loss head and the tail
@@ -851,7 +856,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
     const int r = tid, row = r0 + r;
     float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
     if (row < mb) {
-      const float inv = 1.0f / (float)mb;
+      const float inv = inv_mb;                                   // 1.0f / (float)mb, IEEE on the host
       if (net == 0) {                                              // actor: clipped surrogate + entropy
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
@@ -921,6 +926,9 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         tp[6 * H + 9] = 0.0f; tp[6 * H + 10] = 0.0f; tp[6 * H + 11] = 0.0f;
       }
     }
+  }
+  if constexpr (KX) {
+    if (w == 0) h1_kx();
   }
   rp_barrier();
   PHASE_PROBE(4);
@@ -1951,7 +1959,8 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
   dim3 g((net < 0 ? 2 : 1) * nrb);   // (row block, net) pairs, or row blocks of one net
   hipStream_t s = (hipStream_t)stream;
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
-#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio
+  const float inv_mb = 1.0f / (float)mb;
+#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio, inv_mb
   if (H == 64 && fdw2)
     hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true>), g, dim3(256), 0, s, RP_ARGS);
   else if (H == 64)
