@@ -564,8 +564,10 @@ struct MlpSmem {
 // acc = tanh(fc2) for this wave's columns, h1 = tanh(fc1) (for the fc1
 // backward), w3 = this wave's output-layer weights, and osum holds the
 // per-wave dot products (after a barrier).  h1out (nullable): row r of
-// tanh(fc1) goes to h1out[r * H + n].
-template <int H, int NW, int R, bool APRE, class Gather>
+// tanh(fc1) goes to h1out[r * H + n].  PRIO: the caller raised the wave's
+// issue priority (s_setprio) for its weight loads; it drops back once phase
+// B's are all out (the policy kernel, see there).
+template <int H, int NW, int R, bool APRE, bool PRIO = false, class Gather>
 __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* __restrict__ P,
                                             int net, int nvalid,
                                             Gather gather, float* __restrict__ h1out,
@@ -658,6 +660,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
   else
     mfma_rows<H, LDA, H, RT, CT, APRE>(&sm.h1s[0][0], P + L.W2 + (int64_t)net * H * H, n0, acc);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   PHASE_PROBE(2);
 
   // ---- C (forward part): fc2 tanh, output-layer dot products -----------------
@@ -1082,6 +1085,12 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
                                                      float* __restrict__ act1, float* __restrict__ logp1,
                                                      float* __restrict__ value) {
   constexpr int R = kPolRows, RT = R / 16, CT = H / 16 / NW;
+  // Two or more workgroups share a CU, and one finishing its output layer
+  // would out-issue (oldest first) one that is still streaming W1 / W2: at
+  // priority 3 until phase B's weight loads are out, a starting workgroup's
+  // loads go first and overlap the other's tail (46 against 49 us per H 256
+  // launch at 16 384 envs; bitwise unchanged)
+  __builtin_amdgcn_s_setprio(3);
   const Layout L = layout(H);
   __shared__ MlpSmem<H, NW, R> sm;
   const int agent = MODE == 0 ? (int)(blockIdx.x % nagents) : 0;
@@ -1113,7 +1122,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW, R, false>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  mlp_forward<H, NW, R, false, true>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
   if (r >= nvalid) return;                                       // no barrier follows
   const int64_t i = r0 + r;
