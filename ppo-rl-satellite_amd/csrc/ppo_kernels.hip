@@ -1297,6 +1297,7 @@ __device__ __forceinline__ void dw2_kx_body(int b, int mb, int S, int KR, int ne
     for (int x = 0; x < XN; ++x)
 #pragma unroll
       for (int y = 0; y < XN; ++y) acc[x][y] = mfma6(a[x], bq[y], acc[x][y]);
+    if (c + kKxD - 1 >= nch) __builtin_amdgcn_s_setprio(0);                         // (the last chunk is staged)
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // acc[x][y][q] = dW2[o0 + (TW/2)wo + 16x + 4lg + q][n0 + (TW/2)wn + 16y + li]
@@ -1314,6 +1315,10 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
                                                      const unsigned short* __restrict__ H1x,
                                                      const unsigned short* __restrict__ dZ2x, float* __restrict__ p2) {
   __shared__ __attribute__((aligned(16))) KxSmem<TW> sm;
+  // at priority 3 until a wave has staged its last chunk (dw2_kx_body), as
+  // the policy kernel: in-graph step 48.8 against 49.1 us at mb 4096 over
+  // eight alternations, bitwise the same (EXPERIMENTS.md round 5)
+  __builtin_amdgcn_s_setprio(3);
   dw2_kx_body<TW>(blockIdx.x, mb, S, KR, net_sel, H1x, dZ2x, p2, sm);
 }
 // split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split

@@ -247,7 +247,10 @@ class FusedMinibatch:
         # sized for the largest split count any minibatch size can produce, so
         # a ragged tail minibatch whose S exceeds the full minibatch's never
         # writes past the slabs
-        self.p2 = torch.empty(2 * self.max_splits(H) * H * H, **f32)
+        # (the capacity is fixed here: the launch guard below compares against
+        # it, not against max_splits(), which follows a later change of self.S)
+        self.p2_splits = self.max_splits(H)
+        self.p2 = torch.empty(2 * self.p2_splits * H * H, **f32)
         self.nsq = torch.zeros((2, 2 * self.nblk), dtype=torch.float64, device=dev)   # one per chain
         self.idx = torch.zeros((self.group, self.mb), dtype=torch.int64, device=dev)
         # the rows of one group of minibatches, gathered contiguously once per
@@ -383,8 +386,8 @@ class FusedMinibatch:
         L = self.L
         H = L.H
         S = self.S if mb == self.mb else self.splits(H, mb)
-        if S > self.max_splits(H):
-            raise _lib.NativeError(f"dW2 split count {S} exceeds the slab capacity {self.max_splits(H)}")
+        if S > self.p2_splits:
+            raise _lib.NativeError(f"dW2 split count {S} exceeds the slab capacity {self.p2_splits}")
         lib, sp = _lib.lib(), stream_ptr()
         nsq = self.nsq[max(net, 0)]
         if events is not None:

@@ -31,8 +31,11 @@ def time_variant(H, mb, kw, n=20):
     src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
     S = kw.pop("S", None)
     st = FusedMinibatch(L, mb, 16, **kw)
-    if S is not None:                       # (a valid split count: no empty split, <= the slab capacity)
+    if S is not None:                       # (a valid split count: no empty split)
         st.S = S
+        if S > st.p2_splits:                # the slabs for S splits (the learner sized them for its own S)
+            st.p2_splits = S
+            st.p2 = torch.empty(2 * S * H * H, dtype=torch.float32, device="cuda")
     perm = torch.randperm(B, device="cuda", generator=g)
     L.sync_w2t()
     for _ in range(3):
