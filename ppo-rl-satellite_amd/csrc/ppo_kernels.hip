@@ -833,7 +833,11 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   const float* W2T = static_cast<const float*>(W2X);
   // (H = 256: the H1 store after phase B, not between fc1 and B: 8 fewer VGPRs
   // live through B, so the 32-row kernel stays at <= 104)
-  mlp_forward<H, NW, R, true>(sm, P, net, mb - r0, gather,
+  // (FDW2, H = 64: at priority 3 until phase B's weight loads are out, as the
+  // policy kernel -- in-graph step 18.2 against 18.4 us at configs[1]'s
+  // mb 4096, 15.3 against 15.5 at 512; at H = 256 no gain, not set there)
+  if constexpr (FDW2) __builtin_amdgcn_s_setprio(3);
+  mlp_forward<H, NW, R, true, FDW2>(sm, P, net, mb - r0, gather,
                                    FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   // (KX) the H1 planes: wave 0, which runs the loss head next, stores its
