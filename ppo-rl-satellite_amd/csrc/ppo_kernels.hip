@@ -1321,7 +1321,8 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
   __shared__ __attribute__((aligned(16))) KxSmem<TW> sm;
   // at priority 3 until a wave has staged its last chunk (dw2_kx_body), as
   // the policy kernel: in-graph step 48.8 against 49.1 us at mb 4096 over
-  // eight alternations, bitwise the same (EXPERIMENTS.md round 5)
+  // eight alternations on two boxes, equal (49.4) in three on a third;
+  // bitwise the same (EXPERIMENTS.md round 5)
   __builtin_amdgcn_s_setprio(3);
   dw2_kx_body<TW>(blockIdx.x, mb, S, KR, net_sel, H1x, dZ2x, p2, sm);
 }
