@@ -478,6 +478,7 @@ def run(a, world):
     rowpass_ev_us, rowpass_med = timed_pairs(a.kernel_iters, lambda k, ev: st.step(stage, None, events=ev), 60.0)
     rowpass_flop = st.step_kernel_flops(mb_local)        # + the fused dW2 product at H = 64
     rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
+    t_roll_sp = [0]
     # warm-L2 figure: back-to-back rowpass launches alone (W2/W2T stay in L2)
     rp_launch = st.rowpass_dw2 if st.fused_dw2 else (st.rowpass_kx if st.kx(mb_local) else st.rowpass)
     for _ in range(10):
@@ -523,13 +524,42 @@ def run(a, world):
         return None
 
     rowpass_prof_us = prof_avg_us("rowpass_kernel<%d" % a.hidden)
-    head_us = rowpass_prof_us if rowpass_prof_us else rowpass_us
+
+    # ---- live launch spans (satrl_span_probe, satrl/spans.py): every kernel's
+    # duration measured in THIS run, inside the update's own hipGraphs -- a fresh
+    # stepper captured while the probe is on runs two graph groups of minibatch
+    # steps (its kernels' SPAN instantiations add one 16-B store per wave at its
+    # exit) -- and over eager rollout steps queued behind a GPU spin.  These are
+    # the headline durations; the committed rocprof averages stay beside them.
+    from satrl.ppo import FusedMinibatch
+    from satrl.spans import SpanProbe
+    upd_spans, roll_spans = {}, {}
+    perm_sp = torch.randperm(src.shape[0], device="cuda", generator=g)[:2 * L.graph_group * mb_local].contiguous()
+    with SpanProbe() as probe:
+        stp = FusedMinibatch(L, mb_local, L.graph_group, use_graph=True)
+        stp.run(src, perm_sp)                    # capture (each node keeps its record region), then two replays
+        torch.cuda.synchronize()
+    upd_spans = probe.summary()
+    del stp
+    with SpanProbe() as probe:
+        tr._policy_step(0)                       # (untimed: first launches)
+        torch.cuda.synchronize()
+    with SpanProbe() as probe:
+        backlog(40.0)
+        for _ in range(a.kernel_iters):
+            tr._policy_step(t_roll_sp[0] % a.horizon)
+            t_roll_sp[0] += 1
+        torch.cuda.synchronize()
+    roll_spans = probe.summary()
+    rowpass_live_us = upd_spans.get("rowpass", {}).get("avg_us")
+    head_us = rowpass_live_us if rowpass_live_us else rowpass_us
     traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
     # the rollout's policy kernel (both agents' forward, the (num_envs x hidden)
     # GEMMs): per row and agent fc1 2*18*H + H, fc2 2*H*H + H, mean layer 2*3*H + 3
     policy_roof = None
     pol_nw = 8 if a.hidden == 256 else a.hidden // 16      # waves per policy workgroup (csrc kPolNW at H 256)
-    pol_us = prof_avg_us("policy_kernel<%d;%d;0>" % (a.hidden, pol_nw))
+    pol_prof_us = prof_avg_us("policy_kernel<%d;%d;0>" % (a.hidden, pol_nw))
+    pol_us = roll_spans.get("policy_act", {}).get("avg_us") or pol_prof_us
     if pol_us:
         pol_flop = 2 * a.num_envs * (2 * 18 * a.hidden + a.hidden + 2 * a.hidden * a.hidden + a.hidden
                                      + 2 * 3 * a.hidden + 3)
@@ -539,8 +569,12 @@ def run(a, world):
                                     else "f32 MFMA)"),
                        "bound": "mfma", "achieved": pol_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                        "frac": pol_tfs / FP32_MFMA_PEAK_TFS, "avg_launch_us": pol_us, "flop_per_launch": pol_flop,
-                       "timing": f"rocprofv3 average over the rollout's launches "
-                                 f"(profiles/{os.path.basename(ks_file)})"}
+                       "timing": ("live launch span in this run (satrl_span_probe: max wave exit - min wave start, "
+                                  "s_memrealtime) averaged over kernel_iters eager rollout steps queued behind a GPU "
+                                  "spin" if roll_spans.get("policy_act") else "rocprofv3 average (committed profile)"),
+                       "rocprof_avg_launch_us": pol_prof_us,
+                       "rocprof_source": (f"profiles/{os.path.basename(ks_file)} (committed profile of this command)"
+                                          if ks_file else None)}
         pol_file = os.path.join(ROOT, "profiles", f"{a.profile_tag}_policy{sfx}_mfma_pmc.json")
         d = None
         if os.path.exists(pol_file):
@@ -601,7 +635,8 @@ def run(a, world):
         env_fp64 = {"fp64_flops_per_launch": d["fp64_flops_per_launch"], "fp64_frac": d["fp64_frac"],
                     "peak_tflops": d["fp64_vector_peak_tflops"],
                     "source": f"profiles/{a.profile_tag}_env_fp64_pmc.json (16384 envs mid-episode)"}
-    env_head_us = env_prof_us if env_prof_us else env_us
+    env_span_us = roll_spans.get("env_step", {}).get("avg_us")
+    env_head_us = env_span_us if env_span_us else env_us
     env_gbs = a.num_envs * ENV_BYTES_PER_STEP / (env_head_us * 1e-6) / 1e9
     env_traffic = pmc("env", num_envs=a.num_envs)
     env = tr.env
@@ -832,6 +867,20 @@ def run(a, world):
     upd_tfs = upd_flops / (update_ms * 1e-3) / 1e12
     n_minibatches = a.epochs * ((a.num_envs * a.horizon) // tr.mb_local)
 
+    # self-consistency: the kernels of one step, by their live spans, cannot
+    # take longer than the step itself on the timed region's clock
+    def span_check(kinds, spans, live_us, what):
+        got = [spans[k]["avg_us"] for k in kinds if k in spans]
+        tot = sum(got) if len(got) == len(kinds) else None
+        ok = tot is not None and tot <= live_us
+        if not ok:
+            print(f"bench: {what}: kernel spans {tot} us exceed the live step {live_us:.2f} us", file=sys.stderr)
+        return {"kernels": kinds, "sum_of_span_avgs_us": tot, "live_step_us": live_us, "pass": ok,
+                "rule": f"sum of the kernels' live span averages <= the timed region's {what} time per step"}
+    upd_kinds = ["rowpass", "reduce", "adam"] + ([] if st.fused_dw2 else ["dw2"])
+    upd_check = span_check(upd_kinds, upd_spans, update_ms * 1e3 / n_minibatches, "update (minibatch step)")
+    roll_check = span_check(["policy_act", "env_step"], roll_spans, rollout_ms * 1e3 / a.horizon, "rollout step")
+
     if rank == 0:
         host_baseline = not a.no_cpu_baseline and world == 1          # rank 0 at N = 1 only
         cpu = cpu_baseline(a.cpu_baseline_seconds, a.num_envs, a.horizon, a.hidden, a.minibatch,
@@ -867,10 +916,14 @@ def run(a, world):
                          "unit": "TFLOP/s",
                          "frac": rowpass_flop / (head_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS, "traffic": traffic,
                          "avg_launch_us": head_us, "flop_per_launch": rowpass_flop, "rows_per_launch": mb_local,
-                         "timing": ("in-update kernel duration: the rocprofv3 average of this command's rowpass "
-                                    "launches (profiles/, nearly all inside the update's graphs); the live HIP-event "
-                                    "figures beside it" if rowpass_prof_us else
-                                    "live marginal cost (no rocprof profile of this command's shape)"),
+                         "timing": ("live in-update kernel duration measured in this run: the launch span "
+                                    "(satrl_span_probe: max wave exit - min wave start, s_memrealtime, 100 MHz) "
+                                    "averaged over every rowpass launch of two replays of the update's own 64-"
+                                    "minibatch hipGraph; the committed rocprof average and the live marginal beside it"
+                                    if rowpass_live_us else
+                                    "live marginal cost (the span probe gave no rowpass launches)"),
+                         "live_span_avg_launch_us": rowpass_live_us,
+                         "update_kernel_spans": upd_spans,
                          "live_marginal_avg_launch_us": rowpass_us,
                          "live_marginal_frac": rowpass_tfs / FP32_MFMA_PEAK_TFS,
                          "live_marginal_timing": "HIP events on the launch stream: kernel_iters minibatch steps "
@@ -881,9 +934,12 @@ def run(a, world):
                          "minibatch_step_us": t_chain,
                          "event_bracketed_avg_launch_us": rowpass_ev_us, "event_bracketed_median_us": rowpass_med,
                          "rocprof_avg_launch_us": rowpass_prof_us,
-                         "rocprof_source": (f"profiles/{os.path.basename(ks_file)} (rocprofv3 average over all rowpass "
-                                            "launches of this command, nearly all in the update's graphs)"
-                                            if ks_file else None),
+                         "rocprof_frac": (rowpass_flop / (rowpass_prof_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS
+                                          if rowpass_prof_us else None),
+                         "rocprof_source": (f"profiles/{os.path.basename(ks_file)} (COMMITTED rocprofv3 profile of this "
+                                            "command, not this run: average over all rowpass launches, nearly all in "
+                                            "the update's graphs)" if ks_file else None),
+                         "check": upd_check,
                          "back_to_back_avg_launch_us": b2b_us,
                          "back_to_back_frac": rowpass_flop / (b2b_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFS,
                          "traffic_source": f"profiles/{a.profile_tag}_rowpass{sfx}_pmc.json (FETCH_SIZE x2 + WRITE_SIZE, "
@@ -895,17 +951,21 @@ def run(a, world):
                              "achieved": env_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": env_gbs / HBM_PEAK_GBS,
                              "avg_launch_us": env_head_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
                              "num_envs": a.num_envs,
-                             "timing": ("in-rollout kernel duration: the rocprofv3 average over every env-step launch "
-                                        "of a process running only the training rollout (16384 envs, H 256, hipGraph "
-                                        "chunks; profiles/%s_env_rollout.json)" % a.profile_tag
-                                        if env_prof_us else "live marginal cost (no env-rollout profile)"),
+                             "timing": ("live in-rollout kernel duration measured in this run: the launch span "
+                                        "(satrl_span_probe) averaged over kernel_iters eager rollout steps of the "
+                                        "trainer's envs queued behind a GPU spin; the committed rocprof average "
+                                        "beside it" if env_span_us else "live marginal cost (no span)"),
+                             "live_span_avg_launch_us": env_span_us,
+                             "rollout_kernel_spans": roll_spans,
+                             "check": roll_check,
                              "live_marginal_avg_launch_us": env_us, "live_marginal_GBs": env_live_gbs,
                              "live_marginal_timing": "HIP events: kernel_iters eager rollout steps (policy kernel -> "
                                                      "env step) on the trainer's envs after the timed region, minus "
                                                      "the same steps without the env step, per launch",
                              "event_bracketed_avg_launch_us": env_ev_us, "event_bracketed_median_us": env_med,
                              "rocprof_avg_launch_us": env_prof_us,
-                             "rocprof_source": f"profiles/{a.profile_tag}_env_rollout.json / _env_rollout_kernel_stats.csv",
+                             "rocprof_source": (f"profiles/{a.profile_tag}_env_rollout.json / _env_rollout_kernel_stats"
+                                                ".csv (COMMITTED profile, not this run)"),
                              "rocprof_mid_episode_by_num_envs": env_sweep_prof,
                              "fp64_utilisation": env_fp64,
                              "traffic": env_traffic,

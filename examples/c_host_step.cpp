@@ -143,11 +143,12 @@ void ppo_step(const std::string& out, int mb, hipStream_t st) {
   uint16_t* d_H1x = dev<uint16_t>((size_t)kxe);
   uint16_t* d_dZ2x = dev<uint16_t>((size_t)kxe);
   const int S = satrl_ppo_dw2_kx_splits(H, mb, -1);
-  float* d_p2 = dev<float>(2 * (size_t)S * H * H);
-  PPO_OK(satrl_ppo_rowpass_kx(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1x, d_dZ2x, d_pt, d_pw,
-                              st));
-  PPO_OK(satrl_ppo_dw2_kx(H, mb, -1, S, d_H1x, d_dZ2x, d_p2, st));
-  PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, d_pw, d_pt, d_G, d_nsq, d_steps, st));
+  const int64_t p2n = 2LL * S * H * H;          // every slab call takes these capacities and refuses past them
+  float* d_p2 = dev<float>((size_t)p2n);
+  PPO_OK(satrl_ppo_rowpass_kx(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1x, d_dZ2x, kxe, d_pt,
+                              d_pw, st));
+  PPO_OK(satrl_ppo_dw2_kx(H, mb, -1, S, d_H1x, d_dZ2x, kxe, d_p2, p2n, st));
+  PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, p2n, d_pw, d_pt, d_G, d_nsq, d_steps, st));
   PPO_OK(satrl_ppo_adam(H, mb, -1, d_nsq, d_steps, d_bct, (int)(bct.size() / 2), d_lr, 0.9f, 0.999f, 1e-5f, 0.5f, 1,
                         d_G, d_P, d_M, d_V, d_W2X, st));
   HIP_OK(hipStreamSynchronize(st));

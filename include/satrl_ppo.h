@@ -57,15 +57,21 @@ int satrl_ppo_sizes(int H, int mb, int64_t* n_head_wg, int64_t* n_norm_blocks);
  * (satrl_ppo_rowpass_dw2), H = 256 runs it from k-packed planes
  * (satrl_ppo_rowpass_kx + satrl_ppo_dw2_kx).                              */
 int satrl_ppo_dw2_splits(int H, int mb);
-int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream);
+/* Capacities (every call that writes or reads the dW2 slabs or the k-packed
+ * planes takes the caller's buffer size and refuses with -1, before any
+ * launch, when the call would run past it): p2_floats = elements of p2,
+ * at least (net == 0 ? 1 : 2) * S * H * H; kx_elems = elements of EACH of
+ * H1x / dZ2x, at least satrl_ppo_kx_elems(H, mb) (half of it for net 0).  */
+int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, int64_t p2_floats,
+                  void* stream);
 
 /* mode 1: sum the partial slabs into G (p2: dW2 split-K [2][S][H][H], p1:
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
  * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and
  * advance steps [net] (f64); mode 3: both.  (mode 1 | all-reduce(G) | mode 2
  * under data parallelism.)  Every sum has a fixed order.                  */
-int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, const float* p1, const float* pt,
-                     float* G, double* nsq, double* steps, void* stream);
+int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, int64_t p2_floats, const float* p1,
+                     const float* pt, float* G, double* nsq, double* steps, void* stream);
 
 /* Data parallelism, after the all-reduce (SUM) of G over `world` ranks:
  * G /= world (IEEE division, = torch's div_ of the gradient average), then
@@ -125,8 +131,9 @@ int satrl_ppo_rowpass_ratio(int H, int mb, int net, const float* src, const int6
  * minibatch step is three launches (rowpass_dw2, reduce, adam).            */
 int satrl_ppo_row_blocks(int H, int mb);
 int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                          const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
-                          float* pw1, void* stream);
+                          const void* W2X, float epsilon, float ent_coef, float max_action, float* p2,
+                          int64_t p2_floats /* >= (net == 0 ? 1 : 2) * S * H * H */, float* ptail, float* pw1,
+                          void* stream);
 
 /* H = 256, every minibatch (32-row workgroups above 1024 rows, 16-row ones
  * up to it): the rowpass with H1 and dZ2 written as k-packed bf16 planes (each element split hi + mid +
@@ -139,10 +146,11 @@ int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_
  * minibatch step is then rowpass_kx, dw2_kx, reduce(S), adam.              */
 int64_t satrl_ppo_kx_elems(int H, int mb);
 int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
-                         float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, float* ptail,
-                         float* pw1, void* stream);
+                         float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, int64_t kx_elems,
+                         float* ptail, float* pw1, void* stream);
 int satrl_ppo_dw2_kx_splits(int H, int mb, int net);
-int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, float* p2, void* stream);
+int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
+                     int64_t p2_floats, void* stream);
 
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result
  * is independent of N and of the sharding, and the rollout's log-probs equal
@@ -175,6 +183,23 @@ int satrl_ppo_group_advance(int64_t* group, void* stream);
  * for torch.tanh in Actor_Gaussian / Critic.forward (ppo_continuous.py:61-134):
  * the hook of its exhaustive accuracy test.                               */
 int satrl_ppo_tanh(int64_t n, const float* x, float* y, void* stream);
+
+/* Live launch spans (measurement only; bench.py): while a probe buffer is
+ * set, every launch of the rowpass, dW2 (k-packed), reduce, Adam, policy /
+ * value and env-step (satenv.h) kernels -- eager or captured into a graph --
+ * runs the kernel's SPAN instantiation, which differs from the product one
+ * only in that lane 0 of every wave stores the wave's (start, exit)
+ * s_memrealtime pair (100 MHz) into a region of the buffer of its own: 2
+ * u64 per wave, regions taken in launch order.  A graph captured meanwhile
+ * keeps its regions: each replay rewrites them.  satrl_span_probe(buf,
+ * bytes, stream) zeroes buf on `stream` and starts the log; (NULL, 0) stops
+ * probing (launches run the product instantiations again).  Launch i of the
+ * log: its kernel kind (0 rowpass, 1 dW2, 2 reduce, 3 Adam, 4 policy_act, 5
+ * policy_value, 6 env step), the u64 offset of its records and its wave
+ * count; its span = max(exit) - min(start) over its waves.                */
+int satrl_span_probe(void* buf, int64_t bytes, void* stream);
+int64_t satrl_span_probe_launches(void);
+int satrl_span_probe_launch(int64_t i, int* kind, int64_t* word_offset, int64_t* waves);
 
 const char* satrl_ppo_last_error(void);
 

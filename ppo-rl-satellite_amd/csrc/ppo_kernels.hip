@@ -17,8 +17,10 @@
 #include <cstdlib>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "philox_device.h"
+#include "span_probe.h"
 #include "satrl_ppo.h"
 #include "satrl_peer.h"
 
@@ -728,14 +730,16 @@ __device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d
   return od;
 }
 
-template <int H, int NW, int R = kRows, bool FDW2 = false, bool KX = false>
+template <int H, int NW, int R = kRows, bool FDW2 = false, bool KX = false, bool SPAN = false>
 __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb, const float* __restrict__ src,
                                                       const int64_t* __restrict__ idx, const float* __restrict__ P,
                                                       const void* __restrict__ W2X, float epsilon, float ent_coef,
                                                       float max_action, float* __restrict__ H1g,
                                                       float* __restrict__ dZ2g, float* __restrict__ ptail,
                                                       float* __restrict__ pw1, int net_sel, float* __restrict__ p2,
-                                                      int S2, float* __restrict__ ratio_out, float inv_mb) {
+                                                      int S2, float* __restrict__ ratio_out, float inv_mb,
+                                                      unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;   // (SPAN: the measurement instantiation)
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, NT = NW * 64;
   static_assert(!FDW2 || R == 32, "the fused dW2 partial covers one 32-row block (dw2_kernel's chunk)");
   // KX: H1 / dZ2 go out as k-packed bf16 planes (store_kx; H1g / dZ2g point at
@@ -1062,6 +1066,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         for (int q = 0; q < 4; ++q) out[(int64_t)(n0 + 16 * t + 4 * lg + q) * H + 16 * j + li] = a2[j][q];
     }
   }
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1080,7 +1085,7 @@ constexpr int kPolRows = 32;   // rows per policy workgroup
 constexpr int kPolNW = 8;      // waves per policy workgroup at H = 256 (16: 61.6 vs 52.3 us per rollout step;
                                // with the wave priority 46.5-47.6 vs 45.1-45.2 us per launch)
 
-template <int H, int NW, int MODE>
+template <int H, int NW, int MODE, bool SPAN = false>
 __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float* __restrict__ obs,
                                                      const float* __restrict__ P0, const float* __restrict__ P1,
                                                      int nagents, float max_action, uint32_t k00, uint32_t k01,
@@ -1088,7 +1093,8 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
                                                      const uint64_t* __restrict__ step_base,
                                                      float* __restrict__ act0, float* __restrict__ logp0,
                                                      float* __restrict__ act1, float* __restrict__ logp1,
-                                                     float* __restrict__ value) {
+                                                     float* __restrict__ value, unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;
   constexpr int R = kPolRows, RT = R / 16, CT = H / 16 / NW;
   // Two or more workgroups share a CU, and one finishing its output layer
   // would out-issue (oldest first) one that is still streaming W1 / W2: at
@@ -1129,10 +1135,14 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   float w3[CT][3];
   mlp_forward<H, NW, R, false, true>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
   const int r = threadIdx.x;
-  if (r >= nvalid) return;                                       // no barrier follows
+  if (r >= nvalid) {                                             // no barrier follows
+    if constexpr (SPAN) satrl_span::exit(span, span_t0);
+    return;
+  }
   const int64_t i = r0 + r;
   if (MODE == 1) {
     value[i] = out_sum<H / 16, R>(sm.osum, r, 0) + P[L.b3c];
+    if constexpr (SPAN) satrl_span::exit(span, span_t0);
     return;
   }
   float z[4];
@@ -1145,6 +1155,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
     const float mu = max_action * tanh_f32(out_sum<H / 16, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
     gaussian_act(mu, P[L.ls + d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
   }
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1314,10 +1325,12 @@ __device__ __forceinline__ void dw2_kx_body(int b, int mb, int S, int KR, int ne
       for (int q = 0; q < 4; ++q)
         out[(int64_t)(o0 + (TW / 2) * wo + 16 * x + 4 * lg + q) * H + n0 + (TW / 2) * wn + 16 * y + li] = acc[x][y][q];
 }
-template <int TW>
+template <int TW, bool SPAN = false>
 __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int net_sel,
                                                      const unsigned short* __restrict__ H1x,
-                                                     const unsigned short* __restrict__ dZ2x, float* __restrict__ p2) {
+                                                     const unsigned short* __restrict__ dZ2x, float* __restrict__ p2,
+                                                     unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;
   __shared__ __attribute__((aligned(16))) KxSmem<TW> sm;
   // at priority 3 until a wave has staged its last chunk (dw2_kx_body), as
   // the policy kernel: in-graph step 48.8 against 49.1 us at mb 4096 over
@@ -1325,6 +1338,7 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
   // bitwise the same (EXPERIMENTS.md round 5)
   __builtin_amdgcn_s_setprio(3);
   dw2_kx_body<TW>(blockIdx.x, mb, S, KR, net_sel, H1x, dZ2x, p2, sm);
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 // split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split
 constexpr int kKxWgs = 256;
@@ -1558,10 +1572,13 @@ __device__ __forceinline__ void reduce_block(int H, const Layout& L, const RedGe
   }
 }
 
+template <bool SPAN = false>
 __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode, const float* __restrict__ p2,
                                                      const float* __restrict__ p1, const float* __restrict__ pt,
                                                      float* __restrict__ G, double* __restrict__ nsq,
-                                                     double* __restrict__ steps, int world) {
+                                                     double* __restrict__ steps, int world,
+                                                     unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float4 red[256];
@@ -1585,6 +1602,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
       }
     }
   }
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1631,13 +1649,16 @@ __device__ __forceinline__ float adam_elem(float g, float& m, float& v, float p,
   return p + (-step_size) * (m / denom);                           // addcdiv_(m, denom, -step_size)
 }
 
+template <bool SPAN = false>
 __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double* __restrict__ nsq,
                                                    const double* __restrict__ steps, const double* __restrict__ bct,
                                                    int bct_len, const float* __restrict__ lr, float beta1,
                                                    float beta2, float eps, float max_norm, int use_clip,
                                                    const float* __restrict__ G, float* __restrict__ P,
                                                    float* __restrict__ M, float* __restrict__ V,
-                                                   void* __restrict__ W2X, int net_sel) {
+                                                   void* __restrict__ W2X, int net_sel,
+                                                   unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;
   const Layout L = layout(H);
   __shared__ double sh[8];
   __shared__ float tile[32][33];
@@ -1713,7 +1734,10 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   }
   const float w1 = (float)(1.0 - (double)beta1);                  // lerp weight 1 - beta1
   const float w2 = (float)(1.0 - (double)beta2);
-  if (!live) return;                                               // (W1.. tail blocks only: no barrier follows)
+  if (!live) {                                                     // (W1.. tail blocks only: no barrier follows)
+    if constexpr (SPAN) satrl_span::exit(span, span_t0);
+    return;
+  }
   float4 pn;
   pn.x = adam_elem(g.x, m.x, v.x, p.x, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
   pn.y = adam_elem(g.y, m.y, v.y, p.y, coef, ss, b2s, w1, w2, beta2, eps, use_clip);
@@ -1724,6 +1748,7 @@ __global__ void __launch_bounds__(256) adam_kernel(int H, int nblk, const double
   V4[e4] = v;
   if ((int)blockIdx.x < nbw && W2X != nullptr)                     // keep the fc2 operand image current
     w2x_tile(H, net, blockIdx.x % (ntc * ntc), pn, W2X, tile);
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1788,6 +1813,27 @@ int n_adam_blocks(int H, int net) {
 
 bool valid_h(int H) { return H == 64 || H == 128 || H == 256; }
 
+// Caller-buffer capacity checks of the C-ABI (before any launch).  A one-net
+// call (net 1) addresses the second half of a [2][...] buffer, so only net 0
+// may pass half the size.
+int64_t nets_span(int net) { return net == 0 ? 1 : 2; }
+// p2 [2][S][H][H] f32 split-K slabs
+bool p2_fits(int H, int net, int S, int64_t p2_floats, const char* who) {
+  const int64_t need = nets_span(net) * (int64_t)S * H * H;
+  if (p2_floats >= need) return true;
+  g_err = std::string(who) + ": p2 holds " + std::to_string(p2_floats) + " floats, " + std::to_string(S) +
+          " splits need " + std::to_string(need);
+  return false;
+}
+// the k-packed planes u16 [2][3][kx_rows(mb)][H] (satrl_ppo_kx_elems)
+bool kx_fits(int H, int mb, int net, int64_t kx_elems, const char* who) {
+  const int64_t need = nets_span(net) * 3 * kx_rows(mb) * H;
+  if (kx_elems >= need) return true;
+  g_err = std::string(who) + ": the H1x / dZ2x planes hold " + std::to_string(kx_elems) + " elements, mb " +
+          std::to_string(mb) + " needs " + std::to_string(need);
+  return false;
+}
+
 #define LAUNCH_CHECK()                                                      \
   do {                                                                      \
     hipError_t e_ = hipGetLastError();                                      \
@@ -1840,14 +1886,28 @@ __device__ __forceinline__ void peer_push(unsigned long long* base, int64_t word
   __hip_atomic_store((gu64*)(base) + word, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// the sticky error word of a rank's buffer (after the per-block counters)
+__device__ __forceinline__ gu64* peer_err_word(unsigned long long* base) {
+  return (gu64*)(base) + (4 * kPeerMaxBlocks) / 8;
+}
 // the value of a granule once its tag is `tag` (bounded wait: once a wait of
-// this thread has run out, the rest return at once, the call being invalid)
+// this thread has run out, the rest return at once, the call being invalid).
+// Every 16th poll also reads this rank's own error word (`mine`): a peer that
+// gave up sets it in every rank's buffer, so the survivors fail fast instead
+// of spending their own deadline
 __device__ __forceinline__ float peer_pull(const unsigned long long* base, int64_t word, unsigned tag,
-                                           unsigned long long t0, unsigned long long ticks, bool& ok) {
+                                           unsigned long long* mine, unsigned long long t0,
+                                           unsigned long long ticks, bool& ok) {
   const gu64* g = (const gu64*)(base) + word;
   unsigned long long x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned polls = 0;
   while (ok && (unsigned)(x >> 32) != tag) {
     if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { ok = false; break; }   // 100 MHz ticks
+    if ((++polls & 15u) == 0 &&
+        __hip_atomic_load(peer_err_word(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) {
+      ok = false;
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
     x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -1876,13 +1936,20 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
   const int64_t n = L.total, sl = peer_slice(n, world);
   unsigned long long* mine = pb.buf[rank];
   const int64_t rs = kPeerHdr / 8, ag = rs + (int64_t)world * sl;  // word offsets of the two slot arrays
+  __shared__ int failed_s;
   if (t == 0) {                                                    // this call's tag: block b's counter + 1
+    // a failed call earlier (this rank's or a peer's: the word is set in every
+    // buffer) makes every later call return at once -- the update is invalid
+    // until PeerComm.reset, and the calls queued behind the failure (up to a
+    // graph group of them) must not each spend the deadline again
+    failed_s = __hip_atomic_load(peer_err_word(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull;
     gu32* ep = (gu32*)(reinterpret_cast<unsigned*>(mine)) + b;
     const unsigned e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
     __hip_atomic_store(ep, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     tag_s = e;
   }
   __syncthreads();
+  if (failed_s) return;                                            // (uniform: no barrier skipped by some threads)
   const unsigned tag = tag_s;
   double st0 = 0.0, st1 = 0.0;                                     // (advanced at the end, as reduce_kernel)
   if (b == 0 && t == 0) { st0 = steps[0]; st1 = steps[1]; }
@@ -1905,10 +1972,13 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
   // 2: this rank's slice, summed in rank order, / world, to every gather slot [rank]
   const int64_t mylen = min(sl, n - (int64_t)rank * sl);
   for (int64_t k = (int64_t)b * 256 + t; k < mylen; k += (int64_t)nb * 256) {
-    float v = peer_pull(mine, rs + k, tag, t0, ticks, ok);
-    for (int j = 1; j < world; ++j) v += peer_pull(mine, rs + (int64_t)j * sl + k, tag, t0, ticks, ok);
+    float v = peer_pull(mine, rs + k, tag, mine, t0, ticks, ok);
+    for (int j = 1; j < world; ++j) v += peer_pull(mine, rs + (int64_t)j * sl + k, tag, mine, t0, ticks, ok);
     v = v / (float)world;                                         // G.div_(world) (reduce_dp's IEEE division)
-    for (int j = 0; j < world; ++j) peer_push(pb.buf[j], ag + (int64_t)rank * sl + k, tag, v);
+    // a sum with a missing term is never pushed: a slow peer must not take it
+    // for a valid result (it times out, or fails fast on the error word)
+    if (ok)
+      for (int j = 0; j < world; ++j) peer_push(pb.buf[j], ag + (int64_t)rank * sl + k, tag, v);
   }
   // 3: gather each float4 into G; its squares to that reduce_dp block's norm pair
   for (int rb = b; rb < nred; rb += nb) {
@@ -1919,7 +1989,7 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t e = col * 4 + q, j = e / sl;
-        e4[q] = peer_pull(mine, ag + j * sl + (e - j * sl), tag, t0, ticks, ok);
+        e4[q] = peer_pull(mine, ag + j * sl + (e - j * sl), tag, mine, t0, ticks, ok);
       }
       const float4 v = make_float4(e4[0], e4[1], e4[2], e4[3]);
       reinterpret_cast<float4*>(G)[col] = v;
@@ -1935,15 +2005,34 @@ __global__ void __launch_bounds__(256) peer_allreduce_kernel(int H, RedGeom g, i
     }
     __syncthreads();                                               // sh is reused by the next block_sum2
   }
-  if (!ok) {                                                       // a peer never pushed: flag it
-    gu64* err = (gu64*)(mine) + (4 * kPeerMaxBlocks) / 8;
-    __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!ok) {
+    // a peer never pushed (or one gave up): flag it in EVERY rank's buffer, so
+    // a peer that is slow but alive fails this call too (its waits poll the
+    // word) instead of completing it, and every later call returns at once
+    for (int j = 0; j < world; ++j)
+      __hip_atomic_store(peer_err_word(pb.buf[j]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (b == 0 && t == 0) { steps[0] = st0 + 1.0; steps[1] = st1 + 1.0; }
 }
 
 
+struct SpanLaunch { int kind; int64_t off, waves; };
+struct SpanState {
+  unsigned long long* buf = nullptr;
+  int64_t words = 0, used = 0;
+  std::vector<SpanLaunch> log;
+};
+SpanState g_span;
+
 }  // namespace
+
+unsigned long long* satrl_span::take(int kind, int64_t waves) {
+  if (!g_span.buf || waves <= 0 || g_span.used + 2 * waves > g_span.words) return nullptr;
+  unsigned long long* p = g_span.buf + g_span.used;
+  g_span.log.push_back(SpanLaunch{kind, g_span.used, waves});
+  g_span.used += 2 * waves;
+  return p;
+}
 
 extern "C" {
 
@@ -1980,23 +2069,31 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
   hipStream_t s = (hipStream_t)stream;
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
   const float inv_mb = 1.0f / (float)mb;
-#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio, inv_mb
+  const int nw = H == 64 ? 4 : H == 128 ? 8 : 16;                  // waves per workgroup
+  unsigned long long* sp = satrl_span::take(satrl_span::kRowpass, (int64_t)g.x * nw);
+#define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio, inv_mb, sp
+#define RP_LAUNCH(HH, NWW, RR, F, K)                                                                          \
+  do {                                                                                                        \
+    if (sp) hipLaunchKernelGGL((rowpass_kernel<HH, NWW, RR, F, K, true>), g, dim3(NWW * 64), 0, s, RP_ARGS);  \
+    else hipLaunchKernelGGL((rowpass_kernel<HH, NWW, RR, F, K>), g, dim3(NWW * 64), 0, s, RP_ARGS);           \
+  } while (0)
   if (H == 64 && fdw2)
-    hipLaunchKernelGGL((rowpass_kernel<64, 4, kRows, true>), g, dim3(256), 0, s, RP_ARGS);
+    RP_LAUNCH(64, 4, kRows, true, false);
   else if (H == 64)
-    hipLaunchKernelGGL((rowpass_kernel<64, 4>), g, dim3(256), 0, s, RP_ARGS);
+    RP_LAUNCH(64, 4, kRows, false, false);
   else if (H == 128 && fdw2)
-    hipLaunchKernelGGL((rowpass_kernel<128, 8, kRows, true>), g, dim3(512), 0, s, RP_ARGS);
+    RP_LAUNCH(128, 8, kRows, true, false);
   else if (H == 128)
-    hipLaunchKernelGGL((rowpass_kernel<128, 8>), g, dim3(512), 0, s, RP_ARGS);
+    RP_LAUNCH(128, 8, kRows, false, false);
   else if (kx && R == kRowsShort)
-    hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort, false, true>), g, dim3(16 * 64), 0, s, RP_ARGS);
+    RP_LAUNCH(256, 16, kRowsShort, false, true);
   else if (kx)
-    hipLaunchKernelGGL((rowpass_kernel<256, kNW256, kRows, false, true>), g, dim3(kNW256 * 64), 0, s, RP_ARGS);
+    RP_LAUNCH(256, kNW256, kRows, false, true);
   else if (R == kRowsShort)
-    hipLaunchKernelGGL((rowpass_kernel<256, 16, kRowsShort>), g, dim3(16 * 64), 0, s, RP_ARGS);
+    RP_LAUNCH(256, 16, kRowsShort, false, false);
   else
-    hipLaunchKernelGGL((rowpass_kernel<256, kNW256>), g, dim3(kNW256 * 64), 0, s, RP_ARGS);
+    RP_LAUNCH(256, kNW256, kRows, false, false);
+#undef RP_LAUNCH
 #undef RP_ARGS
   LAUNCH_CHECK();
   return 0;
@@ -2027,10 +2124,11 @@ int satrl_ppo_row_blocks(int H, int mb) {
 }
 
 int satrl_ppo_rowpass_dw2(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
-                          const void* W2X, float epsilon, float ent_coef, float max_action, float* p2, float* ptail,
-                          float* pw1, void* stream) {
+                          const void* W2X, float epsilon, float ent_coef, float max_action, float* p2,
+                          int64_t p2_floats, float* ptail, float* pw1, void* stream) {
   if ((H != 64 && H != 128) || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !p2 || !ptail || !pw1)
     return -1;
+  if (!p2_fits(H, net, n_head_wg(H, mb), p2_floats, "satrl_ppo_rowpass_dw2")) return -1;   // one slab per row block
   return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, nullptr, nullptr, ptail, pw1, p2,
                         nullptr, true, stream);
 }
@@ -2041,11 +2139,12 @@ int64_t satrl_ppo_kx_elems(int H, int mb) {
 }
 
 int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t* idx, const float* P, const void* W2X,
-                         float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, float* ptail,
-                         float* pw1, void* stream) {
+                         float epsilon, float ent_coef, float max_action, void* H1x, void* dZ2x, int64_t kx_elems,
+                         float* ptail, float* pw1, void* stream) {
   if (H != 256 || mb <= 0 || net < -1 || net > 1 || !src || !P || !W2X || !H1x || !dZ2x ||
       !ptail || !pw1)
     return -1;
+  if (!kx_fits(H, mb, net, kx_elems, "satrl_ppo_rowpass_kx")) return -1;
   return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, static_cast<float*>(H1x),
                         static_cast<float*>(dZ2x), ptail, pw1, nullptr, nullptr, false, stream, true);
 }
@@ -2055,13 +2154,21 @@ int satrl_ppo_dw2_kx_splits(int H, int mb, int net) {
   return kx_splits(mb, net);
 }
 
-int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, float* p2, void* stream) {
+int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
+                     int64_t p2_floats, void* stream) {
   if (H != 256 || mb <= 0 || net < -1 || net > 1 || S < 1 || !H1x || !dZ2x || !p2) return -1;
   const int nch = (int)(kx_rows(mb) / 32), cps = (nch + S - 1) / S;
   if ((int64_t)cps * (S - 1) >= nch) return -1;                  // an empty split: use satrl_ppo_dw2_kx_splits
+  if (!kx_fits(H, mb, net, kx_elems, "satrl_ppo_dw2_kx") || !p2_fits(H, net, S, p2_floats, "satrl_ppo_dw2_kx"))
+    return -1;
   const dim3 g((unsigned)((net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW) * S));
-  hipLaunchKernelGGL(dw2_kx_kernel<kKxTW>, g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net,
-                     static_cast<const unsigned short*>(H1x), static_cast<const unsigned short*>(dZ2x), p2);
+  unsigned long long* sp = satrl_span::take(satrl_span::kDw2, (int64_t)g.x * 4);
+  if (sp)
+    hipLaunchKernelGGL((dw2_kx_kernel<kKxTW, true>), g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net,
+                       static_cast<const unsigned short*>(H1x), static_cast<const unsigned short*>(dZ2x), p2, sp);
+  else
+    hipLaunchKernelGGL((dw2_kx_kernel<kKxTW>), g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net,
+                       static_cast<const unsigned short*>(H1x), static_cast<const unsigned short*>(dZ2x), p2, sp);
   LAUNCH_CHECK();
   return 0;
 }
@@ -2071,10 +2178,12 @@ int satrl_ppo_dw2_splits(int H, int mb) {
   return dw2_splits(H, mb, -1);
 }
 
-int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, void* stream) {
+int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* dZ2, float* p2, int64_t p2_floats,
+                  void* stream) {
   if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || S < 1 || !H1 || !dZ2 || !p2) return -1;
   const int KR = ((mb + S - 1) / S + kDwKC - 1) / kDwKC * kDwKC;
   if ((int64_t)KR * (S - 1) >= mb) return -1;                    // an empty split: use satrl_ppo_dw2_splits
+  if (!p2_fits(H, net, S, p2_floats, "satrl_ppo_dw2")) return -1;
   const dim3 g((unsigned)((net < 0 ? 2 : 1) * (H / 64) * (H / 64) * S));
   hipStream_t st = (hipStream_t)stream;
   if (H == 64)
@@ -2087,14 +2196,20 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
   return 0;
 }
 
-int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, const float* p1, const float* pt,
-                     float* G, double* nsq, double* steps, void* stream) {
+int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, int64_t p2_floats, const float* p1,
+                     const float* pt, float* G, double* nsq, double* steps, void* stream) {
   if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || S < 1 || mode < 1 || mode > 3 || !G) return -1;
   if ((mode & 1) && (!p2 || !p1 || !pt)) return -1;
+  if ((mode & 1) && !p2_fits(H, net, S, p2_floats, "satrl_ppo_reduce")) return -1;   // the slabs it reads
   if ((mode & 2) && (!nsq || !steps)) return -1;
   const RedGeom g = geom(H, mb, S, net);
-  hipLaunchKernelGGL(reduce_kernel, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1, pt, G,
-                     nsq, steps, 1);
+  unsigned long long* sp = satrl_span::take(satrl_span::kReduce, (int64_t)n_blocks(g) * 4);
+  if (sp)
+    hipLaunchKernelGGL(reduce_kernel<true>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1,
+                       pt, G, nsq, steps, 1, sp);
+  else
+    hipLaunchKernelGGL(reduce_kernel<false>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2,
+                       p1, pt, G, nsq, steps, 1, sp);
   LAUNCH_CHECK();
   return 0;
 }
@@ -2102,8 +2217,8 @@ int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, c
 int satrl_ppo_reduce_dp(int H, int mb, int net, int world, float* G, double* nsq, double* steps, void* stream) {
   if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || world < 1 || !G || !nsq || !steps) return -1;
   const RedGeom g = geom(H, mb, 1, net);
-  hipLaunchKernelGGL(reduce_kernel, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, 2, nullptr, nullptr,
-                     nullptr, G, nsq, steps, world);
+  hipLaunchKernelGGL(reduce_kernel<false>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, 2, nullptr,
+                     nullptr, nullptr, G, nsq, steps, world, nullptr);
   LAUNCH_CHECK();
   return 0;
 }
@@ -2217,8 +2332,13 @@ int satrl_ppo_adam(int H, int mb, int net, const double* nsq, const double* step
       !M || !V)
     return -1;
   const int nblk = n_blocks(geom(H, mb, 1, net));
-  hipLaunchKernelGGL(adam_kernel, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk, nsq,
-                     steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2X, net);
+  unsigned long long* sp = satrl_span::take(satrl_span::kAdam, (int64_t)n_adam_blocks(H, net) * 4);
+  if (sp)
+    hipLaunchKernelGGL(adam_kernel<true>, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk,
+                       nsq, steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2X, net, sp);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, dim3(n_adam_blocks(H, net)), dim3(256), 0, (hipStream_t)stream, H, nblk,
+                       nsq, steps, bct, bct_len, lr, beta1, beta2, eps, max_norm, use_clip, G, P, M, V, W2X, net, sp);
   LAUNCH_CHECK();
   return 0;
 }
@@ -2261,15 +2381,23 @@ int satrl_policy_act(int H, int64_t N, const float* obs, const float* P0, const 
   philox_key(seed, 1, k10, k11);
   const dim3 g((unsigned)(nag * ((N + kPolRows - 1) / kPolRows)));
   hipStream_t s = (hipStream_t)stream;
+  const int nw = H == 64 ? 4 : H == 128 ? 8 : kPolNW;
+  unsigned long long* sp = satrl_span::take(satrl_span::kPolicyAct, (int64_t)g.x * nw);
+#define POL_ARGS N, obs, P0, P1, nag, max_action, k00, k01, k10, k11, env_offset, step, step_base, act0, logp0, act1, \
+                 logp1, nullptr, sp
+#define POL_LAUNCH(HH, NWW)                                                                               \
+  do {                                                                                                    \
+    if (sp) hipLaunchKernelGGL((policy_kernel<HH, NWW, 0, true>), g, dim3(NWW * 64), 0, s, POL_ARGS);     \
+    else hipLaunchKernelGGL((policy_kernel<HH, NWW, 0>), g, dim3(NWW * 64), 0, s, POL_ARGS);              \
+  } while (0)
   if (H == 64)
-    hipLaunchKernelGGL((policy_kernel<64, 4, 0>), g, dim3(256), 0, s, N, obs, P0, P1, nag, max_action, k00, k01, k10,
-                       k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
+    POL_LAUNCH(64, 4);
   else if (H == 128)
-    hipLaunchKernelGGL((policy_kernel<128, 8, 0>), g, dim3(512), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
-                       k10, k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
+    POL_LAUNCH(128, 8);
   else
-    hipLaunchKernelGGL((policy_kernel<256, kPolNW, 0>), g, dim3(kPolNW * 64), 0, s, N, obs, P0, P1, nag, max_action, k00, k01,
-                       k10, k11, env_offset, step, step_base, act0, logp0, act1, logp1, nullptr);
+    POL_LAUNCH(256, kPolNW);
+#undef POL_LAUNCH
+#undef POL_ARGS
   LAUNCH_CHECK();
   return 0;
 }
@@ -2278,15 +2406,23 @@ int satrl_policy_value(int H, int64_t N, const float* obs, const float* P, float
   if (!valid_h(H) || N <= 0 || !obs || !P || !v_out) return -1;
   const dim3 g((unsigned)((N + kPolRows - 1) / kPolRows));
   hipStream_t s = (hipStream_t)stream;
+  const int nw = H == 64 ? 4 : H == 128 ? 8 : kPolNW;
+  unsigned long long* sp = satrl_span::take(satrl_span::kPolicyValue, (int64_t)g.x * nw);
+#define VAL_ARGS N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u, (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, \
+                 nullptr, nullptr, v_out, sp
+#define VAL_LAUNCH(HH, NWW)                                                                               \
+  do {                                                                                                    \
+    if (sp) hipLaunchKernelGGL((policy_kernel<HH, NWW, 1, true>), g, dim3(NWW * 64), 0, s, VAL_ARGS);     \
+    else hipLaunchKernelGGL((policy_kernel<HH, NWW, 1>), g, dim3(NWW * 64), 0, s, VAL_ARGS);              \
+  } while (0)
   if (H == 64)
-    hipLaunchKernelGGL((policy_kernel<64, 4, 1>), g, dim3(256), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
-                       (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
+    VAL_LAUNCH(64, 4);
   else if (H == 128)
-    hipLaunchKernelGGL((policy_kernel<128, 8, 1>), g, dim3(512), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
-                       (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
+    VAL_LAUNCH(128, 8);
   else
-    hipLaunchKernelGGL((policy_kernel<256, kPolNW, 1>), g, dim3(kPolNW * 64), 0, s, N, obs, P, nullptr, 1, 0.0f, 0u, 0u, 0u, 0u,
-                       (int64_t)0, (uint64_t)0, nullptr, nullptr, nullptr, nullptr, nullptr, v_out);
+    VAL_LAUNCH(256, kPolNW);
+#undef VAL_LAUNCH
+#undef VAL_ARGS
   LAUNCH_CHECK();
   return 0;
 }
@@ -2295,6 +2431,33 @@ int satrl_ppo_tanh(int64_t n, const float* x, float* y, void* stream) {
   if (n <= 0 || n > (int64_t)256 * 0x7FFFFFFF || !x || !y) return -1;
   hipLaunchKernelGGL(tanh_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, x, y);
   LAUNCH_CHECK();
+  return 0;
+}
+
+// live launch spans (span_probe.h): the probe buffer, its bump pointer and
+// the launch log, host state of the library (one probe per process)
+int satrl_span_probe(void* buf, int64_t bytes, void* stream) {
+  if ((buf == nullptr) != (bytes == 0) || bytes < 0) return -1;
+  g_span.buf = static_cast<unsigned long long*>(buf);
+  g_span.words = bytes / 8;
+  if (!buf) return 0;                                              // stop: the log stays readable
+  g_span.used = 0;
+  g_span.log.clear();
+  if (hipMemsetAsync(buf, 0, (size_t)bytes, (hipStream_t)stream) != hipSuccess) {
+    g_span = SpanState{};
+    g_err = "satrl_span_probe: hipMemsetAsync failed";
+    return -2;
+  }
+  return 0;
+}
+
+int64_t satrl_span_probe_launches(void) { return (int64_t)g_span.log.size(); }
+
+int satrl_span_probe_launch(int64_t i, int* kind, int64_t* word_offset, int64_t* waves) {
+  if (i < 0 || i >= (int64_t)g_span.log.size() || !kind || !word_offset || !waves) return -1;
+  *kind = g_span.log[(size_t)i].kind;
+  *word_offset = g_span.log[(size_t)i].off;
+  *waves = g_span.log[(size_t)i].waves;
   return 0;
 }
 

@@ -19,6 +19,7 @@
 #include "satenv.h"
 #include "satenv_device.h"
 #include "satenv_step.h"
+#include "span_probe.h"
 #include "ellipse_device.h"
 #include "surrogate_device.h"
 
@@ -213,9 +214,11 @@ __device__ __forceinline__ Elements get_elements(const double (*src)[E], int lan
 // ENVS envs per workgroup (lanes >= ENVS of each wave idle): fewer envs per
 // wave put more waves, i.e. more independent dependency chains, on each SIMD
 // when N is small (the step is latency bound there); 64 at large N
-template <bool AUTORESET, int ENVS>
+template <bool AUTORESET, int ENVS, bool SPAN = false>
 __global__ void __launch_bounds__(256) step_kernel_wide(const Params prm, int64_t n, double* __restrict__ f64,
-                                                        int32_t* __restrict__ i32, StepIO io) {
+                                                        int32_t* __restrict__ i32, StepIO io,
+                                                        unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;   // (SPAN: span_probe.h)
   __shared__ WideSmem<ENVS> sm;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool env_lane = lane < ENVS;
@@ -340,6 +343,7 @@ __global__ void __launch_bounds__(256) step_kernel_wide(const Params prm, int64_
   }
   if (w == 0 && io.stats) wave_stats(io.stats, fin, fin_ret, rew_acc, cap);
   ENV_PROBE(6);
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 
 __global__ void __launch_bounds__(256) reset_kernel(const Params prm, int64_t n, double* __restrict__ f64,
@@ -689,15 +693,21 @@ void launch_step(satenv_env* h, const StepIO& io, void* stream) {
   else if (h->split == 2) {
     const int envs = wide_envs(h);
     const dim3 gw(grid_for(h->n, envs));
+    // the product geometry (64 envs per workgroup) has a SPAN instantiation
+    // for the bench's live launch spans (span_probe.h)
+    unsigned long long* sp = envs == 64 ? satrl_span::take(satrl_span::kEnvStep, (int64_t)gw.x * 4) : nullptr;
     if (envs == 16)
       hipLaunchKernelGGL((step_kernel_wide<AR, 16>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
-                         h->i32, io);
+                         h->i32, io, nullptr);
     else if (envs == 32)
       hipLaunchKernelGGL((step_kernel_wide<AR, 32>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
-                         h->i32, io);
+                         h->i32, io, nullptr);
+    else if (sp)
+      hipLaunchKernelGGL((step_kernel_wide<AR, 64, true>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n,
+                         h->f64, h->i32, io, sp);
     else
       hipLaunchKernelGGL((step_kernel_wide<AR, 64>), gw, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64,
-                         h->i32, io);
+                         h->i32, io, nullptr);
   }
   else if (h->split == 1)
     hipLaunchKernelGGL(step_kernel_split<AR>, grid, dim3(256), 0, (hipStream_t)stream, h->prm, h->n, h->f64, h->i32,

@@ -107,8 +107,9 @@ _SIGS = {
     "satrl_ppo_layout": ([C.c_int, C.POINTER(_i64)], C.c_int),
     "satrl_ppo_sizes": ([C.c_int, C.c_int, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
     "satrl_ppo_dw2_splits": ([C.c_int, C.c_int], C.c_int),
-    "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
-    "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_dw2": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _i64, _vp], C.c_int),
+    "satrl_ppo_reduce": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+                         C.c_int),
     "satrl_ppo_reduce_dp": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_adam": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_float, C.c_float, C.c_float,
                         C.c_float, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
@@ -120,12 +121,12 @@ _SIGS = {
     "satrl_ppo_w2x_floats": ([C.c_int], _i64),
     "satrl_ppo_kx_elems": ([C.c_int, C.c_int], _i64),
     "satrl_ppo_rowpass_kx": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
-                              _vp, _vp, _vp, _vp], C.c_int),
+                              _vp, _i64, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_dw2_kx_splits": ([C.c_int, C.c_int, C.c_int], C.c_int),
-    "satrl_ppo_dw2_kx": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "satrl_ppo_dw2_kx": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _i64, _vp, _i64, _vp], C.c_int),
     "satrl_ppo_w2x_sync": ([C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
-                               _vp, _vp, _vp], C.c_int),
+                               _i64, _vp, _vp, _vp], C.c_int),
     "satrl_peer_buffer_bytes": ([_i64, C.c_int, _vp], C.c_int),
     "satrl_peer_alloc": ([_i64, _vp, _vp], C.c_int),
     "satrl_peer_open": ([_vp, _vp], C.c_int),
@@ -142,6 +143,9 @@ _SIGS = {
     "satrl_ppo_stage": ([_i64, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_group_advance": ([_vp, _vp], C.c_int),
     "satrl_ppo_tanh": ([_i64, _vp, _vp, _vp], C.c_int),
+    "satrl_span_probe": ([_vp, _i64, _vp], C.c_int),
+    "satrl_span_probe_launches": ([], _i64),
+    "satrl_span_probe_launch": ([_i64, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_last_error": ([], C.c_char_p),
 }
 

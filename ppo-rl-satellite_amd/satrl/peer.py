@@ -103,22 +103,54 @@ class PeerComm:
                                                   stream_ptr()), "satrl_ppo_allreduce_peer")
         return G
 
-    def error(self) -> int:
-        """The sticky error word, after the work queued on the current stream."""
+    def error(self, stream=None) -> int:
+        """The sticky error word, after the work queued on `stream` (default:
+        the current stream, which the read drains)."""
         err = C.c_uint64()
-        check(_lib.lib().satrl_peer_error(self._own, C.byref(err), stream_ptr()), "satrl_peer_error")
+        check(_lib.lib().satrl_peer_error(self._own, C.byref(err), stream_ptr(stream)), "satrl_peer_error")
         return int(err.value)
+
+    def _raise(self):
+        raise PeerError("peer all-reduce: a peer's granule never arrived within "
+                        f"{self.timeout_s:g} s (a rank stalled or died); PeerComm.reset re-arms the buffers")
 
     def check(self):
         if self.error():
-            raise PeerError("peer all-reduce: a peer's granule never arrived within "
-                            f"{self.timeout_s:g} s (a rank stalled or died); PeerComm.reset re-arms the buffers")
+            self._raise()
+
+    def wait_event(self, ev, poll_s: float = 0.001):
+        """The watchdog between graph replays (FusedMinibatch.run): wait for
+        `ev` (recorded after a replay) by polling it against a host deadline,
+        then read the error word on a side stream that waits for nothing, so
+        the replays queued behind `ev` keep running (reading it on the compute
+        stream would drain them).  Every wait in the kernel is bounded by
+        timeout_s, and after one call fails the later ones return at once, so
+        a replay with a lost peer ends within about timeout_s: the host
+        deadline is twice that plus a margin."""
+        import time
+        t0, limit = time.monotonic(), 2.0 * self.timeout_s + 30.0
+        while not ev.query():
+            if time.monotonic() - t0 > limit:
+                raise PeerError(f"peer all-reduce: replay not complete after {limit:.0f} s (GPU stalled?)")
+            time.sleep(poll_s)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        if self.error(self._side):
+            self._raise()
+
+    _side = None
 
     def reset(self):
-        """Re-arm after a failure: every rank zeroes its own buffer (counters,
-        slots, error word), then all meet at a barrier (a collective call)."""
+        """Re-arm after a failure (a collective call): a barrier, so every rank
+        has stopped queueing calls; each rank drains its device, so none of
+        its kernels still pushes into a peer's slots; a second barrier, so no
+        buffer is zeroed while any rank's kernel may still write into it; then
+        every rank zeroes its own buffer (counters, slots, error word) and a
+        third barrier holds every rank until all buffers are re-armed."""
         import torch.distributed as dist
+        dist.barrier(group=self.pg)
         torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.pg)
         check(_lib.lib().satrl_peer_reset(self._own, self.nbytes, stream_ptr()), "satrl_peer_reset")
         dist.barrier(group=self.pg)
 

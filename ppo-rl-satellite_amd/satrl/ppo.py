@@ -299,13 +299,14 @@ class FusedMinibatch:
         mb = self.mb if mb is None else int(mb)
         check(_lib.lib().satrl_ppo_rowpass_kx(L.H, mb, int(net), ptr(src), None if idx is None else ptr(idx),
                                               ptr(L.P), ptr(L.W2T), float(L.epsilon), float(L.entropy_coef),
-                                              float(L.max_action), ptr(self.H1x), ptr(self.dZ2x), ptr(self.ptail),
-                                              ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass_kx")
+                                              float(L.max_action), ptr(self.H1x), ptr(self.dZ2x), self.H1x.numel(),
+                                              ptr(self.ptail), ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass_kx")
 
     def dw2_kx(self, mb, S, net=-1):
         """satrl_ppo_dw2_kx: the dW2 split-K slabs from the k-packed planes."""
         check(_lib.lib().satrl_ppo_dw2_kx(self.L.H, int(mb), int(net), int(S), ptr(self.H1x), ptr(self.dZ2x),
-                                          ptr(self.p2), stream_ptr()), "satrl_ppo_dw2_kx")
+                                          self.H1x.numel(), ptr(self.p2), self.p2.numel(), stream_ptr()),
+              "satrl_ppo_dw2_kx")
 
     def rowpass_dw2(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass_dw2 (H = 64): the rowpass with each block's dW2
@@ -314,8 +315,8 @@ class FusedMinibatch:
         mb = self.mb if mb is None else int(mb)
         check(_lib.lib().satrl_ppo_rowpass_dw2(L.H, mb, int(net), ptr(src), None if idx is None else ptr(idx),
                                                ptr(L.P), ptr(L.W2T), float(L.epsilon), float(L.entropy_coef),
-                                               float(L.max_action), ptr(self.p2), ptr(self.ptail), ptr(self.pw1),
-                                               stream_ptr()), "satrl_ppo_rowpass_dw2")
+                                               float(L.max_action), ptr(self.p2), self.p2.numel(), ptr(self.ptail),
+                                               ptr(self.pw1), stream_ptr()), "satrl_ppo_rowpass_dw2")
 
     def rowpass_ratio(self, src, idx, ratio, mb=None, net=-1):
         """satrl_ppo_rowpass_ratio: satrl_ppo_rowpass that also writes the
@@ -376,8 +377,8 @@ class FusedMinibatch:
 
     def _dw2(self, H1, dZ2, mb, S, net):
         """dW2 = dZ2^T @ H1 split-K S ways into the slabs p2 [2][S][H][H] (f32 rows)."""
-        check(_lib.lib().satrl_ppo_dw2(self.L.H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), stream_ptr()),
-              "satrl_ppo_dw2")
+        check(_lib.lib().satrl_ppo_dw2(self.L.H, mb, net, S, ptr(H1), ptr(dZ2), ptr(self.p2), self.p2.numel(),
+                                       stream_ptr()), "satrl_ppo_dw2")
 
     def _net_step(self, src, idx, mb, net, events=None, skip_rowpass=False):
         """One minibatch step of one chain.  Bench-only knobs: `events` (a pair
@@ -411,15 +412,15 @@ class FusedMinibatch:
                 self.dw2_kx(mb, S, net)
             elif not self.fused_dw2:
                 self._dw2(H1, dZ2, mb, S, net)
-            check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
-                                       ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), self.p2.numel(), ptr(self.pw1),
+                                       ptr(self.ptail), ptr(L.G), ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
             if kx:
                 self.dw2_kx(mb, S, net)
             elif not self.fused_dw2:
                 self._dw2(H1, dZ2, mb, S, net)
-            check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), ptr(self.pw1), ptr(self.ptail), ptr(L.G),
-                                       None, None, sp), "satrl_ppo_reduce")
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), self.p2.numel(), ptr(self.pw1),
+                                       ptr(self.ptail), ptr(L.G), None, None, sp), "satrl_ppo_reduce")
             # one bucket, both nets: SUM over the ranks, then G /= world and the norms in one launch
             if L.peer is not None and net < 0:
                 L.peer.all_reduce_dp_(H, mb, L.G, nsq, L.steps)              # peer kernel, reduce_dp fused
@@ -514,8 +515,10 @@ class FusedMinibatch:
                     # watchdog between replays: at most two replays queued ahead
                     # of the host.  RCCL: the oldest is waited for with the
                     # deadline while ncclCommGetAsyncError is polled
-                    # (rccl.Comm.wait_event); peer: once it has finished, the
-                    # error word is read, so a lost rank stops the update there
+                    # (rccl.Comm.wait_event); peer: the oldest is polled against
+                    # a host deadline, then the error word is read on a side
+                    # stream (the queued replays keep running), so a lost rank
+                    # stops the update there
                     ev = torch.cuda.Event()
                     ev.record()
                     inflight.append(ev)
@@ -523,8 +526,7 @@ class FusedMinibatch:
                         if comm is not None:
                             comm.wait_event(inflight.pop(0), _dist.dp_timeout_s())
                         else:
-                            inflight.pop(0).synchronize()
-                            peer.check()
+                            peer.wait_event(inflight.pop(0))
             k = (nfull // G) * G
         while k < nfull:                      # the rest of the full minibatches, eagerly
             ng = min(G, nfull - k)

@@ -84,10 +84,11 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_rowpass(256, 0, -1, *args) == -1                      # empty minibatch
     assert lib.satrl_ppo_rowpass(256, 64, 2, *args) == -1                      # net not -1/0/1
     assert lib.satrl_ppo_rowpass(256, 64, -1, None, *args[1:]) == -1           # null rows
-    assert lib.satrl_ppo_dw2(256, 4096, -1, 0, fake, fake, fake, None) == -1   # S < 1
-    assert lib.satrl_ppo_dw2(256, 64, -1, 64, fake, fake, fake, None) == -1    # an empty split
-    assert lib.satrl_ppo_reduce(256, 64, -1, 1, 4, fake, fake, fake, fake, fake, fake, None) == -1   # mode
-    assert lib.satrl_ppo_reduce(256, 64, -1, 1, 2, fake, fake, fake, fake, None, None, None) == -1   # no nsq
+    big = 1 << 40                                # a p2 / plane capacity no call exceeds
+    assert lib.satrl_ppo_dw2(256, 4096, -1, 0, fake, fake, fake, big, None) == -1   # S < 1
+    assert lib.satrl_ppo_dw2(256, 64, -1, 64, fake, fake, fake, big, None) == -1    # an empty split
+    assert lib.satrl_ppo_reduce(256, 64, -1, 1, 4, fake, big, fake, fake, fake, fake, fake, None) == -1   # mode
+    assert lib.satrl_ppo_reduce(256, 64, -1, 1, 2, fake, big, fake, fake, fake, None, None, None) == -1   # no nsq
     assert lib.satrl_gae(0, 4, fake, fake, fake, 0.99, 0.95, fake, fake, None) == -1
     assert lib.satrl_gae(4, 4, fake, None, fake, 0.99, 0.95, fake, fake, None) == -1
     assert lib.satrl_policy_act(256, 8, fake, fake, fake, 1.6, 0, 0, 0, None, fake, fake, None, None,
@@ -100,12 +101,13 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_w2x_sync(100, -1, fake, fake, None) == -1 and lib.satrl_ppo_w2x_sync(256, -1, None, fake, None) == -1
     assert lib.satrl_ppo_kx_elems(256, 4096) == 2 * 3 * 4096 * 256 and lib.satrl_ppo_kx_elems(256, 1500) == 6 * 1504 * 256
     assert lib.satrl_ppo_kx_elems(64, 4096) == -1
-    assert lib.satrl_ppo_rowpass_kx(256, 512, -1, None, *args[1:]) == -1        # null rows (16-row kernel's minibatch)
-    assert lib.satrl_ppo_rowpass_kx(64, 4096, -1, *args) == -1                  # H 256 only
+    kx_args = args[:9] + [big] + args[9:]        # (H1x, dZ2x, kx_elems, ptail, pw1, stream)
+    assert lib.satrl_ppo_rowpass_kx(256, 512, -1, None, *kx_args[1:]) == -1     # null rows (16-row kernel's minibatch)
+    assert lib.satrl_ppo_rowpass_kx(64, 4096, -1, *kx_args) == -1               # H 256 only
     assert lib.satrl_ppo_dw2_kx_splits(256, 4096, -1) == 8 and lib.satrl_ppo_dw2_kx_splits(256, 4096, 0) == 16
-    assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, fake, None) == -1     # S < 1
-    assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, fake, None) == -1       # an empty split (2 chunks)
-    assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, fake, None) == -1     # null H1x
+    assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, big, fake, big, None) == -1     # S < 1
+    assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, big, fake, big, None) == -1       # an empty split (2 chunks)
+    assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, big, fake, big, None) == -1     # null H1x
     # the peer all-reduce: grid, deadline, buffers
     bufs = (C.c_void_p * 2)(16, 16)
     pa = [C.cast(bufs, C.c_void_p), fake, fake, fake]
@@ -117,6 +119,39 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_peer_blocks(100, C.byref(C.c_int())) == -1 and lib.satrl_peer_blocks(256, None) == -1
     assert lib.satrl_peer_error(None, C.byref(C.c_uint64()), None) == -1
     assert lib.satrl_peer_reset(fake, 8, None) == -1                                         # smaller than the header
+
+
+def test_capi_refuses_calls_past_the_callers_buffers():
+    """Round-5 fault (a dW2 run with more splits than its slabs were sized
+    for wrote past p2): every call that writes or reads the dW2 slabs or the
+    k-packed planes takes the caller's capacity and refuses with -1 before
+    any launch (fake pointers, never touched; a launch would fail with -2 on
+    this GPU-less host instead)."""
+    import ctypes as C
+    import satrl._lib as L
+    lib = L.lib()
+    fake = C.c_void_p(16)
+    H, mb = 256, 4096
+    S = lib.satrl_ppo_dw2_kx_splits(H, mb, -1)                    # 8
+    kx = lib.satrl_ppo_kx_elems(H, mb)
+    p2_8 = 2 * 8 * H * H                                         # slabs sized for 8 splits
+    # an oversize split count (the round-5 case: 16 splits into slabs for 8)
+    assert lib.satrl_ppo_dw2_kx(H, mb, -1, 16, fake, fake, kx, fake, p2_8, None) == -1
+    assert b"p2 holds" in lib.satrl_ppo_last_error()
+    assert lib.satrl_ppo_reduce(H, mb, -1, 16, 3, fake, p2_8, fake, fake, fake, fake, fake, None) == -1
+    assert b"p2 holds" in lib.satrl_ppo_last_error()
+    assert lib.satrl_ppo_dw2(H, mb, -1, 16, fake, fake, fake, p2_8, None) == -1
+    # one net: the actor passes half, the critic (second half) the whole buffer
+    assert lib.satrl_ppo_dw2_kx(H, mb, 1, S, fake, fake, kx, fake, p2_8 // 2, None) == -1
+    # undersized planes, for the rowpass that writes them and the dW2 that reads them
+    assert lib.satrl_ppo_rowpass_kx(H, mb, -1, fake, None, fake, fake, 0.1, 0.01, 1.6, fake, fake, kx - 1, fake,
+                                    fake, None) == -1
+    assert b"planes hold" in lib.satrl_ppo_last_error()
+    assert lib.satrl_ppo_dw2_kx(H, mb, -1, S, fake, fake, kx - 1, fake, p2_8, None) == -1
+    # H 64: one slab per 32-row block (128 at mb 4096) written by the fused rowpass
+    assert lib.satrl_ppo_rowpass_dw2(64, mb, -1, fake, None, fake, fake, 0.1, 0.01, 1.6, fake, 2 * 127 * 64 * 64,
+                                     fake, fake, None) == -1
+    assert b"p2 holds" in lib.satrl_ppo_last_error()
 
 
 def test_product_has_no_cpu_fallback():

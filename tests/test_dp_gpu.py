@@ -379,6 +379,23 @@ def _peer_rank(rank, port, q):
         torch.cuda.synchronize()
         out["reset"] = (torch.equal(Gp, Gg), torch.equal(nsq_p, nsq_g), torch.equal(steps_p, steps_g),
                         Lp.peer.error() == 0)
+        # (1c) a rank that arrives LATE (after the other's deadline) rather than
+        # never: the early rank's waits run out, it pushes no sum with a missing
+        # term and flags every rank's buffer, so the late rank's call fails at
+        # once (its own deadline is 30 s) instead of completing on partial sums
+        import time
+        Lp.peer.timeout_s = 2.0 if rank == 0 else 30.0
+        dist.barrier()
+        if rank == 1:
+            time.sleep(5.0)
+        t0 = time.monotonic()
+        Gp.copy_(G0)
+        Lp.peer.all_reduce_dp_(256, 512, Gp, nsq_p, steps_p)
+        torch.cuda.synchronize()
+        out["late"] = (time.monotonic() - t0, Lp.peer.error() != 0)
+        Lp.peer.timeout_s = 30.0
+        Lp.peer.reset()
+        assert Lp.peer.error() == 0
         # (2) DP updates, H 64: peer path (graph-replayed and eager) vs the gloo path
         res = {}
         for mode, graph in (("peer", True), ("peer", False), ("rccl", False)):
@@ -416,7 +433,9 @@ def test_peer_allreduce_world2_one_device():
     device): bitwise c10d's SUM / world and reduce_dp's norms and step
     counters on a raw gradient over three calls, bitwise identical on both
     ranks; a call one rank skips times out into the error word, and after
-    PeerComm.reset the next call is bitwise right again; whole DP updates (2 epochs of 5 minibatches + a ragged tail,
+    PeerComm.reset the next call is bitwise right again; a rank that arrives
+    after the other's deadline fails fast on the error word the other set in
+    its buffer; whole DP updates (2 epochs of 5 minibatches + a ragged tail,
     graph-replayed and eager) bitwise equal to the gloo-all-reduce path."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -446,7 +465,9 @@ def test_peer_allreduce_world2_one_device():
         eqG, eqN, eqS, _ = res[r]["raw"]
         assert eqG and eqN and eqS, (r, eqG, eqN, eqS)
         assert all(res[r]["reset"]), (r, res[r]["reset"])
+        assert res[r]["late"][1], (r, "late peer: the failed call was not flagged on this rank")
         assert all(res[r]["update"][0]), (r, res[r]["update"][0])
+    assert res[1]["late"][0] < 10.0, res[1]["late"]        # the late rank failed fast, not after its 30 s
     import numpy as np
     assert np.array_equal(res[0]["raw"][3], res[1]["raw"][3])
     assert np.array_equal(res[0]["update"][1], res[1]["update"][1])

@@ -545,8 +545,8 @@ def test_dw2_kernel_vs_torch(H, mb):
     S = _lib.lib().satrl_ppo_dw2_splits(H, mb)
     assert S >= 1
     p2 = torch.full((2 * S * H * H,), float("nan"), device="cuda")
-    _lib.check(_lib.lib().satrl_ppo_dw2(H, mb, -1, S, _lib.ptr(H1), _lib.ptr(dZ2), _lib.ptr(p2), _lib.stream_ptr()),
-               "satrl_ppo_dw2")
+    _lib.check(_lib.lib().satrl_ppo_dw2(H, mb, -1, S, _lib.ptr(H1), _lib.ptr(dZ2), _lib.ptr(p2), p2.numel(),
+                                        _lib.stream_ptr()), "satrl_ppo_dw2")
     got = p2.view(2, S, H, H).double().sum(1)
     ref = torch.bmm(dZ2.view(2, mb, H).double().transpose(1, 2), H1.view(2, mb, H).double())
     err = (got - ref).abs().max().item()
@@ -586,11 +586,13 @@ def test_fused_dw2_rowpass_bitwise_equals_separate(mb, contig):
             st.rowpass_dw2(src, idx)
         else:
             H1, dZ2 = st.rowpass(src, idx)
-            _L.check(lib.satrl_ppo_dw2(64, mb, -1, S, _L.ptr(H1), _L.ptr(dZ2), _L.ptr(st.p2), sp), "satrl_ppo_dw2")
+            _L.check(lib.satrl_ppo_dw2(64, mb, -1, S, _L.ptr(H1), _L.ptr(dZ2), _L.ptr(st.p2), st.p2.numel(), sp),
+                     "satrl_ppo_dw2")
         G = torch.full_like(L.G, float("nan"))
         nsq = torch.zeros_like(st.nsq[0])
-        _L.check(lib.satrl_ppo_reduce(64, mb, -1, S, 3, _L.ptr(st.p2), _L.ptr(st.pw1), _L.ptr(st.ptail), _L.ptr(G),
-                                      _L.ptr(nsq), _L.ptr(L.steps), sp), "satrl_ppo_reduce")
+        _L.check(lib.satrl_ppo_reduce(64, mb, -1, S, 3, _L.ptr(st.p2), st.p2.numel(), _L.ptr(st.pw1),
+                                      _L.ptr(st.ptail), _L.ptr(G), _L.ptr(nsq), _L.ptr(L.steps), sp),
+                 "satrl_ppo_reduce")
         torch.cuda.synchronize()
         outs.append([st.p2[:2 * S * 64 * 64].clone(), st.ptail[:S * (6 * 64 + 12)].clone(),
                      st.pw1[:S * 2 * 64 * 20].clone(), G, nsq])

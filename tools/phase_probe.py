@@ -114,7 +114,7 @@ nsq = st.nsq[0]
 res = {
     "rowpass": t(lambda: st.rowpass_kx(src, None) if st.kx(mb) else st.rowpass(src, None)),
     "dw2": t(lambda: st.dw2_kx(mb, S) if st.kx(mb) else st._dw2(H1, dZ2, mb, S, -1)),
-    "reduce": t(lambda: lib.satrl_ppo_reduce(H, mb, -1, S, 3, _L.ptr(st.p2), _L.ptr(st.pw1), _L.ptr(st.ptail),
+    "reduce": t(lambda: lib.satrl_ppo_reduce(H, mb, -1, S, 3, _L.ptr(st.p2), st.p2.numel(), _L.ptr(st.pw1), _L.ptr(st.ptail),
                                              _L.ptr(L.G), _L.ptr(nsq), _L.ptr(L.steps), sp)),
     "adam": t(lambda: lib.satrl_ppo_adam(H, mb, -1, _L.ptr(nsq), _L.ptr(L.steps), _L.ptr(L.bct), L.bct.shape[0],
                                          _L.ptr(L.lr), 0.9, 0.999, 1e-5, 0.5, 1, _L.ptr(L.G), _L.ptr(L.P),

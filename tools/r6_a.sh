@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU box (round 6, first pass): the whole -m gpu suite on the round's first
+# changes (C-ABI capacities, peer fail-fast, live span probe), then the
+# default bench and the configs[1] bench (live spans + rocprof cross-checks
+# from the committed r5 profiles).
+set -euo pipefail
+ROOT=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$ROOT"
+mkdir -p gpurun_out
+( while true; do date >> gpurun_out/heartbeat.log; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null || true' EXIT
+rc=0
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+    > gpurun_out/r6a_gpu_tests.log 2>&1 || rc=$?
+echo "gpu tests rc=$rc" | tee gpurun_out/r6a_gpu_tests.rc
+[ "$rc" -ge 124 ] && exit "$rc"
+timeout -k 10 400 python3 bench.py --profile-tag r5 > gpurun_out/r6a_bench.json 2> gpurun_out/r6a_bench.err
+timeout -k 10 300 python3 bench.py --num-envs 4096 --hidden 64 --no-cpu-baseline --profile-tag r5 \
+    > gpurun_out/r6a_bench_configs1.json 2> gpurun_out/r6a_bench_configs1.err
+tail -c 300 gpurun_out/r6a_bench.json
