@@ -478,7 +478,6 @@ def run(a, world):
     rowpass_ev_us, rowpass_med = timed_pairs(a.kernel_iters, lambda k, ev: st.step(stage, None, events=ev), 60.0)
     rowpass_flop = st.step_kernel_flops(mb_local)        # + the fused dW2 product at H = 64
     rowpass_tfs = rowpass_flop / (rowpass_us * 1e-6) / 1e12
-    t_roll_sp = [0]
     # warm-L2 figure: back-to-back rowpass launches alone (W2/W2T stay in L2)
     rp_launch = st.rowpass_dw2 if st.fused_dw2 else (st.rowpass_kx if st.kx(mb_local) else st.rowpass)
     for _ in range(10):
@@ -540,17 +539,22 @@ def run(a, world):
         stp.run(src, perm_sp)                    # capture (each node keeps its record region), then two replays
         torch.cuda.synchronize()
     upd_spans = probe.summary()
+    upd_gaps = probe.gaps(["rowpass", "dw2", "reduce", "adam"])
     del stp
-    with SpanProbe() as probe:
-        tr._policy_step(0)                       # (untimed: first launches)
-        torch.cuda.synchronize()
-    with SpanProbe() as probe:
-        backlog(40.0)
-        for _ in range(a.kernel_iters):
-            tr._policy_step(t_roll_sp[0] % a.horizon)
-            t_roll_sp[0] += 1
+    # the rollout: one whole training rollout (T steps, both agents' policy kernel
+    # and the env step per step) through freshly captured chunk graphs, so every
+    # env-step launch of the rollout has its span (the trainer's graphs are kept
+    # aside and put back afterwards)
+    saved_graphs = tr._graphs
+    tr._graphs = {}
+    with SpanProbe(int(2.2 * a.horizon * (2 * a.num_envs // 32 * 8 + a.num_envs // 64 * 4) * 16) + (64 << 20)) as probe:
+        e0.record()
+        tr.collect()
+        e1.record()
         torch.cuda.synchronize()
     roll_spans = probe.summary()
+    roll_span_run_ms = e0.elapsed_time(e1)
+    tr._graphs = saved_graphs
     rowpass_live_us = upd_spans.get("rowpass", {}).get("avg_us")
     head_us = rowpass_live_us if rowpass_live_us else rowpass_us
     traffic = pmc("rowpass", hidden=a.hidden, minibatch=mb_local)
@@ -570,8 +574,8 @@ def run(a, world):
                        "bound": "mfma", "achieved": pol_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                        "frac": pol_tfs / FP32_MFMA_PEAK_TFS, "avg_launch_us": pol_us, "flop_per_launch": pol_flop,
                        "timing": ("live launch span in this run (satrl_span_probe: max wave exit - min wave start, "
-                                  "s_memrealtime) averaged over kernel_iters eager rollout steps queued behind a GPU "
-                                  "spin" if roll_spans.get("policy_act") else "rocprofv3 average (committed profile)"),
+                                  "s_memrealtime) averaged over every launch of one whole training rollout"
+                                  if roll_spans.get("policy_act") else "rocprofv3 average (committed profile)"),
                        "rocprof_avg_launch_us": pol_prof_us,
                        "rocprof_source": (f"profiles/{os.path.basename(ks_file)} (committed profile of this command)"
                                           if ks_file else None)}
@@ -924,6 +928,10 @@ def run(a, world):
                                     "live marginal cost (the span probe gave no rowpass launches)"),
                          "live_span_avg_launch_us": rowpass_live_us,
                          "update_kernel_spans": upd_spans,
+                         "update_boundary_gaps": upd_gaps,
+                         "update_boundary_gaps_timing": ("next launch's first wave start minus the previous launch's "
+                                                         "last wave exit (span clock), one replay of the update's "
+                                                         "64-minibatch graph"),
                          "live_marginal_avg_launch_us": rowpass_us,
                          "live_marginal_frac": rowpass_tfs / FP32_MFMA_PEAK_TFS,
                          "live_marginal_timing": "HIP events on the launch stream: kernel_iters minibatch steps "
@@ -952,9 +960,11 @@ def run(a, world):
                              "avg_launch_us": env_head_us, "bytes_per_env_step": ENV_BYTES_PER_STEP,
                              "num_envs": a.num_envs,
                              "timing": ("live in-rollout kernel duration measured in this run: the launch span "
-                                        "(satrl_span_probe) averaged over kernel_iters eager rollout steps of the "
-                                        "trainer's envs queued behind a GPU spin; the committed rocprof average "
-                                        "beside it" if env_span_us else "live marginal cost (no span)"),
+                                        "(satrl_span_probe) averaged over every env-step launch of one whole "
+                                        "training rollout (T steps through freshly captured chunk graphs, after the "
+                                        "timed region); the committed rocprof average beside it"
+                                        if env_span_us else "live marginal cost (no span)"),
+                             "span_rollout_ms": roll_span_run_ms,
                              "live_span_avg_launch_us": env_span_us,
                              "rollout_kernel_spans": roll_spans,
                              "check": roll_check,

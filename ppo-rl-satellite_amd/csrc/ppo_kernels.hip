@@ -494,6 +494,58 @@ __device__ __forceinline__ void store_kx(unsigned short* __restrict__ img, int64
              make_float4(v[rt][t][0], v[rt][t][1], v[rt][t][2], v[rt][t][3]));
     }
 }
+// one 8-B store of the k-packed planes; WT: agent-scope write-through
+// (global_store_dwordx2 sc0 sc1), so the planes leave L2 during the kernel
+// instead of in the release at its end, which the next launch's start waits
+// for.  The 16-row (short-minibatch) rowpass writes through: in-graph step at
+// mb 512 33.1-33.2 against 34.1 us with plain stores (three alternations on
+// two boxes, tools/ab_spans.sh); at mb 4096 the 32-row kernel gets as much
+// longer as the boundary gets shorter (rowpass span +2-3 us, step equal), so
+// it stores plainly (EXPERIMENTS.md round 6)
+template <bool WT>
+__device__ __forceinline__ void st_kx(unsigned short* p, uint2 v) {
+  if constexpr (WT)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), ((unsigned long long)v.y << 32) | v.x,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *reinterpret_cast<uint2*>(p) = v;
+}
+
+// store_kx from values already split (split3x2 of rows j, j+1 and j+2, j+3 of
+// each lane's four; w[rt][t] = {hi01, hi23, mid01, mid23, lo01, lo23}): the
+// same stores, no split VALU
+template <int H, int R, int CT, bool WT = false>
+__device__ __forceinline__ void store_kx_w(unsigned short* __restrict__ img, int64_t PL, int r0, int n0,
+                                           const unsigned (&w)[R / 16][CT][6]) {
+  const int l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+#pragma unroll
+  for (int rt = 0; rt < R / 16; ++rt)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int r = r0 + 16 * rt + 4 * lg, n = n0 + 16 * t + li;
+      const int64_t e = ((int64_t)(r >> 3) * H + n) * 8 + (r & 7);
+      st_kx<WT>(img + e, make_uint2(w[rt][t][0], w[rt][t][1]));
+      st_kx<WT>(img + PL + e, make_uint2(w[rt][t][2], w[rt][t][3]));
+      st_kx<WT>(img + 2 * PL + e, make_uint2(w[rt][t][4], w[rt][t][5]));
+    }
+}
+// four values of one column, rows e, e + LDP, e + 2 LDP, e + 3 LDP of an LDS
+// plane image (plane stride PS), split once as pairs (split3x2) into w: each
+// bf16 goes out by a 16-bit store of its half of the packed word
+// (ds_write_b16 / ds_write_b16_d16_hi), so the planes get the bits put3 gives
+// each value, with the split VALU of two pairs instead of four scalars
+template <int PS, int LDP>
+__device__ __forceinline__ void put3_col4(unsigned short* img, int e, const float (&v)[4], unsigned (&w)[6]) {
+  split3x2(f2v{v[0], v[1]}, w[0], w[2], w[4]);
+  split3x2(f2v{v[2], v[3]}, w[1], w[3], w[5]);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    img[p * PS + e] = (unsigned short)w[2 * p];
+    img[p * PS + e + LDP] = (unsigned short)(w[2 * p] >> 16);
+    img[p * PS + e + 2 * LDP] = (unsigned short)w[2 * p + 1];
+    img[p * PS + e + 3 * LDP] = (unsigned short)(w[2 * p + 1] >> 16);
+  }
+}
 // rows of a k-packed tensor: the minibatch padded to whole 32-row chunks
 __host__ __device__ constexpr int64_t kx_rows(int mb) { return (mb + 31) / 32 * 32LL; }
 // the three planes of x at element e of an LDS plane image (plane stride PS)
@@ -575,7 +627,8 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
                                             Gather gather, float* __restrict__ h1out,
                                             f4 (&acc)[R / 16][H / 16 / NW],
                                             float (&h1)[R / 16][H / 16 / NW][4],
-                                            float (&w3)[H / 16 / NW][3]) {
+                                            float (&w3)[H / 16 / NW][3],
+                                            unsigned (&h1w)[R / 16][H / 16 / NW][6]) {
   constexpr int RT = R / 16, LDA = H + 4, CT = H / 16 / NW, LDS_S = 36, NT = NW * 64;
   static_assert(CT >= 1 && H % (16 * NW) == 0, "tile split");
   const Layout L = layout(H);
@@ -646,9 +699,13 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         const int r = 16 * rt + 4 * lg + j;
         const float h = tanh_f32(acc[rt][t][j]);                   // fc1 + tanh
         h1[rt][t][j] = h;
-        if constexpr (kBf3<H>) put3<MlpSmem<H, NW, R>::PS>(sm.h1p, r * MlpSmem<H, NW, R>::LDP + n, h);
-        else sm.h1s[r][n] = h;
+        if constexpr (!kBf3<H>) sm.h1s[r][n] = h;
       }
+      // (split-bf16) the three planes of the lane's four rows, split once as
+      // pairs; the words stay in h1w for the k-packed H1 store (rowpass_kx)
+      if constexpr (kBf3<H>)
+        put3_col4<MlpSmem<H, NW, R>::PS, MlpSmem<H, NW, R>::LDP>(
+            sm.h1p, (16 * rt + 4 * lg) * MlpSmem<H, NW, R>::LDP + n, h1[rt][t], h1w[rt][t]);
       acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
   if (h1out != nullptr) store_rows<R, CT>(h1out, H, n0, nvalid, h1);   // straight-line unless ragged
@@ -788,6 +845,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
+  unsigned h1w[RT][CT][6];                                         // (split-bf16) the split H1 words
   auto gather = [&](int t0, int nt) {
     auto head_consts = [&] {
       // (opaque to the compiler and ordered after the row loads: otherwise it
@@ -842,12 +900,13 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   // mb 4096, 15.3 against 15.5 at 512; at H = 256 no gain, not set there)
   if constexpr (FDW2) __builtin_amdgcn_s_setprio(3);
   mlp_forward<H, NW, R, true, FDW2>(sm, P, net, mb - r0, gather,
-                                   FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3);
+                                   FDW2 || KX || BF3 ? nullptr : H1g + ((int64_t)net * mb + r0) * H, acc, h1, w3,
+                                   h1w);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   // (KX) the H1 planes: wave 0, which runs the loss head next, stores its
   // share after the head, off the head's path; the other waves now
   auto h1_kx = [&] {
-    store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1);
+    store_kx_w<H, R, CT, R == kRowsShort>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1w);
     if (R < 32 && r0 + R < kx_rows(mb) && r0 + R >= mb) {            // (uniform) the padded chunk's rows past this block
       const float z[R / 16][CT][4] = {};
       store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0 + R, n0, z);
@@ -945,6 +1004,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   PHASE_PROBE(4);
   float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
   float d2v[RT][CT][4];
+  unsigned d2w[RT][CT][6];                                         // (split-bf16) the split dZ2 words
   // unswitched on the (workgroup-uniform) net: no per-element branches, and
   // the critic skips the actor's three output columns.  (Moving the db2 /
   // dW3 partial sums into phase D's MFMA gaps measured slower: D +2.6 k
@@ -959,7 +1019,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 #pragma unroll
       for (int q = 0; q < NC; ++q) cw[q] = 0.f;
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
+      for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 16 * rt + 4 * lg + j;
@@ -968,8 +1028,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
           if constexpr (ACT) dh = (dz3s[r][0] * w3[t][0] + dz3s[r][1] * w3[t][1]) + dz3s[r][2] * w3[t][2];
           else dh = dz3s[r][3] * w3[t][0];
           const float d2 = dh * (1.0f - h * h);                     // tanh backward
-          if constexpr (BF3) put3<PS>(dzp, r * LDP + n, d2);
-          else dzs[r][n] = d2;
+          if constexpr (!BF3) dzs[r][n] = d2;
           d2v[rt][t][j] = d2;
           cb2 += d2;
           if constexpr (ACT) {
@@ -978,6 +1037,10 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
             cw[0] = fmaf(dz3s[r][3], h, cw[0]);
           }
         }
+        // (split-bf16) dZ2's LDS planes (phase D's A operand), split once as
+        // pairs; the words stay in d2w for the k-packed dZ2 store
+        if constexpr (BF3) put3_col4<PS, LDP>(dzp, (16 * rt + 4 * lg) * LDP + n, d2v[rt][t], d2w[rt][t]);
+      }
       cb2 = xor32_sum(xor16_sum(cb2));
 #pragma unroll
       for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
@@ -993,7 +1056,8 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   };
   if (net == 0) tail(std::true_type{});
   else tail(std::false_type{});
-  if constexpr (KX) store_kx<H, R, CT>(reinterpret_cast<unsigned short*>(dZ2g) + net * 3 * PLX, PLX, r0, n0, d2v);
+  if constexpr (KX)
+    store_kx_w<H, R, CT, R == kRowsShort>(reinterpret_cast<unsigned short*>(dZ2g) + net * 3 * PLX, PLX, r0, n0, d2w);
   else if constexpr (!FDW2) store_rows<R, CT>(dZ2g + ((int64_t)net * mb + r0) * H, H, n0, mb - r0, d2v);
   rp_barrier();
   PHASE_PROBE(5);
@@ -1063,7 +1127,9 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 #pragma unroll
       for (int j = 0; j < MT; ++j)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) out[(int64_t)(n0 + 16 * t + 4 * lg + q) * H + 16 * j + li] = a2[j][q];
+        for (int q = 0; q < 4; ++q) {
+          out[(int64_t)(n0 + 16 * t + 4 * lg + q) * H + 16 * j + li] = a2[j][q];
+        }
     }
   }
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
@@ -1133,7 +1199,8 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   f4 acc[RT][CT];
   float h1[RT][CT][4];
   float w3[CT][3];
-  mlp_forward<H, NW, R, false, true>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3);
+  unsigned h1w[RT][CT][6];
+  mlp_forward<H, NW, R, false, true>(sm, P, MODE == 0 ? 0 : 1, nvalid, gather, nullptr, acc, h1, w3, h1w);
   const int r = threadIdx.x;
   if (r >= nvalid) {                                             // no barrier follows
     if constexpr (SPAN) satrl_span::exit(span, span_t0);
@@ -1322,8 +1389,9 @@ __device__ __forceinline__ void dw2_kx_body(int b, int mb, int S, int KR, int ne
 #pragma unroll
     for (int y = 0; y < XN; ++y)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < 4; ++q) {
         out[(int64_t)(o0 + (TW / 2) * wo + 16 * x + 4 * lg + q) * H + n0 + (TW / 2) * wn + 16 * y + li] = acc[x][y][q];
+      }
 }
 template <int TW, bool SPAN = false>
 __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int net_sel,

@@ -19,7 +19,7 @@ import torch  # noqa: F401  (must be loaded before libsatrl.so, see module doc)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
-LIB_PATH = os.path.join(PKG_DIR, "libsatrl.so")
+LIB_PATH = _PRODUCT_LIB = os.path.join(PKG_DIR, "libsatrl.so")
 # development A/B builds only (tools/_probe variants); the shipped path is LIB_PATH
 LIB_PATH = os.environ.get("SATRL_LIB_PATH", LIB_PATH)
 
@@ -165,6 +165,8 @@ def lib():
         except OSError as e:
             raise NativeError(f"cannot load {LIB_PATH}: {e}") from e
         for name, (argt, rest) in _SIGS.items():
+            if LIB_PATH != _PRODUCT_LIB and not hasattr(L, name):
+                continue                     # (an older development build: A/B only)
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest

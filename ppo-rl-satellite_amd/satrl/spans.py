@@ -53,6 +53,35 @@ class SpanProbe:
             out.append((KINDS.get(kind.value, str(kind.value)), span, int(ok.sum()), int(waves.value)))
         return out
 
+    def raw(self):
+        """[(kind name, first wave start, last wave exit)] in s_memrealtime ticks, launch order."""
+        torch.cuda.synchronize()
+        lib = _lib.lib()
+        rec = self.buf.cpu().numpy().view(np.uint64)
+        out = []
+        kind, off, waves = C.c_int(), C.c_int64(), C.c_int64()
+        for i in range(int(lib.satrl_span_probe_launches())):
+            check(lib.satrl_span_probe_launch(i, C.byref(kind), C.byref(off), C.byref(waves)),
+                  "satrl_span_probe_launch")
+            r = rec[off.value:off.value + 2 * waves.value].reshape(-1, 2)
+            ok = r[:, 1] != 0
+            out.append((KINDS.get(kind.value, str(kind.value)), int(r[ok, 0].min()) if ok.any() else 0,
+                        int(r[ok, 1].max()) if ok.any() else 0))
+        return out
+
+    def gaps(self, chain):
+        """Mean idle time (us) between consecutive launches of a repeating kernel
+        chain (e.g. ["rowpass", "dw2", "reduce", "adam"]): for each boundary
+        "a->b", the next launch's first wave start minus the previous launch's
+        last wave exit, over the log's launches in order (one graph replay's
+        records); the span clock is one counter for the whole chip."""
+        seq = [x for x in self.raw() if x[0] in chain and x[2] > 0]
+        out = {}
+        for (ka, _, ea), (kb, sb, _) in zip(seq, seq[1:]):
+            out.setdefault(f"{ka}->{kb}", []).append((int(sb) - int(ea)) * TICK_US)
+        return {k: {"mean_us": float(np.mean(v)), "median_us": float(np.median(v)), "n": len(v)}
+                for k, v in out.items()}
+
     def summary(self):
         """{kind: {"launches", "avg_us", "median_us", "min_us", "max_us", "complete"}} over the log."""
         per = {}
