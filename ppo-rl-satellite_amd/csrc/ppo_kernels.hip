@@ -814,8 +814,22 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
   __shared__ float dz3s[R][4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
   // net_sel < 0: both nets, blockIdx = (row block, net); else that net only
-  const int net = net_sel < 0 ? (int)(blockIdx.x & 1) : net_sel;
-  const int rb = net_sel < 0 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, n0 = w * (H / NW);
+  // XCD-matched placement (32-row k-packed kernel, both nets, a row-block
+  // count divisible by 8): the row blocks of dW2 split s -- row blocks
+  // [s nrb/8, (s+1) nrb/8), both nets -- go to the workgroups b with
+  // b % 8 == s, i.e. under round-robin dispatch to the XCD that dw2_kx's
+  // split s runs on (its block b takes split b % 8), so the planes dw2_kx
+  // reads were written through that XCD's L2 (placement only: every bit is
+  // the same; in-graph step at mb 4096 47.5-47.8 against 48.7-49.2 us over
+  // three alternations, the rowpass->dw2 boundary 3.6-3.9 against 4.1-4.6
+  // us; at mb 512 the 16-row kernel measured 0.2-0.3 us slower with it, so
+  // it keeps the (row block, net) = (b / 2, b % 2) order; EXPERIMENTS.md
+  // round 6).  Otherwise the actor lands on the even XCDs, the critic on the odd.
+  const int nrbk = (mb + R - 1) / R;
+  const bool xmap = KX && R == kRows && net_sel < 0 && nrbk % 8 == 0;
+  const int bx = (int)blockIdx.x, kx8 = bx >> 3;
+  const int net = net_sel < 0 ? (xmap ? (kx8 & 1) : (bx & 1)) : net_sel;
+  const int rb = net_sel < 0 ? (xmap ? (bx & 7) * (nrbk >> 3) + (kx8 >> 1) : (bx >> 1)) : bx, n0 = w * (H / NW);
   const int r0 = rb * R;
   auto& S = sm.S;
 #ifdef SATRL_PHASE_PROBE

@@ -44,7 +44,7 @@ def step_and_spans(H, mb, n=20):
         for _ in range(3):
             sp.run(src, perm)
         torch.cuda.synchronize()
-    return step, pr.summary()
+    return step, pr.summary(), pr.gaps(["rowpass", "dw2", "reduce", "adam"])
 
 
 def rollout_spans(H, n_envs=16384, n=64):
@@ -75,9 +75,10 @@ if __name__ == "__main__":
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     for _ in range(reps):
         for mb in mbs:
-            step, s = step_and_spans(H, mb)
+            step, s, gp = step_and_spans(H, mb)
             ks = " ".join(f"{k} {v['median_us']:.2f}" for k, v in s.items())
-            print(f"[{tag}] H {H} mb {mb:5d}: step {step:6.2f} us | span medians: {ks}", flush=True)
+            gs = " ".join(f"{k} {v['median_us']:.2f}" for k, v in gp.items())
+            print(f"[{tag}] H {H} mb {mb:5d}: step {step:6.2f} us | span medians: {ks} | gaps: {gs}", flush=True)
     if len(sys.argv) > 4 and sys.argv[4] == "rollout":
         step, s = rollout_spans(H)
         ks = " ".join(f"{k} {v['median_us']:.2f}" for k, v in s.items())
