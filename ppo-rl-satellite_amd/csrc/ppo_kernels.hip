@@ -610,7 +610,13 @@ struct MlpSmem {
   float h1s[BF3 ? 0 : R][LDA] __attribute__((aligned(16)));                // tanh(fc1)
   unsigned short h1p[BF3 ? 3 * PS : 0] __attribute__((aligned(16)));      // (BF3) its three bf16 planes
   float S[R][LDS_S] __attribute__((aligned(16)));     // [s(18) | 1 | 0...] per row
-  float osum[H / 16][R][3];                           // per-column-tile output-layer partial sums
+  // per-column-tile output-layer partial sums, [row][output][tile] with the
+  // tiles of a (row, output) contiguous (16-B aligned runs, padded to 4k+4
+  // floats so the writers' rows 4 apart fall on different bank pairs): the
+  // loss head reads each sum's partials as ds_read_b128s instead of one
+  // ds_read per tile (the same partials, added in the same tile order)
+  static constexpr int OSP = H / 16 + (H == 64 ? 8 : 4);
+  float osum[R][3][OSP] __attribute__((aligned(16)));
 };
 
 // Rows r < nvalid of the block must be in S[r][0..17] when gather() returns;
@@ -770,7 +776,7 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            sm.osum[w * CT + t][16 * rt + 4 * lg + j][q] = ps[((q * CT + t) * RT + rt) * 4 + j];
+            sm.osum[16 * rt + 4 * lg + j][q][w * CT + t] = ps[((q * CT + t) * RT + rt) * 4 + j];
     }
   }
   rp_barrier();
@@ -779,11 +785,11 @@ __device__ __forceinline__ void mlp_forward(MlpSmem<H, NW, R>& sm, const float* 
 
 // output-layer pre-activation of row r, column d: the NTL column-tile
 // partials in fixed order
-template <int NTL, int R>
-__device__ __forceinline__ float out_sum(const float (*osum)[R][3], int r, int d) {
+template <int NTL, int OSP>
+__device__ __forceinline__ float out_sum(const float (*osum)[3][OSP], int r, int d) {
   float od = 0.0f;
 #pragma unroll
-  for (int k = 0; k < NTL; ++k) od += osum[k][r][d];
+  for (int k = 0; k < NTL; ++k) od += osum[r][d][k];
   return od;
 }
 
@@ -945,7 +951,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
         float th[3], mu[3], dv[3], var[3], logp[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          th[d] = tanh_f32(out_sum<H / 16, R>(sm.osum, r, d) + hb3s[d]);
+          th[d] = tanh_f32(out_sum<H / 16>(sm.osum, r, d) + hb3s[d]);
           mu[d] = max_action * th[d];                              // 1.6 * tanh(mean_layer)
           var[d] = hcs[0][d];
           dv[d] = ax[r][d] - mu[d];
@@ -975,7 +981,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
           dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
         }
       } else {                                                     // critic: MSE
-        const float vc = out_sum<H / 16, R>(sm.osum, r, 0) + hb3s[3];
+        const float vc = out_sum<H / 16>(sm.osum, r, 0) + hb3s[3];
         dz[3] = 2.0f * inv * (vc - ax[r][7]);                      // d mse / d v
       }
     }
@@ -1222,7 +1228,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   }
   const int64_t i = r0 + r;
   if (MODE == 1) {
-    value[i] = out_sum<H / 16, R>(sm.osum, r, 0) + P[L.b3c];
+    value[i] = out_sum<H / 16>(sm.osum, r, 0) + P[L.b3c];
     if constexpr (SPAN) satrl_span::exit(span, span_t0);
     return;
   }
@@ -1233,7 +1239,7 @@ __global__ void __launch_bounds__(NW * 64) policy_kernel(int64_t N, const float*
   float* logp = agent == 0 ? logp0 : logp1;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const float mu = max_action * tanh_f32(out_sum<H / 16, R>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
+    const float mu = max_action * tanh_f32(out_sum<H / 16>(sm.osum, r, d) + P[L.b3a + d]);   // 1.6 * tanh(mean_layer)
     gaussian_act(mu, P[L.ls + d], z[d], max_action, act[i * 3 + d], logp[i * 3 + d]);
   }
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
@@ -1329,7 +1335,7 @@ __global__ void __launch_bounds__(256) dw2_kernel(int mb, int S, int KR, int net
 // and raw s_barrier; the MFMA operands are ds_read_b128 of consecutive 16-B
 // (row groups 16 B apart in bank space).  Every sum has a fixed order.
 // ---------------------------------------------------------------------------
-constexpr int kKxD = 3;                         // ring slots (chunks kKxD - 1 ahead)
+constexpr int kKxD = 3;        // ring slots (chunks kKxD - 1 ahead; 4 and 5 measured no faster, round 6)
 // output tile width TW (64: 16 tiles per net, 8 splits of 512 rows at mb 4096;
 // 128: 4 tiles per net, half the plane bytes per workgroup, 32 splits)
 constexpr int kKxTW = 64;
@@ -1423,7 +1429,10 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 // split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split
-constexpr int kKxWgs = 256;
+#ifndef SATRL_KX_WGS
+#define SATRL_KX_WGS 256   // (A/B builds: -DSATRL_KX_WGS=n)
+#endif
+constexpr int kKxWgs = SATRL_KX_WGS;
 int kx_splits(int mb, int net, int target = kKxWgs) {
   const int tiles = (net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW), nch = (int)(kx_rows(mb) / 32);
   int S = target / tiles;
