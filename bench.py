@@ -67,7 +67,7 @@ def parse():
                     help="N > 1: the update's per-minibatch gradient all-reduce: RCCL (ncclAllReduce + reduce_dp in "
                          "the graphs) or the peer kernel (satrl_ppo_allreduce_peer: two-shot over IPC-mapped "
                          "buffers, fused with reduce_dp); the line times the other one beside it")
-    ap.add_argument("--profile-tag", default="r5", help="profiles/<tag>_* files the rocprof cross-check fields read")
+    ap.add_argument("--profile-tag", default="r6", help="profiles/<tag>_* files the rocprof cross-check fields read")
     ap.add_argument("--global-slice", type=int, default=256,
                     help="N > 1: minibatches of the configs[3]-semantics slice timed after the run (global "
                          "minibatch --minibatch, i.e. --minibatch/N rows per rank per Adam step); 0 = off")
