@@ -151,6 +151,18 @@ int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t
 int satrl_ppo_dw2_kx_splits(int H, int mb, int net);
 int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
                      int64_t p2_floats, void* stream);
+/* Up to 512 rows (configs[3]'s per-rank minibatch), both nets, when its
+ * grid is resident at once, satrl_ppo_rowpass_kx runs the column-split
+ * kernel: each (16-row block, net) on four workgroups of four waves, one per
+ * 64 hidden columns, which exchange the output-layer partials and the dZ2
+ * planes inside the launch (bitwise the 16-wave kernel's outputs).  Its
+ * exchange state is the library's own, per device: launches of it must not
+ * run concurrently on two streams of one device.  A wait that times out
+ * (0.5 s; a grid not co-resident) leaves the kernel with its outputs invalid
+ * and sets an error word: satrl_ppo_rowpass_error synchronises the stream,
+ * reports it in *err (1; 0 = none), and on an error re-arms the exchange
+ * state (the update that saw it must be discarded).                       */
+int satrl_ppo_rowpass_error(int* err, void* stream);
 
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result
  * is independent of N and of the sharding, and the rollout's log-probs equal

@@ -1156,6 +1156,429 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 }
 
 // ---------------------------------------------------------------------------
+// rowpass_cs: the short-minibatch H = 256 k-packed rowpass (16-row blocks)
+// with each (row block, net) split by hidden columns over kCsSplit workgroups
+// of kCsWaves waves: quarter j owns the 16-column tiles 4j .. 4j+3, its wave w
+// the tile 4j + w (columns 64j + 16w ..).  At configs[3]'s 512 rows per rank
+// rowpass_kernel<256, 16, 16> puts 64 workgroups of 16 waves on 256 CUs, four
+// waves per SIMD issuing phases B and D one after another; here 256
+// workgroups of 4 waves, one wave per SIMD.  Every value is computed by the
+// instructions of rowpass_kernel<256, 16, kRowsShort, false, true> in the same
+// order -- fc1 of all 16 tiles in every quarter (phase B's A operand is all of
+// H1), then the same per-tile fc2, output-layer, loss-head, tail, dH1 and dW1
+// sequences -- so every output is bitwise that kernel's.
+// Two hand-offs inside the launch between the kCsSplit workgroups of a group,
+// in the form of row 3 of MI355X_MICROARCH.md's sc1 hand-off table: __device__
+// arrays; payload stores sc1 (8 B, every 128-B line by 16 lanes of one store
+// instruction); every storing wave's vmcnt(0) wait and a workgroup barrier
+// before ONE agent-scope add per workgroup; a global_load_dword sc1 poll; a
+// workgroup barrier between the poll and every payload load
+// (buffer_load_dwordx4 sc1):
+//   X1  each quarter's output-layer tile partials (the loss head sums all 16
+//       tiles, in tile order, in every quarter);
+//   X2  each quarter's columns of the dZ2 bf16 planes (phase D's k runs over
+//       all 256).
+// A group's counter only grows, by kCsSplit at each hand-off, so a launch
+// finds it at 2 kCsSplit L (L = the group's launches so far) and the value
+// an add returns names the launch's targets.  A wait longer than
+// kCsTimeoutTicks (a group not co-resident: the launcher checks residency
+// first) sets g_cs_err and leaves the kernel, so the grid always drains;
+// satrl_ppo_rowpass_error reports it and re-arms the counters.
+// ---------------------------------------------------------------------------
+constexpr int kCsWaves = 4, kCsSplit = 256 / 16 / kCsWaves;   // waves per workgroup, workgroups per group
+constexpr int kCsMaxMb = 512;                                  // minibatches of up to this many rows
+constexpr int kCsMaxGroups = 2 * (kCsMaxMb / kRowsShort);      // (row block, net) groups
+constexpr unsigned long long kCsTimeoutTicks = 50000000ull;     // 0.5 s of s_memrealtime (100 MHz)
+__device__ __attribute__((aligned(128))) unsigned g_cs_ctr[kCsMaxGroups][32];   // a 128-B line per counter
+__device__ __attribute__((aligned(128))) unsigned g_cs_err[32];
+__device__ __attribute__((aligned(128))) float g_cs_x1[kCsMaxGroups][kCsSplit][kRowsShort][3][kCsWaves];
+__device__ __attribute__((aligned(128))) unsigned short g_cs_x2[kCsMaxGroups][3][kRowsShort][256];
+
+// one hand-off step (1: X1, 2: X2) of a group: true once every workgroup of
+// the group has published it, false (every thread) after a timeout
+__device__ __forceinline__ bool cs_handoff(unsigned* ctr, unsigned step, unsigned* ok_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // this wave's payload stores are out
+  __syncthreads();                                            // ... and every other wave's
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = old - old % (2u * kCsSplit) + step * kCsSplit;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned ok = 1;
+    while ((int)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kCsTimeoutTicks) {
+        __hip_atomic_store(&g_cs_err[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *ok_lds = ok;
+  }
+  __syncthreads();
+  return *ok_lds != 0;
+}
+// 16 B of a hand-off payload, from L2 (sc1: never a stale L1 line)
+__device__ __forceinline__ float4 cs_load16(const void* base, int bytes, int off) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+}
+__device__ __forceinline__ void cs_store8(void* p, unsigned long long v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool SPAN = false>
+__global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
+    int mb, const float* __restrict__ src, const int64_t* __restrict__ idx, const float* __restrict__ P,
+    const float* __restrict__ W2T, float epsilon, float ent_coef, float max_action,
+    unsigned short* __restrict__ H1x, unsigned short* __restrict__ dZ2x, float* __restrict__ ptail,
+    float* __restrict__ pw1, float* __restrict__ ratio_out, float inv_mb, unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;
+  constexpr int H = 256, R = kRowsShort, NT = kCsWaves * 64, LDS_S = 36;
+  constexpr int LDP = MlpSmem<H, 16, R>::LDP, PS = MlpSmem<H, 16, R>::PS, OSP = MlpSmem<H, 16, R>::OSP;
+  struct Smem {
+    unsigned short h1p[3 * PS];                  // tanh(fc1), all 256 columns, three bf16 planes
+    unsigned short dzp[3 * PS];                  // dZ2 planes (this quarter's columns, then all)
+    float S[R][LDS_S];
+    float osum[R][3][OSP];                       // every tile's output-layer partials (after X1)
+    float xs[R][3][kCsWaves];                    // this quarter's (X1 staging)
+    float ax[R][8];
+    float dz3s[R][4];
+    float hcs[3][3];
+    float hb3s[4];
+    unsigned ok;
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  // group g = (row block, net), quarter j: blocks b, b + 8, b + 16, b + 24 of
+  // each 32 form a group (one XCD under round-robin dealing: placement only)
+  const int nrbk = (mb + R - 1) / R, ngrp = 2 * nrbk;
+  const int bx = (int)blockIdx.x, j = (bx >> 3) & (kCsSplit - 1), grp = (bx & 7) | ((bx >> 5) << 3);
+  if (grp >= ngrp) {                                               // (whole groups of the last window)
+    if constexpr (SPAN) satrl_span::exit(span, span_t0);
+    return;
+  }
+  const int net = grp & 1, rb = grp >> 1, r0 = rb * R;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, li = l & 15, lg = l >> 4;
+  const int n0 = 64 * j + 16 * w;                                  // this wave's tile: 4j + w
+  const int64_t PLX = kx_rows(mb) * H;
+  const Layout L = layout(H);
+  unsigned* ctr = &g_cs_ctr[grp][0];
+
+  // head scalars: lanes 0-3 of the last wave (no row load of its own)
+  const int hd = tid - (NT - 64);
+  float hls_d = 0.0f, hb3_d = 0.0f;
+  if (hd >= 0 && hd < 4) {
+    hb3_d = P[hd < 3 ? L.b3a + hd : L.b3c];
+    hls_d = P[L.ls + (hd < 3 ? hd : 0)];
+  }
+  // fc1 weights of the wave's four fc1 tiles w, w + 4, w + 8, w + 12 (tile 4j + w
+  // among them, t = j), this tile's fc2 bias and output-layer weights
+  float4 w1raw[4][2];
+  float b2v, w3raw[3];
+  {
+    const float* W1 = P + L.W1 + (int64_t)net * H * 20;
+    const int o0 = lg < 2 ? 8 * lg : 16, o1 = lg < 2 ? 8 * lg + 4 : 16;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float* bp = W1 + (int64_t)(16 * (w + 4 * t) + li) * 20;
+      w1raw[t][0] = *reinterpret_cast<const float4*>(bp + o0);
+      w1raw[t][1] = *reinterpret_cast<const float4*>(bp + o1);
+    }
+    const int n = n0 + li;
+    b2v = P[L.b2 + net * H + n];
+    w3raw[0] = P[(net == 0 ? L.W3a : L.W3c) + n];
+    w3raw[1] = P[L.W3a + H + n];
+    w3raw[2] = P[L.W3a + 2 * H + n];
+  }
+  // ---- A: gather (rowpass_kernel's), fc1 of all 16 tiles ---------------------
+  {
+    auto head_consts = [&] {
+      asm volatile("" : "+v"(hls_d), "+v"(hb3_d)::"memory");
+      if (hd >= 0 && hd < 4) {
+        sm.hb3s[hd] = hb3_d;
+        if (hd < 3) {
+          const float sd = expf(hls_d), var = sd * sd;
+          sm.hcs[0][hd] = var;
+          sm.hcs[1][hd] = logf(sd);
+          sm.hcs[2][hd] = 1.0f / var;
+        }
+      }
+    };
+    if (idx == nullptr) {
+      static_assert(R * 8 <= NT, "one float4 per thread");
+      const int r = (tid >> 3) & (R - 1), c4 = tid & 7, row = r0 + r;
+      const bool in = tid < R * 8;
+      float4 v = reinterpret_cast<const float4*>(src)[(int64_t)(row < mb ? row : mb - 1) * 8 + c4];
+      head_consts();
+      if (row >= mb) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in) {
+        const float e4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * c4 + e;
+          if (c < 18) sm.S[r][c] = e4[e];
+          else if (c < 26) sm.ax[r][c - 18] = e4[e];
+        }
+      }
+    } else {
+      for (int q = tid; q < R * 26; q += NT) {
+        const int r = q / 26, c = q % 26, row = r0 + r;
+        const float v = row < mb ? src[idx[row] * 32 + c] : 0.0f;
+        if (c < 18) sm.S[r][c] = v; else sm.ax[r][c - 18] = v;
+      }
+      head_consts();
+    }
+  }
+  for (int q = tid; q < R * (LDS_S - 18); q += NT) {
+    const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
+    sm.S[r][c] = (c == 18 && r < mb - r0) ? 1.0f : 0.0f;
+  }
+  rp_barrier();
+  WPre<1> preB;
+  mfma_rows_pre<H, 1>(P + L.W2 + (int64_t)net * H * H, n0, preB);
+  float w3[3];
+  float4 bw1[4][2];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    bw1[t][0] = lg < 3 ? w1raw[t][0] : z4;
+    bw1[t][1] = lg < 2 ? w1raw[t][1] : z4;
+  }
+  w3[0] = w3raw[0];
+  w3[1] = net == 0 ? w3raw[1] : 0.0f;
+  w3[2] = net == 0 ? w3raw[2] : 0.0f;
+  f4 a1[1][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) a1[0][t] = f4{0.f, 0.f, 0.f, 0.f};
+  mfma_chunk<LDS_S, 1, 4, 4>(&sm.S[li][8 * lg], bw1, a1);
+  float h1[1][1][4];
+  unsigned h1w[1][1][6];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float hv[4];
+    unsigned wd[6];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hv[q] = tanh_f32(a1[0][t][q]);
+    put3_col4<PS, LDP>(sm.h1p, (4 * lg) * LDP + 16 * (w + 4 * t) + li, hv, wd);
+    if (t == j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h1[0][0][q] = hv[q];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) h1w[0][0][q] = wd[q];
+    }
+  }
+  rp_barrier();
+  // ---- B: this tile of Z2 = H1 W2^T ------------------------------------------
+  f4 acc[1][1];
+  acc[0][0] = f4{0.f, 0.f, 0.f, 0.f};
+  mfma_rows3<H, LDP, PS, H, 1, 1, true>(sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
+  // the H1 k-packed planes of this tile (and the padded chunk's zero rows)
+  auto h1_kx = [&] {
+    store_kx_w<H, R, 1, true>(H1x + net * 3 * PLX, PLX, r0, n0, h1w);
+    if (r0 + R < kx_rows(mb) && r0 + R >= mb) {
+      const float z[1][1][4] = {};
+      store_kx<H, R, 1>(H1x + net * 3 * PLX, PLX, r0 + R, n0, z);
+      store_kx<H, R, 1>(dZ2x + net * 3 * PLX, PLX, r0 + R, n0, z);
+    }
+  };
+  h1_kx();
+  WPre<1> preD;
+  mfma_rows_pre<H, 1>(W2T + (int64_t)net * H * H, n0, preD);
+  // ---- C (forward): tanh(fc2), this tile's output-layer partials -> X1 -------
+  const int NQ = net == 0 ? 3 : 1;
+  {
+    float ps[12];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const float h = tanh_f32(acc[0][0][q4] + b2v);
+      acc[0][0][q4] = h;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) ps[q * 4 + q4] = fmaf(h, w3[q], 0.0f);
+    }
+    if (NQ == 3) {
+      row16_sum_n<12>(ps);
+    } else {
+      float p0[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p0[k] = ps[k];
+      row16_sum_n<4>(p0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ps[k] = p0[k];
+    }
+    if (li == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (q >= NQ) break;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) sm.xs[4 * lg + q4][q][w] = ps[q * 4 + q4];
+      }
+    }
+  }
+  rp_barrier();
+  static_assert(sizeof(sm.xs) == 96 * 8, "X1 staging: 96 8-B stores, six 128-B lines");
+  if (tid < 96)
+    cs_store8(reinterpret_cast<unsigned long long*>(&g_cs_x1[grp][j][0][0][0]) + tid,
+              reinterpret_cast<const unsigned long long*>(&sm.xs[0][0][0])[tid]);
+  if (!cs_handoff(ctr, 1u, &sm.ok)) {
+    if constexpr (SPAN) satrl_span::exit(span, span_t0);
+    return;
+  }
+  if (tid < kCsSplit * R * 3) {                                    // every quarter's partials -> osum[r][q][4jq + w]
+    const int jq = tid / (R * 3), rq = tid % (R * 3), r = rq / 3, q = rq % 3;
+    *reinterpret_cast<float4*>(&sm.osum[r][q][4 * jq]) =
+        cs_load16(&g_cs_x1[grp][0][0][0][0], (int)sizeof(g_cs_x1[0]), ((jq * R + r) * 3 + q) * 16);
+  }
+  rp_barrier();
+  // ---- C: the loss head (rowpass_kernel's, in every quarter; quarter 0 stores) --
+  float* tp = ptail + (int64_t)rb * L.tail;
+  if (tid < R) {
+    const int r = tid, row = r0 + r;
+    float dz[4] = {0.f, 0.f, 0.f, 0.f}, dls[4] = {0.f, 0.f, 0.f, 0.f};
+    if (row < mb) {
+      const float inv = inv_mb;
+      if (net == 0) {
+        float th[3], mu[3], dv[3], var[3], logp[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          th[d] = tanh_f32(out_sum<H / 16>(sm.osum, r, d) + sm.hb3s[d]);
+          mu[d] = max_action * th[d];
+          var[d] = sm.hcs[0][d];
+          dv[d] = sm.ax[r][d] - mu[d];
+          logp[d] = (-(dv[d] * dv[d]) / (2.0f * var[d]) - sm.hcs[1][d]) - kLogSqrt2Pi;
+        }
+        const float lsum = (logp[0] + logp[1]) + logp[2];
+        const float lold = (sm.ax[r][3] + sm.ax[r][4]) + sm.ax[r][5];
+        const float ratio = expf(lsum - lold);
+        if (ratio_out != nullptr && j == 0) ratio_out[row] = ratio;
+        const float adv = sm.ax[r][6];
+        const float s1 = ratio * adv;
+        const float cr = fminf(fmaxf(ratio, 1.0f - epsilon), 1.0f + epsilon);
+        const float s2 = cr * adv;
+        const float g1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+        const float g2 = s2 < s1 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+        const float inside = (ratio >= 1.0f - epsilon && ratio <= 1.0f + epsilon) ? 1.0f : 0.0f;
+        const float dmin = -inv;
+        const float dratio = dmin * g1 * adv + dmin * g2 * adv * inside;
+        const float dlsum = dratio * ratio;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const float dvv = dv[d] * sm.hcs[2][d];
+          const float dmu = dlsum * dvv;
+          dz[d] = (dmu * max_action) * (1.0f - th[d] * th[d]);
+          dls[d] = dlsum * (dv[d] * dvv - 1.0f) - ent_coef * inv;
+        }
+      } else {
+        const float vc = out_sum<H / 16>(sm.osum, r, 0) + sm.hb3s[3];
+        dz[3] = 2.0f * inv * (vc - sm.ax[r][7]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sm.dz3s[r][q] = dz[q];
+    float red[7] = {dz[0], dz[1], dz[2], dls[0], dls[1], dls[2], dz[3]};
+    row16_sum_n<7>(red);
+    if (r == 0 && j == 0) {
+      if (net == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          tp[5 * H + q] = red[q];
+          tp[5 * H + 4 + q] = red[3 + q];
+        }
+        tp[5 * H + 3] = 0.0f;
+        tp[5 * H + 7] = 0.0f;
+      } else {
+        tp[6 * H + 8] = red[6];
+        tp[6 * H + 9] = 0.0f; tp[6 * H + 10] = 0.0f; tp[6 * H + 11] = 0.0f;
+      }
+    }
+  }
+  rp_barrier();
+  // ---- C: tail of this tile (rowpass_kernel's), dZ2 planes -> LDS, k-packed, X2 --
+  float d2v[1][1][4];
+  unsigned d2w[1][1][6];
+  auto tail = [&](auto actor) {
+    constexpr bool ACT = decltype(actor)::value;
+    constexpr int NC = ACT ? 3 : 1;
+    const int n = n0 + li;
+    float cb2 = 0.f, cw[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) cw[q] = 0.f;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int r = 4 * lg + q4;
+      const float h = acc[0][0][q4];
+      float dh;
+      if constexpr (ACT) dh = (sm.dz3s[r][0] * w3[0] + sm.dz3s[r][1] * w3[1]) + sm.dz3s[r][2] * w3[2];
+      else dh = sm.dz3s[r][3] * w3[0];
+      const float d2 = dh * (1.0f - h * h);
+      d2v[0][0][q4] = d2;
+      cb2 += d2;
+      if constexpr (ACT) {
+        cw[0] = fmaf(sm.dz3s[r][0], h, cw[0]); cw[1] = fmaf(sm.dz3s[r][1], h, cw[1]); cw[2] = fmaf(sm.dz3s[r][2], h, cw[2]);
+      } else {
+        cw[0] = fmaf(sm.dz3s[r][3], h, cw[0]);
+      }
+    }
+    put3_col4<PS, LDP>(sm.dzp, (4 * lg) * LDP + n, d2v[0][0], d2w[0][0]);
+    cb2 = xor32_sum(xor16_sum(cb2));
+#pragma unroll
+    for (int q = 0; q < NC; ++q) cw[q] = xor32_sum(xor16_sum(cw[q]));
+    if (lg == 0) {
+      tp[net * H + n] = cb2;
+      if constexpr (ACT) {
+        tp[2 * H + n] = cw[0]; tp[3 * H + n] = cw[1]; tp[4 * H + n] = cw[2];
+      } else {
+        tp[5 * H + 8 + n] = cw[0];
+      }
+    }
+  };
+  if (net == 0) tail(std::true_type{});
+  else tail(std::false_type{});
+  store_kx_w<H, R, 1, true>(dZ2x + net * 3 * PLX, PLX, r0, n0, d2w);
+  rp_barrier();
+  // this quarter's 64 columns of the three planes: 48 runs of 128 B, one run
+  // per 16 lanes of one 8-B store instruction
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int u = tid + NT * k, c8 = u & 15, pr = u >> 4, p = pr / R, r = pr % R;
+    cs_store8(&g_cs_x2[grp][p][r][64 * j + 4 * c8],
+              *reinterpret_cast<const unsigned long long*>(&sm.dzp[p * PS + r * LDP + 64 * j + 4 * c8]));
+  }
+  if (!cs_handoff(ctr, 2u, &sm.ok)) {
+    if constexpr (SPAN) satrl_span::exit(span, span_t0);
+    return;
+  }
+  // the other quarters' columns -> dzp (16-B runs)
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int u = tid + NT * k, c16 = u & 7, pr = (u >> 3) % (3 * R), jq = u / (8 * 3 * R);
+    if (jq != j) {
+      const int p = pr / R, r = pr % R, col = 64 * jq + 8 * c16;
+      *reinterpret_cast<float4*>(&sm.dzp[p * PS + r * LDP + col]) =
+          cs_load16(&g_cs_x2[grp][0][0][0], (int)sizeof(g_cs_x2[0]), ((p * R + r) * 256 + col) * 2);
+    }
+  }
+  rp_barrier();
+  // ---- D: this tile of dH1 = dZ2 W2 ------------------------------------------
+  acc[0][0] = f4{0.f, 0.f, 0.f, 0.f};
+  mfma_rows3<H, LDP, PS, H, 1, 1, true>(sm.dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
+  // ---- E: dZ1, [dW1 | db1] rows of this tile (rowpass_kernel's) ---------------
+  float* pw = pw1 + (int64_t)rb * 2 * H * 20 + (int64_t)net * H * 20;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) acc[0][0][q4] = acc[0][0][q4] * (1.0f - h1[0][0][q4] * h1[0][0][q4]);
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {
+    f4 d = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) d = mfma4(acc[0][0][kk], sm.S[4 * lg + kk][16 * hb + li], d);
+    const int kp = 16 * hb + li;
+    if (kp < 20) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) pw[(int64_t)(n0 + 4 * lg + q4) * 20 + kp] = d[q4];
+    }
+  }
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
+}
+
+// ---------------------------------------------------------------------------
 // policy: the rollout's forward passes on the rowpass's own MLP code
 // (mlp_forward), one workgroup per 32-row block and net.
 //   MODE 0  actor -> mean = max_action*tanh(.) -> Normal sample -> clamp ->
@@ -2149,6 +2572,23 @@ int satrl_ppo_sizes(int H, int mb, int64_t* nwg, int64_t* nblk) {
   return 0;
 }
 
+// the column-split short rowpass (rowpass_cs_kernel) runs when mb <= kCsMaxMb
+// and every workgroup of its grid is resident at once (its groups wait on
+// each other inside the launch): the occupancy API's answer, once per process
+static bool cs_fits(int mb) {
+  if (mb > kCsMaxMb) return false;
+  static const int resident = [] {
+    int dev = 0, per_cu = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rowpass_cs_kernel<false>, kCsWaves * 64, 0) !=
+            hipSuccess)
+      return 0;
+    return per_cu * cus;
+  }();
+  return (2 * ((mb + kRowsShort - 1) / kRowsShort) + 7) / 8 * 32 <= resident;
+}
+
 // every rowpass launch: fdw2 (H <= 128) writes the block's dW2 partial to p2
 // instead of H1 / dZ2; ratio (nullable) receives the actor's per-row ratio
 static int launch_rowpass(int H, int mb, int net, const float* src, const int64_t* idx, const float* P,
@@ -2161,7 +2601,12 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
   // waves per workgroup: one 16-column tile per wave for both 16-row tiles
   const float inv_mb = 1.0f / (float)mb;
   const int nw = H == 64 ? 4 : H == 128 ? 8 : 16;                  // waves per workgroup
-  unsigned long long* sp = satrl_span::take(satrl_span::kRowpass, (int64_t)g.x * nw);
+  // (H = 256, k-packed, both nets, mb <= kCsMaxMb: the column-split kernel,
+  // groups of kCsSplit workgroups dealt in windows of 32 blocks)
+  const bool cs = H == 256 && kx && R == kRowsShort && net < 0 && cs_fits(mb);
+  const dim3 gc((unsigned)((2 * nrb + 7) / 8 * 32));
+  unsigned long long* sp =
+      satrl_span::take(satrl_span::kRowpass, cs ? (int64_t)gc.x * kCsWaves : (int64_t)g.x * nw);
 #define RP_ARGS mb, src, idx, P, W2X, epsilon, ent_coef, max_action, H1, dZ2, ptail, pw1, net, p2, nrb, ratio, inv_mb, sp
 #define RP_LAUNCH(HH, NWW, RR, F, K)                                                                          \
   do {                                                                                                        \
@@ -2176,7 +2621,18 @@ static int launch_rowpass(int H, int mb, int net, const float* src, const int64_
     RP_LAUNCH(128, 8, kRows, true, false);
   else if (H == 128)
     RP_LAUNCH(128, 8, kRows, false, false);
-  else if (kx && R == kRowsShort)
+  else if (cs) {
+    if (sp)
+      hipLaunchKernelGGL(rowpass_cs_kernel<true>, gc, dim3(kCsWaves * 64), 0, s, mb, src, idx, P,
+                         static_cast<const float*>(W2X), epsilon, ent_coef, max_action,
+                         reinterpret_cast<unsigned short*>(H1), reinterpret_cast<unsigned short*>(dZ2), ptail, pw1,
+                         ratio, inv_mb, sp);
+    else
+      hipLaunchKernelGGL(rowpass_cs_kernel<false>, gc, dim3(kCsWaves * 64), 0, s, mb, src, idx, P,
+                         static_cast<const float*>(W2X), epsilon, ent_coef, max_action,
+                         reinterpret_cast<unsigned short*>(H1), reinterpret_cast<unsigned short*>(dZ2), ptail, pw1,
+                         ratio, inv_mb, nullptr);
+  } else if (kx && R == kRowsShort)
     RP_LAUNCH(256, 16, kRowsShort, false, true);
   else if (kx)
     RP_LAUNCH(256, kNW256, kRows, false, true);
@@ -2238,6 +2694,26 @@ int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t
   if (!kx_fits(H, mb, net, kx_elems, "satrl_ppo_rowpass_kx")) return -1;
   return launch_rowpass(H, mb, net, src, idx, P, W2X, epsilon, ent_coef, max_action, static_cast<float*>(H1x),
                         static_cast<float*>(dZ2x), ptail, pw1, nullptr, nullptr, false, stream, true);
+}
+
+int satrl_ppo_rowpass_error(int* err, void* stream) {
+  if (!err) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  unsigned e = 0;
+  void *pe = nullptr, *pc = nullptr;
+  if (hipGetSymbolAddress(&pe, HIP_SYMBOL(g_cs_err)) != hipSuccess ||
+      hipGetSymbolAddress(&pc, HIP_SYMBOL(g_cs_ctr)) != hipSuccess ||
+      hipMemcpyAsync(&e, pe, sizeof(e), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+    g_err = "satrl_ppo_rowpass_error: reading the exchange error word failed";
+    return -1;
+  }
+  *err = e != 0;
+  if (e != 0 && (hipMemsetAsync(pe, 0, sizeof(g_cs_err), s) != hipSuccess ||
+                 hipMemsetAsync(pc, 0, sizeof(g_cs_ctr), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) {
+    g_err = "satrl_ppo_rowpass_error: re-arming the exchange state failed";
+    return -1;
+  }
+  return 0;
 }
 
 int satrl_ppo_dw2_kx_splits(int H, int mb, int net) {

@@ -196,6 +196,21 @@ def w2x_decode(img, H):
     return img.view(2, H, H)
 
 
+def rowpass_exchange_check(stream=None):
+    """satrl_ppo_rowpass_error (include/satrl_ppo.h): synchronises the stream;
+    raises if a column-split short rowpass launch timed out waiting for the
+    other workgroups of its group (its outputs, hence this update, are
+    invalid), after the library has re-armed the exchange state."""
+    L = _lib.lib()
+    if _lib.LIB_PATH != _lib._PRODUCT_LIB and not hasattr(L, "satrl_ppo_rowpass_error"):
+        return                               # (an older development build: A/B only)
+    e = C.c_int(0)
+    check(L.satrl_ppo_rowpass_error(C.byref(e), stream_ptr(stream)), "satrl_ppo_rowpass_error")
+    if e.value:
+        raise RuntimeError("satrl_ppo_rowpass_kx: a column-split exchange timed out (its workgroups were not "
+                           "resident together); the update is invalid")
+
+
 class FusedMinibatch:
     """One PPO minibatch step for actor + critic on shared rows:
     satrl_ppo_rowpass (gather, MLP forward/backward on f32 MFMA, losses),
@@ -720,6 +735,8 @@ class PPOLearner:
             st.run(src, perm)
         if self.peer is not None:
             self.peer.check()                # a peer's value never arrived: the update is invalid
+        if self.H == 256:
+            rowpass_exchange_check()         # (the column-split short rowpass: minibatches / tails <= 512 rows)
         if self.use_lr_decay:
             self.lr_decay(total_steps)
 
