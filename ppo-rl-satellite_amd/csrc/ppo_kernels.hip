@@ -1262,6 +1262,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
   const int64_t PLX = kx_rows(mb) * H;
   const Layout L = layout(H);
   unsigned* ctr = &g_cs_ctr[grp][0];
+  PHASE_PROBE(0);
 
   // head scalars: lanes 0-3 of the last wave (no row load of its own)
   const int hd = tid - (NT - 64);
@@ -1332,7 +1333,9 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
     const int r = q / (LDS_S - 18), c = 18 + q % (LDS_S - 18);
     sm.S[r][c] = (c == 18 && r < mb - r0) ? 1.0f : 0.0f;
   }
+  PHASE_PROBE(8);
   rp_barrier();
+  PHASE_PROBE(9);
   WPre<1> preB;
   mfma_rows_pre<H, 1>(P + L.W2 + (int64_t)net * H * H, n0, preB);
   float w3[3];
@@ -1350,6 +1353,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
 #pragma unroll
   for (int t = 0; t < 4; ++t) a1[0][t] = f4{0.f, 0.f, 0.f, 0.f};
   mfma_chunk<LDS_S, 1, 4, 4>(&sm.S[li][8 * lg], bw1, a1);
+  PHASE_PROBE(10);
   float h1[1][1][4];
   unsigned h1w[1][1][6];
 #pragma unroll
@@ -1366,11 +1370,14 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
       for (int q = 0; q < 6; ++q) h1w[0][0][q] = wd[q];
     }
   }
+  PHASE_PROBE(11);
   rp_barrier();
+  PHASE_PROBE(1);
   // ---- B: this tile of Z2 = H1 W2^T ------------------------------------------
   f4 acc[1][1];
   acc[0][0] = f4{0.f, 0.f, 0.f, 0.f};
   mfma_rows3<H, LDP, PS, H, 1, 1, true>(sm.h1p, P + L.W2 + (int64_t)net * H * H, n0, acc, &preB);
+  PHASE_PROBE(2);
   // the H1 k-packed planes of this tile (and the padded chunk's zero rows)
   auto h1_kx = [&] {
     store_kx_w<H, R, 1, true>(H1x + net * 3 * PLX, PLX, r0, n0, h1w);
@@ -1413,6 +1420,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
       }
     }
   }
+  PHASE_PROBE(3);
   rp_barrier();
   static_assert(sizeof(sm.xs) == 96 * 8, "X1 staging: 96 8-B stores, six 128-B lines");
   if (tid < 96)
@@ -1422,12 +1430,14 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
     if constexpr (SPAN) satrl_span::exit(span, span_t0);
     return;
   }
+  PHASE_PROBE(12);
   if (tid < kCsSplit * R * 3) {                                    // every quarter's partials -> osum[r][q][4jq + w]
     const int jq = tid / (R * 3), rq = tid % (R * 3), r = rq / 3, q = rq % 3;
     *reinterpret_cast<float4*>(&sm.osum[r][q][4 * jq]) =
         cs_load16(&g_cs_x1[grp][0][0][0][0], (int)sizeof(g_cs_x1[0]), ((jq * R + r) * 3 + q) * 16);
   }
   rp_barrier();
+  PHASE_PROBE(13);
   // ---- C: the loss head (rowpass_kernel's, in every quarter; quarter 0 stores) --
   float* tp = ptail + (int64_t)rb * L.tail;
   if (tid < R) {
@@ -1491,6 +1501,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
     }
   }
   rp_barrier();
+  PHASE_PROBE(4);
   // ---- C: tail of this tile (rowpass_kernel's), dZ2 planes -> LDS, k-packed, X2 --
   float d2v[1][1][4];
   unsigned d2w[1][1][6];
@@ -1534,6 +1545,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
   else tail(std::false_type{});
   store_kx_w<H, R, 1, true>(dZ2x + net * 3 * PLX, PLX, r0, n0, d2w);
   rp_barrier();
+  PHASE_PROBE(5);
   // this quarter's 64 columns of the three planes: 48 runs of 128 B, one run
   // per 16 lanes of one 8-B store instruction
 #pragma unroll
@@ -1546,6 +1558,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
     if constexpr (SPAN) satrl_span::exit(span, span_t0);
     return;
   }
+  PHASE_PROBE(14);
   // the other quarters' columns -> dzp (16-B runs)
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -1560,6 +1573,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
   // ---- D: this tile of dH1 = dZ2 W2 ------------------------------------------
   acc[0][0] = f4{0.f, 0.f, 0.f, 0.f};
   mfma_rows3<H, LDP, PS, H, 1, 1, true>(sm.dzp, W2T + (int64_t)net * H * H, n0, acc, &preD);
+  PHASE_PROBE(6);
   // ---- E: dZ1, [dW1 | db1] rows of this tile (rowpass_kernel's) ---------------
   float* pw = pw1 + (int64_t)rb * 2 * H * 20 + (int64_t)net * H * 20;
 #pragma unroll
@@ -1575,6 +1589,7 @@ __global__ void __launch_bounds__(kCsWaves * 64) rowpass_cs_kernel(
       for (int q4 = 0; q4 < 4; ++q4) pw[(int64_t)(n0 + 4 * lg + q4) * 20 + kp] = d[q4];
     }
   }
+  PHASE_PROBE(7);
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 

@@ -36,7 +36,8 @@ if os.environ.get("SATRL_BLAS"):                       # dev A/B: torch's BLAS b
 from satrl.trainer import args_param  # noqa: E402
 
 H, mb = int(os.environ.get("PROBE_H", "256")), int(os.environ.get("PROBE_MB", "4096"))
-NWV = H // 16                                   # waves per rowpass workgroup
+CS = H == 256 and mb <= 512                     # the column-split short rowpass (4-wave workgroups)
+NWV = 4 if CS else H // 16                      # waves per rowpass workgroup
 print("H", H, "mb", mb)
 a = args_param(hidden_width=H, mini_batch_size=mb, batch_size=16 * mb, chkpt_dir="/tmp")
 L = PPOLearner(a, "pursuer", use_graph=bool(os.environ.get("PROBE_CHAIN")))   # chain: the graphed update
@@ -64,32 +65,59 @@ if probe:
     assert lib.satrl_probe_read(buf.ctypes.data) == 0
     b = buf.astype(np.int64)                     # [wg][stamp][wave][realtime, shader clock]
     order = [0, 8, 9, 10, 11, 1, 2, 3, 12, 13, 14, 4, 5, 6, 7]   # 12-14: inside the loss head (wave 0)
-    b = b[:2 * (mb // 32), :, :NWV]               # the launched workgroups and waves only
-    t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
-    print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
-          "(median over workgroups), waves 0..%d; actor rows then critic rows" % (NWV - 1))
-    for net, sl in (("actor", slice(0, None, 2)), ("critic", slice(1, None, 2))):
-        print(f"  {net}")
-        for k in order:
-            v = b[sl, k, :, 1] - t0[sl, None]
-            print(f"    stamp {k:2d}: " + " ".join(f"{int(x):6d}" for x in np.median(v, axis=0)))
-    if os.environ.get("PROBE_RAW"):
-        for wg in (0, 1, 100):
-            print(f"raw wg {wg}: stamp: realtime ticks rel / clock rel (waves 0, 4, 8, 15)")
-            rt0 = b[wg, 0, :, 0].min()
-            ck0 = b[wg, 0, :, 1].min()
+    if CS:
+        # rowpass_cs: 0 start, 8 gather, 9 S ready, 10 fc1 (16 tiles), 11 tanh + planes, 1 barrier, 2 B,
+        # 3 C fwd, 12 X1 hand-off done, 13 partials in LDS, 4 head, 5 tail + planes, 14 X2 hand-off done,
+        # 6 D (X2 loads included), 7 end.  Rows: per net and quarter j, waves 0..3
+        order = [0, 8, 9, 10, 11, 1, 2, 3, 12, 13, 4, 5, 14, 6, 7]
+        ngrp = 2 * ((mb + 15) // 16)
+        nb = (ngrp + 7) // 8 * 32
+        bb = np.arange(nb)
+        jq, grp = (bb >> 3) & 3, (bb & 7) | ((bb >> 5) << 3)
+        live = grp < ngrp
+        b = b[:nb, :, :4]
+        t0 = b[:, 0, :, 1].min(axis=1)
+        print("per-wave timeline (rowpass_cs): shader-clock time after the workgroup's start, median over groups")
+        for net in (0, 1):
+            for j in range(4):
+                sel = live & (grp % 2 == net) & (jq == j)
+                print(f"  {'actor' if net == 0 else 'critic'} quarter {j}")
+                for k in order:
+                    v = b[sel, k, :, 1] - t0[sel, None]
+                    print(f"    stamp {k:2d}: " + " ".join(f"{int(x):6d}" for x in np.median(v, axis=0)))
+        ws0 = b[live, 0, :, 0].min(axis=1)
+        en = b[live, 7, :, 0].max(axis=1)
+        print("workgroup span: median %.2f us, max %.2f us; start spread %.2f us, kernel span %.2f us" %
+              (np.median(en - ws0) / 100.0, (en - ws0).max() / 100.0, (ws0.max() - ws0.min()) / 100.0,
+               (en.max() - ws0.min()) / 100.0))
+        b = None
+    if b is not None:
+        b = b[:2 * (mb // 32), :, :NWV]               # the launched workgroups and waves only
+        t0 = b[:, 0, :, 1].min(axis=1)               # workgroup start: its first wave's stamp 0
+        print("per-wave timeline: each stamp's shader-clock time after the workgroup's start "
+              "(median over workgroups), waves 0..%d; actor rows then critic rows" % (NWV - 1))
+        for net, sl in (("actor", slice(0, None, 2)), ("critic", slice(1, None, 2))):
+            print(f"  {net}")
             for k in order:
-                print(f"   {k:2d}: " + "  ".join(f"{int(b[wg, k, w_, 0] - rt0):6d}/{int(b[wg, k, w_, 1] - ck0):7d}"
-                                             for w_ in sorted({0, NWV // 4, NWV // 2, NWV - 1})))
-    nwg = 2 * (mb // 32)
-    ws0 = b[:nwg, 0, :, 0].min(axis=1)
-    en = b[:nwg, 7, :, 0].max(axis=1)
-    cyc = (b[:nwg, 7, :, 1].max(axis=1) - b[:nwg, 0, :, 1].min(axis=1)).astype(np.float64)
-    wall = (en - ws0).astype(np.float64) / 100e6
-    print("workgroup span: median %.2f us, max %.2f us; shader clock over it (median GHz) %.3f" %
-          (np.median(wall) * 1e6, wall.max() * 1e6, float(np.median(cyc / wall)) / 1e9))
-    print("start spread %.2f us, end spread %.2f us, kernel span %.2f us" %
-          ((ws0.max() - ws0.min()) / 100.0, (en.max() - en.min()) / 100.0, (en.max() - ws0.min()) / 100.0))
+                v = b[sl, k, :, 1] - t0[sl, None]
+                print(f"    stamp {k:2d}: " + " ".join(f"{int(x):6d}" for x in np.median(v, axis=0)))
+        if os.environ.get("PROBE_RAW"):
+            for wg in (0, 1, 100):
+                print(f"raw wg {wg}: stamp: realtime ticks rel / clock rel (waves 0, 4, 8, 15)")
+                rt0 = b[wg, 0, :, 0].min()
+                ck0 = b[wg, 0, :, 1].min()
+                for k in order:
+                    print(f"   {k:2d}: " + "  ".join(f"{int(b[wg, k, w_, 0] - rt0):6d}/{int(b[wg, k, w_, 1] - ck0):7d}"
+                                                 for w_ in sorted({0, NWV // 4, NWV // 2, NWV - 1})))
+        nwg = 2 * (mb // 32)
+        ws0 = b[:nwg, 0, :, 0].min(axis=1)
+        en = b[:nwg, 7, :, 0].max(axis=1)
+        cyc = (b[:nwg, 7, :, 1].max(axis=1) - b[:nwg, 0, :, 1].min(axis=1)).astype(np.float64)
+        wall = (en - ws0).astype(np.float64) / 100e6
+        print("workgroup span: median %.2f us, max %.2f us; shader clock over it (median GHz) %.3f" %
+              (np.median(wall) * 1e6, wall.max() * 1e6, float(np.median(cyc / wall)) / 1e9))
+        print("start spread %.2f us, end spread %.2f us, kernel span %.2f us" %
+              ((ws0.max() - ws0.min()) / 100.0, (en.max() - en.min()) / 100.0, (en.max() - ws0.min()) / 100.0))
 
 # event timings of each launch of one minibatch step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
