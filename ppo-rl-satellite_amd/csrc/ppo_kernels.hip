@@ -1866,12 +1866,15 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
   dw2_kx_body<TW>(blockIdx.x, mb, S, KR, net_sel, H1x, dZ2x, p2, sm);
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
-// split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks, no empty split
-#ifndef SATRL_KX_WGS
-#define SATRL_KX_WGS 256   // (A/B builds: -DSATRL_KX_WGS=n)
-#endif
-constexpr int kKxWgs = SATRL_KX_WGS;
-int kx_splits(int mb, int net, int target = kKxWgs) {
+// split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks,
+// no empty split; half as many up to kCsMaxMb rows (mb 512: 4 splits of 128
+// rows, in-graph step 28.2-28.8 against 29.2-29.3 us over three
+// alternations -- a slower dW2, 3.3 against 2.5 us, but half the slabs for
+// the reduce and the boundary before it; at mb 1024 slower, 37.2 against
+// 35.6; EXPERIMENTS.md round 6)
+constexpr int kKxWgs = 256;
+int kx_splits(int mb, int net) {
+  const int target = mb <= kCsMaxMb ? kKxWgs / 2 : kKxWgs;
   const int tiles = (net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW), nch = (int)(kx_rows(mb) / 32);
   int S = target / tiles;
   if (S > nch) S = nch;
