@@ -924,7 +924,7 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
                                    h1w);
   // (rows past the minibatch: zero inputs, so tanh(fc1) = 0 and dZ2 = 0 there)
   // (KX) the H1 planes: wave 0, which runs the loss head next, stores its
-  // share after the head, off the head's path; the other waves now
+  // share after the head's barrier, off the head's path; the other waves now
   auto h1_kx = [&] {
     store_kx_w<H, R, CT, R == kRowsShort>(reinterpret_cast<unsigned short*>(H1g) + net * 3 * PLX, PLX, r0, n0, h1w);
     if (R < 32 && r0 + R < kx_rows(mb) && r0 + R >= mb) {            // (uniform) the padded chunk's rows past this block
@@ -1017,11 +1017,15 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
       }
     }
   }
+  rp_barrier();
+  PHASE_PROBE(4);
+  // (wave 0's share of the H1 planes after the head's barrier: before it, the
+  // barrier's vmcnt(0) waited for those stores' write latency with the other
+  // 15 waves idle -- in-graph step 47.73-47.88 against 47.99-48.51 us over
+  // four alternations, bitwise the same; EXPERIMENTS.md round 6)
   if constexpr (KX) {
     if (w == 0) h1_kx();
   }
-  rp_barrier();
-  PHASE_PROBE(4);
   float* tp = ptail + (int64_t)rb * L.tail;                         // tail-relative slab of this row block
   float d2v[RT][CT][4];
   unsigned d2w[RT][CT][6];                                         // (split-bf16) the split dZ2 words

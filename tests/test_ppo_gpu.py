@@ -631,7 +631,8 @@ def test_rollout_logp_equals_update_recomputation(H, mb):
 
 
 
-@pytest.mark.parametrize("mb,contig", [(4096, True), (1500, False), (512, True), (777, False), (520, True)])
+@pytest.mark.parametrize("mb,contig", [(4096, True), (1500, False), (512, True), (777, False), (520, True),
+                                       (288, True), (100, False)])
 def test_kx_rowpass_planes_and_dw2(mb, contig):
     """H 256: satrl_ppo_rowpass_kx writes H1 / dZ2 as k-packed bf16 planes
     whose sum hi + mid + lo is bitwise the f32 rowpass's H1 / dZ2 (rows past
@@ -640,7 +641,11 @@ def test_kx_rowpass_planes_and_dw2(mb, contig):
     f64 reference (ppo_continuous.py:227-233: fc2.weight.grad).  1500: a ragged
     last chunk on the index-gather path.  512 / 777 / 520: the 16-row rowpass
     (configs[3]'s per-rank minibatch, ragged tails), whose last block zero-fills
-    the padded half of its 32-row chunk (777: rows 784-799, 520: 528-543)."""
+    the padded half of its 32-row chunk (777: rows 784-799, 520: 528-543).
+    512 / 288 / 100: the column-split kernel (four workgroups per row block
+    and net exchanging partials inside the launch; 288: a last window of 32
+    blocks with whole groups past the grid, 100: index gather, a ragged
+    block); its exchange reports no timeout."""
     import satrl._lib as _L
     from satrl.ppo import PPOLearner
     torch.manual_seed(5)
@@ -690,4 +695,6 @@ def test_kx_rowpass_planes_and_dw2(mb, contig):
     mag = torch.einsum("brn,brm->bnm", dZ2.double().abs(), H1.double().abs())
     err = ((got - ref).abs() / mag.clamp_min(1e-30)).max().item()
     assert err < 2e-6, err                 # per-slab split-bf16 sums (<= 2.2e-7 each) + f32 slab rounding
+    from satrl.ppo import rowpass_exchange_check
+    rowpass_exchange_check()               # raises if a column-split exchange timed out
 
