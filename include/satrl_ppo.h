@@ -151,10 +151,11 @@ int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t
 int satrl_ppo_dw2_kx_splits(int H, int mb, int net);
 int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
                      int64_t p2_floats, void* stream);
-/* Up to 512 rows (configs[3]'s per-rank minibatch), both nets, when its
- * grid is resident at once, satrl_ppo_rowpass_kx runs the column-split
- * kernel: each (16-row block, net) on four workgroups of four waves, one per
- * 64 hidden columns, which exchange the output-layer partials and the dZ2
+/* Up to 1024 rows (configs[3]'s per-rank minibatch, the 16-row range),
+ * both nets, when its grid is resident at once, satrl_ppo_rowpass_kx runs
+ * the column-split kernel: each (16-row block, net) on four workgroups of
+ * four waves, one per 64 hidden columns, which exchange the output-layer
+ * partials and the dZ2
  * planes inside the launch (bitwise the 16-wave kernel's outputs).  Its
  * exchange state is the library's own, per device: launches of it must not
  * run concurrently on two streams of one device.  A wait that times out

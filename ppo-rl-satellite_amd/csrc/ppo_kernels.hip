@@ -1190,7 +1190,10 @@ __global__ void __launch_bounds__(NW * 64, NW * 64 / 256) rowpass_kernel(int mb,
 // satrl_ppo_rowpass_error reports it and re-arms the counters.
 // ---------------------------------------------------------------------------
 constexpr int kCsWaves = 4, kCsSplit = 256 / 16 / kCsWaves;   // waves per workgroup, workgroups per group
-constexpr int kCsMaxMb = 512;                                  // minibatches of up to this many rows
+// minibatches of up to this many rows (the whole 16-row range: at mb 1024
+// 512 workgroups, two per CU; in-graph step 33.2 against 35.5 us, at mb 768
+// 32.2 against 34.4, three alternations; EXPERIMENTS.md round 6)
+constexpr int kCsMaxMb = 1024;
 constexpr int kCsMaxGroups = 2 * (kCsMaxMb / kRowsShort);      // (row block, net) groups
 constexpr unsigned long long kCsTimeoutTicks = 50000000ull;     // 0.5 s of s_memrealtime (100 MHz)
 __device__ __attribute__((aligned(128))) unsigned g_cs_ctr[kCsMaxGroups][32];   // a 128-B line per counter
@@ -1871,14 +1874,14 @@ __global__ void __launch_bounds__(256) dw2_kx_kernel(int mb, int S, int KR, int 
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 // split-K ways of dw2_kx_kernel: about kKxWgs workgroups, whole 32-row chunks,
-// no empty split; half as many up to kCsMaxMb rows (mb 512: 4 splits of 128
+// no empty split; half as many up to kKxHalfMb rows (mb 512: 4 splits of 128
 // rows, in-graph step 28.2-28.8 against 29.2-29.3 us over three
 // alternations -- a slower dW2, 3.3 against 2.5 us, but half the slabs for
 // the reduce and the boundary before it; at mb 1024 slower, 37.2 against
 // 35.6; EXPERIMENTS.md round 6)
-constexpr int kKxWgs = 256;
+constexpr int kKxWgs = 256, kKxHalfMb = 512;
 int kx_splits(int mb, int net) {
-  const int target = mb <= kCsMaxMb ? kKxWgs / 2 : kKxWgs;
+  const int target = mb <= kKxHalfMb ? kKxWgs / 2 : kKxWgs;
   const int tiles = (net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW), nch = (int)(kx_rows(mb) / 32);
   int S = target / tiles;
   if (S > nch) S = nch;

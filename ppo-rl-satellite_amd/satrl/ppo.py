@@ -736,7 +736,7 @@ class PPOLearner:
         if self.peer is not None:
             self.peer.check()                # a peer's value never arrived: the update is invalid
         if self.H == 256:
-            rowpass_exchange_check()         # (the column-split short rowpass: minibatches / tails <= 512 rows)
+            rowpass_exchange_check()         # (the column-split short rowpass: minibatches / tails <= 1024 rows)
         if self.use_lr_decay:
             self.lr_decay(total_steps)
 

@@ -642,10 +642,10 @@ def test_kx_rowpass_planes_and_dw2(mb, contig):
     last chunk on the index-gather path.  512 / 777 / 520: the 16-row rowpass
     (configs[3]'s per-rank minibatch, ragged tails), whose last block zero-fills
     the padded half of its 32-row chunk (777: rows 784-799, 520: 528-543).
-    512 / 288 / 100: the column-split kernel (four workgroups per row block
-    and net exchanging partials inside the launch; 288: a last window of 32
-    blocks with whole groups past the grid, 100: index gather, a ragged
-    block); its exchange reports no timeout."""
+    Every size up to 1024 runs the column-split kernel (four workgroups per
+    row block and net exchanging partials inside the launch; 288: a last
+    window of 32 blocks with whole groups past the grid, 100: index gather,
+    a ragged block); its exchange reports no timeout."""
     import satrl._lib as _L
     from satrl.ppo import PPOLearner
     torch.manual_seed(5)
