@@ -164,6 +164,12 @@ int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void*
  * reports it in *err (1; 0 = none), and on an error re-arms the exchange
  * state (the update that saw it must be discarded).                       */
 int satrl_ppo_rowpass_error(int* err, void* stream);
+/* Fault injection for tests: sets (row block, net) group `group`'s exchange
+ * counter to `value` (synchronising the stream).  A value that breaks the
+ * counter's invariant (a multiple of 8 at every launch's start, e.g. 5)
+ * makes that group's next launch wait out its timeout, set the error word
+ * and leave the kernel: the path satrl_ppo_rowpass_error reports.        */
+int satrl_ppo_rowpass_fault_inject(int group, unsigned value, void* stream);
 
 /* Rollout forward passes on the rowpass's own MLP code, so every row's result
  * is independent of N and of the sharding, and the rollout's log-probs equal

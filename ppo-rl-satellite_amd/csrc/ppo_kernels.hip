@@ -2741,6 +2741,20 @@ int satrl_ppo_rowpass_error(int* err, void* stream) {
   return 0;
 }
 
+int satrl_ppo_rowpass_fault_inject(int group, unsigned value, void* stream) {
+  if (group < 0 || group >= kCsMaxGroups) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  void* pc = nullptr;
+  if (hipGetSymbolAddress(&pc, HIP_SYMBOL(g_cs_ctr)) != hipSuccess ||
+      hipMemcpyAsync(static_cast<unsigned*>(pc) + (size_t)group * 32, &value, sizeof(value), hipMemcpyHostToDevice, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    g_err = "satrl_ppo_rowpass_fault_inject: writing the exchange counter failed";
+    return -1;
+  }
+  return 0;
+}
+
 int satrl_ppo_dw2_kx_splits(int H, int mb, int net) {
   if (H != 256 || mb <= 0 || net < -1 || net > 1) return -1;
   return kx_splits(mb, net);

@@ -109,6 +109,7 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, big, fake, big, None) == -1       # an empty split (2 chunks)
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, big, fake, big, None) == -1     # null H1x
     assert lib.satrl_ppo_rowpass_error(None, None) == -1                      # the column-split kernel's error word
+    assert lib.satrl_ppo_rowpass_fault_inject(-1, 0, None) == -1 and lib.satrl_ppo_rowpass_fault_inject(1 << 20, 0, None) == -1
     # the peer all-reduce: grid, deadline, buffers
     bufs = (C.c_void_p * 2)(16, 16)
     pa = [C.cast(bufs, C.c_void_p), fake, fake, fake]

@@ -698,3 +698,47 @@ def test_kx_rowpass_planes_and_dw2(mb, contig):
     from satrl.ppo import rowpass_exchange_check
     rowpass_exchange_check()               # raises if a column-split exchange timed out
 
+
+def test_column_split_exchange_timeout_is_reported():
+    """The column-split rowpass's bounded wait (ppo_kernels.hip cs_handoff):
+    a group whose exchange counter breaks its invariant (fault injection:
+    satrl_ppo_rowpass_fault_inject) waits out its 0.5 s timeout and the
+    launch still ends; satrl_ppo_rowpass_error then reports it (the learner
+    raises) and re-arms the exchange, and the next launch's outputs are
+    bitwise a clean launch's."""
+    import time
+    import satrl._lib as _L
+    from satrl.ppo import PPOLearner, rowpass_exchange_check
+    torch.manual_seed(5)
+    H, B, mb = 256, 8192, 512
+    args = _args(hidden_width=H, mini_batch_size=mb, batch_size=B)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    src = torch.randn((B, 32), device="cuda", generator=g)
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+    st = L.stepper(mb)
+    rowpass_exchange_check()
+    for t in (st.ptail, st.pw1):                  # (finite slots past the launched blocks)
+        t.fill_(7.0)
+    st.rowpass_kx(src, None)
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in (st.H1x, st.dZ2x, st.ptail, st.pw1)]
+    # group 0's counter at 5: its four workgroups pass the first hand-off but
+    # wait for 16 at the second while the counter stops at 13
+    assert _L.lib().satrl_ppo_rowpass_fault_inject(0, 5, _L.stream_ptr()) == 0
+    t0 = time.time()
+    st.rowpass_kx(src, None)
+    torch.cuda.synchronize()
+    assert time.time() - t0 < 10.0
+    with pytest.raises(RuntimeError, match="timed out"):
+        rowpass_exchange_check()
+    rowpass_exchange_check()                      # re-armed: no error left
+    for t in (st.ptail, st.pw1):
+        t.fill_(7.0)
+    st.rowpass_kx(src, None)
+    torch.cuda.synchronize()
+    rowpass_exchange_check()
+    for a, b in zip((st.H1x, st.dZ2x, st.ptail, st.pw1), ref):
+        assert torch.equal(a, b)
+
