@@ -151,10 +151,10 @@ void ppo_step(const std::string& out, int mb, hipStream_t st) {
   PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, p2n, d_pw, d_pt, d_G, d_nsq, d_steps, st));
   PPO_OK(satrl_ppo_adam(H, mb, -1, d_nsq, d_steps, d_bct, (int)(bct.size() / 2), d_lr, 0.9f, 0.999f, 1e-5f, 0.5f, 1,
                         d_G, d_P, d_M, d_V, d_W2X, st));
-  // up to 512 rows the rowpass ran the column-split kernel: its in-launch
-  // exchange must not have timed out (the call synchronises the stream)
+  // up to 1024 rows the rowpass ran the column-split kernel: its in-launch
+  // exchange must not have timed out (the call waits for the stream, 60 s at most)
   int xerr = 0;
-  PPO_OK(satrl_ppo_rowpass_error(&xerr, st));
+  PPO_OK(satrl_ppo_rowpass_error(&xerr, 60.0, st));
   if (xerr) {
     std::fprintf(stderr, "c_host_step: the column-split rowpass exchange timed out\n");
     std::exit(1);

@@ -160,10 +160,12 @@ int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void*
  * exchange state is the library's own, per device: launches of it must not
  * run concurrently on two streams of one device.  A wait that times out
  * (0.5 s; a grid not co-resident) leaves the kernel with its outputs invalid
- * and sets an error word: satrl_ppo_rowpass_error synchronises the stream,
- * reports it in *err (1; 0 = none), and on an error re-arms the exchange
- * state (the update that saw it must be discarded).                       */
-int satrl_ppo_rowpass_error(int* err, void* stream);
+ * and sets an error word: satrl_ppo_rowpass_error waits for the stream
+ * (at most timeout_s seconds of host time: -2 when it has not drained by
+ * then, e.g. behind a collective of a dead peer), reports the word in *err
+ * (1; 0 = none), and on an error re-arms the exchange state (the update
+ * that saw it must be discarded).                                          */
+int satrl_ppo_rowpass_error(int* err, double timeout_s, void* stream);
 /* Fault injection for tests: sets (row block, net) group `group`'s exchange
  * counter to `value` (synchronising the stream).  A value that breaks the
  * counter's invariant (a multiple of 8 at every launch's start, e.g. 5)

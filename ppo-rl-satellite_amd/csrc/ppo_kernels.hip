@@ -12,10 +12,13 @@
 // Every reduction has a fixed order, so a step is bitwise reproducible.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -2721,17 +2724,45 @@ int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t
                         static_cast<float*>(dZ2x), ptail, pw1, nullptr, nullptr, false, stream, true);
 }
 
-int satrl_ppo_rowpass_error(int* err, void* stream) {
-  if (!err) return -1;
+int satrl_ppo_rowpass_error(int* err, double timeout_s, void* stream) {
+  if (!err || !(timeout_s > 0)) return -1;
   hipStream_t s = (hipStream_t)stream;
-  unsigned e = 0;
+  // the error word lands in pinned memory behind an event that is polled
+  // against the host deadline: a stream that never drains (e.g. a collective
+  // of a dead peer queued before this call) returns -2 instead of hanging.
+  // After a timeout the buffer and event stay with the stream (leaked): the
+  // next call takes fresh ones.
+  static std::mutex mu;
+  static unsigned* host = nullptr;
+  static hipEvent_t ev = nullptr;
+  std::lock_guard<std::mutex> lock(mu);
   void *pe = nullptr, *pc = nullptr;
-  if (hipGetSymbolAddress(&pe, HIP_SYMBOL(g_cs_err)) != hipSuccess ||
+  if ((!host && hipHostMalloc((void**)&host, 4 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess) ||
+      (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ||
+      hipGetSymbolAddress(&pe, HIP_SYMBOL(g_cs_err)) != hipSuccess ||
       hipGetSymbolAddress(&pc, HIP_SYMBOL(g_cs_ctr)) != hipSuccess ||
-      hipMemcpyAsync(&e, pe, sizeof(e), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+      hipMemcpyAsync(host, pe, sizeof(unsigned), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipEventRecord(ev, s) != hipSuccess) {
     g_err = "satrl_ppo_rowpass_error: reading the exchange error word failed";
     return -1;
   }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) {
+      g_err = "satrl_ppo_rowpass_error: waiting for the stream failed";
+      return -1;
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+      host = nullptr;
+      ev = nullptr;
+      g_err = "satrl_ppo_rowpass_error: the stream did not drain within the deadline";
+      return -2;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  const unsigned e = host[0];
   *err = e != 0;
   if (e != 0 && (hipMemsetAsync(pe, 0, sizeof(g_cs_err), s) != hipSuccess ||
                  hipMemsetAsync(pc, 0, sizeof(g_cs_ctr), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) {

@@ -123,7 +123,7 @@ _SIGS = {
     "satrl_ppo_rowpass_kx": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                               _vp, _i64, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_dw2_kx_splits": ([C.c_int, C.c_int, C.c_int], C.c_int),
-    "satrl_ppo_rowpass_error": ([C.POINTER(C.c_int), _vp], C.c_int),
+    "satrl_ppo_rowpass_error": ([C.POINTER(C.c_int), C.c_double, _vp], C.c_int),
     "satrl_ppo_rowpass_fault_inject": ([C.c_int, C.c_uint, _vp], C.c_int),
     "satrl_ppo_dw2_kx": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _i64, _vp, _i64, _vp], C.c_int),
     "satrl_ppo_w2x_sync": ([C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),

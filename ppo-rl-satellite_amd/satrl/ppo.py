@@ -196,19 +196,33 @@ def w2x_decode(img, H):
     return img.view(2, H, H)
 
 
-def rowpass_exchange_check(stream=None):
-    """satrl_ppo_rowpass_error (include/satrl_ppo.h): synchronises the stream;
-    raises if a column-split short rowpass launch timed out waiting for the
-    other workgroups of its group (its outputs, hence this update, are
-    invalid), after the library has re-armed the exchange state."""
+def rowpass_exchange_check(stream=None, timeout_s=None):
+    """satrl_ppo_rowpass_error (include/satrl_ppo.h): waits for the stream (at
+    most timeout_s of host time, default the DP watchdog's deadline
+    SATRL_DP_TIMEOUT_S: a stream stuck behind a dead peer's collective raises
+    NativeError instead of hanging); raises RuntimeError if a column-split
+    short rowpass launch timed out waiting for the other workgroups of its
+    group (its outputs, hence this update, are invalid), after the library has
+    re-armed the exchange state."""
     L = _lib.lib()
     if _lib.LIB_PATH != _lib._PRODUCT_LIB and not hasattr(L, "satrl_ppo_rowpass_error"):
         return                               # (an older development build: A/B only)
     e = C.c_int(0)
-    check(L.satrl_ppo_rowpass_error(C.byref(e), stream_ptr(stream)), "satrl_ppo_rowpass_error")
+    t = _dist.dp_timeout_s() if timeout_s is None else float(timeout_s)
+    check(L.satrl_ppo_rowpass_error(C.byref(e), t, stream_ptr(stream)), "satrl_ppo_rowpass_error")
     if e.value:
         raise RuntimeError("satrl_ppo_rowpass_kx: a column-split exchange timed out (its workgroups were not "
                            "resident together); the update is invalid")
+
+
+def uses_column_split(H, mb, B):
+    """True when an update of B rows in minibatches of mb may run the
+    column-split short rowpass (H = 256, a full or ragged-tail minibatch of at
+    most 1024 rows; ppo_kernels.hip cs_fits): only such updates need
+    rowpass_exchange_check."""
+    mb = min(int(mb), int(B))
+    tail = int(B) % mb if mb > 0 else 0
+    return H == 256 and mb > 0 and (mb <= 1024 or 0 < tail <= 1024)
 
 
 class FusedMinibatch:
@@ -735,8 +749,8 @@ class PPOLearner:
             st.run(src, perm)
         if self.peer is not None:
             self.peer.check()                # a peer's value never arrived: the update is invalid
-        if self.H == 256:
-            rowpass_exchange_check()         # (the column-split short rowpass: minibatches / tails <= 1024 rows)
+        if uses_column_split(self.H, self.mini_batch_size, B):
+            rowpass_exchange_check()         # (minibatches / tails <= 1024 rows; bounded by the DP deadline)
         if self.use_lr_decay:
             self.lr_decay(total_steps)
 

@@ -108,7 +108,8 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, big, fake, big, None) == -1     # S < 1
     assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, big, fake, big, None) == -1       # an empty split (2 chunks)
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, big, fake, big, None) == -1     # null H1x
-    assert lib.satrl_ppo_rowpass_error(None, None) == -1                      # the column-split kernel's error word
+    assert lib.satrl_ppo_rowpass_error(None, 1.0, None) == -1                 # the column-split kernel's error word
+    assert lib.satrl_ppo_rowpass_error(C.byref(C.c_int()), 0.0, None) == -1  # no deadline
     assert lib.satrl_ppo_rowpass_fault_inject(-1, 0, None) == -1 and lib.satrl_ppo_rowpass_fault_inject(1 << 20, 0, None) == -1
     # the peer all-reduce: grid, deadline, buffers
     bufs = (C.c_void_p * 2)(16, 16)
@@ -218,3 +219,15 @@ def test_w2x_image_host_statement():
         img = w2x_image(W2, H)
         assert img.dtype == torch.float32 and img.numel() == 2 * H * H
         assert torch.equal(w2x_decode(img, H), W2.view(2, H, H).transpose(1, 2))
+
+
+def test_uses_column_split():
+    """Which updates need the exchange check (ppo_kernels.hip cs_fits: H 256,
+    a minibatch or ragged tail of at most 1024 rows)."""
+    from satrl.ppo import uses_column_split
+    assert uses_column_split(256, 512, 8192) and uses_column_split(256, 1024, 8192)
+    assert not uses_column_split(256, 4096, 8192)            # configs[1]-sized minibatches, no tail
+    assert uses_column_split(256, 4096, 8192 + 100)           # a 100-row tail
+    assert not uses_column_split(256, 4096, 8192 + 2000)      # a tail over 1024 rows
+    assert uses_column_split(256, 4096, 700)                  # one minibatch of the whole 700 rows
+    assert not uses_column_split(64, 512, 8192) and not uses_column_split(128, 512, 8192)

@@ -742,3 +742,17 @@ def test_column_split_exchange_timeout_is_reported():
     for a, b in zip((st.H1x, st.dZ2x, st.ptail, st.pw1), ref):
         assert torch.equal(a, b)
 
+
+def test_exchange_check_is_bounded_by_its_deadline():
+    """satrl_ppo_rowpass_error waits for the stream against a host deadline:
+    behind a kernel that outlasts it the call raises (-2, "did not drain")
+    instead of blocking -- the DP learner's guard against a stream stuck
+    behind a dead peer's collective -- and the next call works."""
+    import satrl._lib as _L
+    from satrl.ppo import rowpass_exchange_check
+    rowpass_exchange_check()
+    torch.cuda._sleep(int(1e9))                   # a spin kernel of well over 10 ms
+    with pytest.raises(_L.NativeError, match="did not drain"):
+        rowpass_exchange_check(timeout_s=0.01)
+    torch.cuda.synchronize()
+    rowpass_exchange_check(timeout_s=5.0)
