@@ -147,8 +147,9 @@ void ppo_step(const std::string& out, int mb, hipStream_t st) {
   float* d_p2 = dev<float>((size_t)p2n);
   PPO_OK(satrl_ppo_rowpass_kx(H, mb, -1, d_src, nullptr, d_P, d_W2X, 0.1f, 0.01f, 1.6f, d_H1x, d_dZ2x, kxe, d_pt,
                               d_pw, st));
-  PPO_OK(satrl_ppo_dw2_kx(H, mb, -1, S, d_H1x, d_dZ2x, kxe, d_p2, p2n, st));
-  PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3, d_p2, p2n, d_pw, d_pt, d_G, d_nsq, d_steps, st));
+  // dW2 with the reduce's W1 / tail regions in the same launch, then the W2 region
+  PPO_OK(satrl_ppo_dw2_kx_w1(H, mb, -1, S, d_H1x, d_dZ2x, kxe, d_p2, p2n, 3, d_pw, d_pt, d_G, d_nsq, st));
+  PPO_OK(satrl_ppo_reduce(H, mb, -1, S, 3 | 4, d_p2, p2n, nullptr, nullptr, d_G, d_nsq, d_steps, st));
   PPO_OK(satrl_ppo_adam(H, mb, -1, d_nsq, d_steps, d_bct, (int)(bct.size() / 2), d_lr, 0.9f, 0.999f, 1e-5f, 0.5f, 1,
                         d_G, d_P, d_M, d_V, d_W2X, st));
   // up to 1024 rows the rowpass ran the column-split kernel: its in-launch

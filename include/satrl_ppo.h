@@ -69,7 +69,9 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
  * satrl_ppo_rowpass [dW1|db1] slabs, pt: satrl_ppo_rowpass tail slabs); mode 2: per-block
  * sums of squares of G per net into nsq [n_norm_blocks][2] (f64) and
  * advance steps [net] (f64); mode 3: both.  (mode 1 | all-reduce(G) | mode 2
- * under data parallelism.)  Every sum has a fixed order.                  */
+ * under data parallelism.)  Every sum has a fixed order.  Mode bit 4 (with
+ * 1 or 3): the W2 region only, after satrl_ppo_dw2_kx_w1 summed the W1 and
+ * tail regions (p1 / pt may then be NULL).                                 */
 int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, int64_t p2_floats, const float* p1,
                      const float* pt, float* G, double* nsq, double* steps, void* stream);
 
@@ -151,6 +153,14 @@ int satrl_ppo_rowpass_kx(int H, int mb, int net, const float* src, const int64_t
 int satrl_ppo_dw2_kx_splits(int H, int mb, int net);
 int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
                      int64_t p2_floats, void* stream);
+/* satrl_ppo_dw2_kx and satrl_ppo_reduce's W1 / tail regions in one launch
+ * (their slabs p1 / pt are the rowpass's, ready before dW2 runs): G's W1 and
+ * tail parts, and with mode 3 their squared-norm pairs in nsq; then
+ * satrl_ppo_reduce(..., mode | 4, ...) sums the W2 region.  Bitwise the
+ * dw2_kx + reduce(mode) pair.  mode 1 or 3.                                */
+int satrl_ppo_dw2_kx_w1(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
+                        int64_t p2_floats, int mode, const float* p1, const float* pt, float* G, double* nsq,
+                        void* stream);
 /* Up to 1024 rows (configs[3]'s per-rank minibatch, the 16-row range),
  * both nets, when its grid is resident at once, satrl_ppo_rowpass_kx runs
  * the column-split kernel: each (16-row block, net) on four workgroups of

@@ -2147,6 +2147,47 @@ __global__ void __launch_bounds__(256) reduce_kernel(int H, RedGeom g, int mode,
   if constexpr (SPAN) satrl_span::exit(span, span_t0);
 }
 
+// dw2_kx and the reduce's W1 / tail regions in one launch
+// (satrl_ppo_dw2_kx_w1): blocks [0, ndw) are dw2_kx_kernel's, the rest
+// reduce_kernel's W1 / tail blocks.  Their slabs are the rowpass's (ready when
+// this launch starts), so they run beside the dW2 stream instead of on the
+// reduce's critical path; they write G's W1 / tail regions and (mode & 2)
+// their squared-norm pairs at the reduce's own block indices, and
+// satrl_ppo_reduce with mode bit 4 then runs the W2 blocks only.  Same code,
+// same order: bitwise the two launches' G and norms.
+template <int TW, bool SPAN = false>
+__global__ void __launch_bounds__(256) dw2_kx_w1_kernel(int mb, int S, int KR, int net_sel,
+                                                        const unsigned short* __restrict__ H1x,
+                                                        const unsigned short* __restrict__ dZ2x, float* __restrict__ p2,
+                                                        int ndw, RedGeom g, int mode, const float* __restrict__ p1,
+                                                        const float* __restrict__ pt, float* __restrict__ G,
+                                                        double* __restrict__ nsq, unsigned long long* __restrict__ span) {
+  const unsigned long long span_t0 = SPAN ? satrl_span::now() : 0ull;
+  __shared__ __attribute__((aligned(16))) KxSmem<TW> sm;
+  if ((int)blockIdx.x < ndw) {
+    __builtin_amdgcn_s_setprio(3);                               // (as dw2_kx_kernel)
+    dw2_kx_body<TW>(blockIdx.x, mb, S, KR, net_sel, H1x, dZ2x, p2, sm);
+  } else {
+    // the reduce block's LDS (its float4 chunk sums, the block's norm pair)
+    // inside the ring, which no block of this kind uses
+    static_assert(sizeof(KxSmem<TW>) >= 256 * sizeof(float4) + 8 * sizeof(double), "reduce LDS in the ring");
+    float4* red = reinterpret_cast<float4*>(&sm.ring[0][0][0]);
+    double* sh = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(&sm.ring[0][0][0]) + 256 * sizeof(float4));
+    const int b = (int)blockIdx.x - ndw;
+    double sa = 0.0, sc = 0.0;
+    RedOut o;
+    reduce_w1_tail(256, layout(256), g, b, mode, p1, pt, reinterpret_cast<float4*>(G), 1, red, sa, sc, o);
+    if (mode & 2) {
+      block_sum2(sa, sc, sh);
+      if (threadIdx.x == 0) {
+        nsq[2 * (g.nb2 + b)] = sa;
+        nsq[2 * (g.nb2 + b) + 1] = sc;
+      }
+    }
+  }
+  if constexpr (SPAN) satrl_span::exit(span, span_t0);
+}
+
 // ---------------------------------------------------------------------------
 // adam: torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (_single_tensor_adam)
 // Every block first folds the per-block norms (fixed order, identical in
@@ -2810,6 +2851,30 @@ int satrl_ppo_dw2_kx(int H, int mb, int net, int S, const void* H1x, const void*
   return 0;
 }
 
+int satrl_ppo_dw2_kx_w1(int H, int mb, int net, int S, const void* H1x, const void* dZ2x, int64_t kx_elems, float* p2,
+                        int64_t p2_floats, int mode, const float* p1, const float* pt, float* G, double* nsq,
+                        void* stream) {
+  if (H != 256 || mb <= 0 || net < -1 || net > 1 || S < 1 || !H1x || !dZ2x || !p2) return -1;
+  if (!(mode == 1 || mode == 3) || !p1 || !pt || !G || ((mode & 2) && !nsq)) return -1;
+  const int nch = (int)(kx_rows(mb) / 32), cps = (nch + S - 1) / S;
+  if ((int64_t)cps * (S - 1) >= nch) return -1;                  // an empty split: use satrl_ppo_dw2_kx_splits
+  if (!kx_fits(H, mb, net, kx_elems, "satrl_ppo_dw2_kx_w1") || !p2_fits(H, net, S, p2_floats, "satrl_ppo_dw2_kx_w1"))
+    return -1;
+  const RedGeom rg = geom(H, mb, S, net);
+  const int ndw = (net < 0 ? 2 : 1) * (256 / kKxTW) * (256 / kKxTW) * S;
+  const dim3 g((unsigned)(ndw + rg.nb1 + rg.nbt));
+  unsigned long long* sp = satrl_span::take(satrl_span::kDw2, (int64_t)g.x * 4);
+  const unsigned short *h1 = static_cast<const unsigned short*>(H1x), *dz = static_cast<const unsigned short*>(dZ2x);
+  if (sp)
+    hipLaunchKernelGGL((dw2_kx_w1_kernel<kKxTW, true>), g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net, h1,
+                       dz, p2, ndw, rg, mode, p1, pt, G, nsq, sp);
+  else
+    hipLaunchKernelGGL((dw2_kx_w1_kernel<kKxTW>), g, dim3(256), 0, (hipStream_t)stream, mb, S, cps * 32, net, h1, dz,
+                       p2, ndw, rg, mode, p1, pt, G, nsq, sp);
+  LAUNCH_CHECK();
+  return 0;
+}
+
 int satrl_ppo_dw2_splits(int H, int mb) {
   if (!valid_h(H) || mb <= 0) return -1;
   return dw2_splits(H, mb, -1);
@@ -2835,18 +2900,23 @@ int satrl_ppo_dw2(int H, int mb, int net, int S, const float* H1, const float* d
 
 int satrl_ppo_reduce(int H, int mb, int net, int S, int mode, const float* p2, int64_t p2_floats, const float* p1,
                      const float* pt, float* G, double* nsq, double* steps, void* stream) {
-  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || S < 1 || mode < 1 || mode > 3 || !G) return -1;
-  if ((mode & 1) && (!p2 || !p1 || !pt)) return -1;
+  // mode bit 4: the W2 region only (satrl_ppo_dw2_kx_w1 summed the others)
+  const bool w2_only = (mode & 4) != 0;
+  mode &= 3;
+  if (!valid_h(H) || mb <= 0 || net < -1 || net > 1 || S < 1 || mode < 1 || !G || (w2_only && !(mode & 1)))
+    return -1;
+  if ((mode & 1) && (!p2 || (!w2_only && (!p1 || !pt)))) return -1;
   if ((mode & 1) && !p2_fits(H, net, S, p2_floats, "satrl_ppo_reduce")) return -1;   // the slabs it reads
   if ((mode & 2) && (!nsq || !steps)) return -1;
   const RedGeom g = geom(H, mb, S, net);
-  unsigned long long* sp = satrl_span::take(satrl_span::kReduce, (int64_t)n_blocks(g) * 4);
+  const int nb = w2_only ? g.nb2 : n_blocks(g);
+  unsigned long long* sp = satrl_span::take(satrl_span::kReduce, (int64_t)nb * 4);
   if (sp)
-    hipLaunchKernelGGL(reduce_kernel<true>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1,
-                       pt, G, nsq, steps, 1, sp);
+    hipLaunchKernelGGL(reduce_kernel<true>, dim3(nb), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1, pt, G,
+                       nsq, steps, 1, sp);
   else
-    hipLaunchKernelGGL(reduce_kernel<false>, dim3(n_blocks(g)), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2,
-                       p1, pt, G, nsq, steps, 1, sp);
+    hipLaunchKernelGGL(reduce_kernel<false>, dim3(nb), dim3(256), 0, (hipStream_t)stream, H, g, mode, p2, p1, pt, G,
+                       nsq, steps, 1, sp);
   LAUNCH_CHECK();
   return 0;
 }

@@ -126,6 +126,8 @@ _SIGS = {
     "satrl_ppo_rowpass_error": ([C.POINTER(C.c_int), C.c_double, _vp], C.c_int),
     "satrl_ppo_rowpass_fault_inject": ([C.c_int, C.c_uint, _vp], C.c_int),
     "satrl_ppo_dw2_kx": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _i64, _vp, _i64, _vp], C.c_int),
+    "satrl_ppo_dw2_kx_w1": ([C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _i64, _vp, _i64, C.c_int, _vp, _vp, _vp,
+                             _vp, _vp], C.c_int),
     "satrl_ppo_w2x_sync": ([C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "satrl_ppo_rowpass_dw2": ([C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float, _vp,
                                _i64, _vp, _vp, _vp], C.c_int),

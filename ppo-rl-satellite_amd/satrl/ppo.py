@@ -337,6 +337,21 @@ class FusedMinibatch:
                                           self.H1x.numel(), ptr(self.p2), self.p2.numel(), stream_ptr()),
               "satrl_ppo_dw2_kx")
 
+    def dw2_kx_w1(self, mb, S, net, mode, nsq):
+        """satrl_ppo_dw2_kx_w1: dw2_kx with the reduce's W1 / tail regions
+        (G, and their norm pairs with mode 3) in the same launch; returns the
+        reduce mode bit that leaves it the W2 region (4), or 0 when the
+        library has no such entry (an older development build: A/B only)."""
+        lib = _lib.lib()
+        if _lib.LIB_PATH != _lib._PRODUCT_LIB and not hasattr(lib, "satrl_ppo_dw2_kx_w1"):
+            self.dw2_kx(mb, S, net)
+            return 0
+        check(lib.satrl_ppo_dw2_kx_w1(self.L.H, int(mb), int(net), int(S), ptr(self.H1x), ptr(self.dZ2x),
+                                      self.H1x.numel(), ptr(self.p2), self.p2.numel(), int(mode), ptr(self.pw1),
+                                      ptr(self.ptail), ptr(self.L.G), None if nsq is None else ptr(nsq), stream_ptr()),
+              "satrl_ppo_dw2_kx_w1")
+        return 4
+
     def rowpass_dw2(self, src, idx, mb=None, net=-1):
         """satrl_ppo_rowpass_dw2 (H = 64): the rowpass with each block's dW2
         partial written as split-K slab of p2 (no H1 / dZ2 stores)."""
@@ -436,19 +451,23 @@ class FusedMinibatch:
             H1, dZ2 = self.rowpass(src, idx, mb, net)
         if events is not None:
             events[1].record()
+        # H = 256: the reduce's W1 / tail regions ride in the dW2 launch
+        # (satrl_ppo_dw2_kx_w1), the reduce sums the W2 region (mode bit 4)
         if L.pg is None:
+            w2 = 0
             if kx:
-                self.dw2_kx(mb, S, net)
+                w2 = self.dw2_kx_w1(mb, S, net, 3, nsq)
             elif not self.fused_dw2:
                 self._dw2(H1, dZ2, mb, S, net)
-            check(lib.satrl_ppo_reduce(H, mb, net, S, 3, ptr(self.p2), self.p2.numel(), ptr(self.pw1),
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 3 | w2, ptr(self.p2), self.p2.numel(), ptr(self.pw1),
                                        ptr(self.ptail), ptr(L.G), ptr(nsq), ptr(L.steps), sp), "satrl_ppo_reduce")
         else:
+            w2 = 0
             if kx:
-                self.dw2_kx(mb, S, net)
+                w2 = self.dw2_kx_w1(mb, S, net, 1, None)
             elif not self.fused_dw2:
                 self._dw2(H1, dZ2, mb, S, net)
-            check(lib.satrl_ppo_reduce(H, mb, net, S, 1, ptr(self.p2), self.p2.numel(), ptr(self.pw1),
+            check(lib.satrl_ppo_reduce(H, mb, net, S, 1 | w2, ptr(self.p2), self.p2.numel(), ptr(self.pw1),
                                        ptr(self.ptail), ptr(L.G), None, None, sp), "satrl_ppo_reduce")
             # one bucket, both nets: SUM over the ranks, then G /= world and the norms in one launch
             if L.peer is not None and net < 0:

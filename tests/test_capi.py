@@ -108,6 +108,12 @@ def test_entry_points_reject_bad_arguments_before_any_device_call():
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 0, fake, fake, big, fake, big, None) == -1     # S < 1
     assert lib.satrl_ppo_dw2_kx(256, 64, -1, 3, fake, fake, big, fake, big, None) == -1       # an empty split (2 chunks)
     assert lib.satrl_ppo_dw2_kx(256, 4096, -1, 8, None, fake, big, fake, big, None) == -1     # null H1x
+    w1a = [fake, fake, big, fake, big]                     # (H1x, dZ2x, kx_elems, p2, p2_floats)
+    assert lib.satrl_ppo_dw2_kx_w1(256, 4096, -1, 8, *w1a, 2, fake, fake, fake, fake, None) == -1   # mode 1 or 3
+    assert lib.satrl_ppo_dw2_kx_w1(256, 4096, -1, 8, *w1a, 3, None, fake, fake, fake, None) == -1   # null p1
+    assert lib.satrl_ppo_dw2_kx_w1(256, 4096, -1, 8, *w1a, 3, fake, fake, fake, None, None) == -1   # mode 3: nsq
+    assert lib.satrl_ppo_dw2_kx_w1(64, 4096, -1, 8, *w1a, 1, fake, fake, fake, None, None) == -1    # H 256 only
+    assert lib.satrl_ppo_reduce(256, 4096, -1, 8, 6, fake, big, None, None, fake, fake, fake, None) == -1  # 4 needs 1
     assert lib.satrl_ppo_rowpass_error(None, 1.0, None) == -1                 # the column-split kernel's error word
     assert lib.satrl_ppo_rowpass_error(C.byref(C.c_int()), 0.0, None) == -1  # no deadline
     assert lib.satrl_ppo_rowpass_fault_inject(-1, 0, None) == -1 and lib.satrl_ppo_rowpass_fault_inject(1 << 20, 0, None) == -1

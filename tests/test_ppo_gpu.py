@@ -756,3 +756,55 @@ def test_exchange_check_is_bounded_by_its_deadline():
         rowpass_exchange_check(timeout_s=0.01)
     torch.cuda.synchronize()
     rowpass_exchange_check(timeout_s=5.0)
+
+
+@pytest.mark.parametrize("mb,net", [(4096, -1), (777, -1), (100, -1), (4096, 0), (512, 0)])
+def test_dw2_kx_w1_equals_dw2_kx_then_reduce(mb, net):
+    """satrl_ppo_dw2_kx_w1 (the reduce's W1 / tail regions inside the dW2
+    launch) + satrl_ppo_reduce(mode | 4) writes bitwise the slabs, G, norm
+    pairs and step counters of satrl_ppo_dw2_kx + satrl_ppo_reduce(mode), for
+    mode 3 and mode 1 (the data-parallel sum)."""
+    import ctypes as C
+    import satrl._lib as _L
+    from satrl.ppo import PPOLearner
+    from satrl._lib import ptr
+    torch.manual_seed(5)
+    H, B = 256, 8192
+    args = _args(hidden_width=H, mini_batch_size=mb, batch_size=B)
+    L = PPOLearner(args, "pursuer", use_graph=False)
+    L.sync_w2t()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    src = torch.randn((B, 32), device="cuda", generator=g)
+    src[:, 21:24] = -1.0 - torch.rand((B, 3), device="cuda", generator=g)
+    st = L.stepper(mb)
+    st.rowpass_kx(src, None, mb, net)
+    lib, sp = _L.lib(), _L.stream_ptr()
+    S = lib.satrl_ppo_dw2_kx_splits(H, mb, net)
+    assert S >= 1 and (1 if net == 0 else 2) * S * H * H <= st.p2.numel()     # (net 0: the first half)
+    nsq = st.nsq[0]
+
+    def run(fused, mode):
+        st.p2.fill_(float("nan"))
+        L.G.fill_(float("nan"))
+        nsq.fill_(float("nan"))
+        L.steps.zero_()
+        if fused:
+            assert lib.satrl_ppo_dw2_kx_w1(H, mb, net, S, ptr(st.H1x), ptr(st.dZ2x), st.H1x.numel(), ptr(st.p2),
+                                           st.p2.numel(), mode, ptr(st.pw1), ptr(st.ptail), ptr(L.G),
+                                           ptr(nsq) if mode & 2 else None, sp) == 0
+        else:
+            assert lib.satrl_ppo_dw2_kx(H, mb, net, S, ptr(st.H1x), ptr(st.dZ2x), st.H1x.numel(), ptr(st.p2),
+                                        st.p2.numel(), sp) == 0
+        assert lib.satrl_ppo_reduce(H, mb, net, S, mode | (4 if fused else 0), ptr(st.p2), st.p2.numel(),
+                                    ptr(st.pw1), ptr(st.ptail), ptr(L.G), ptr(nsq) if mode & 2 else None,
+                                    ptr(L.steps) if mode & 2 else None, sp) == 0
+        torch.cuda.synchronize()
+        return [t.clone() for t in (st.p2, L.G, nsq, L.steps)]
+
+    for mode in (3, 1):
+        ref, got = run(False, mode), run(True, mode)
+        for a, b in zip(ref, got):
+            assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a.view(torch.int64),
+                               b.view(torch.int32) if b.dtype == torch.float32 else b.view(torch.int64))
+        if net < 0:
+            assert not torch.isnan(got[1]).any()          # every region of G written

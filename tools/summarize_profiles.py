@@ -53,13 +53,16 @@ def main():
     if os.path.exists(sf) and os.path.exists(sw) and os.path.exists(sm):
         # the post-rowpass chain per launch: HBM bytes (FETCH x2 + WRITE) against
         # the algorithmic bytes, and matrix-core busy cycles (dW2 only has MFMA work)
-        # the product's dW2 at this shape: dw2_kx_kernel (k-packed bf16 planes, 8 splits)
+        # the product's dW2 at this shape: dw2_kx_w1_kernel (k-packed bf16 planes, 8
+        # splits, with the reduce's W1 / tail regions: their slabs in, G's parts out);
+        # reduce_kernel then sums the W2 region only
         kx = True
         H, mb, S, nwg = 256, 4096, 8, 128
         tot = 2 * H * H + 2 * H * 20 + 6 * H + 12            # flat layout incl. pads (satrl_ppo_layout)
-        dw2 = "dw2_kx_kernel"
-        alg = {dw2: (2 * 2 * 3 * mb * H * 2 if kx else 2 * 2 * mb * H * 4) + 2 * S * H * H * 4,
-               "reduce_kernel": (2 * S * H * H + nwg * 2 * H * 20 + nwg * (6 * H + 12)) * 4 + tot * 4,
+        w1t = (nwg * 2 * H * 20 + nwg * (6 * H + 12)) * 4 + (2 * H * 20 + 6 * H + 12) * 4
+        dw2 = "dw2_kx_w1_kernel"
+        alg = {dw2: (2 * 2 * 3 * mb * H * 2 if kx else 2 * 2 * mb * H * 4) + 2 * S * H * H * 4 + w1t,
+               "reduce_kernel": 2 * S * H * H * 4 + 2 * H * H * 4,
                "adam_kernel": 4 * tot * 4 + 3 * tot * 4 + 2 * H * H * (6 if kx else 4)}
         chain = {}
         for sub in (dw2, "reduce_kernel", "adam_kernel"):
@@ -75,8 +78,8 @@ def main():
                           "mfma_busy_frac_dispatch_window": busy / (grbm / 8.0 * 1024) if busy and grbm else None}
         res = {"kernels": chain, "hidden": H, "minibatch": mb, "dw2_splits": S,
                "correction": "FETCH_SIZE x2 (gfx950 16-B/lane reads), WRITE_SIZE x1; kB = 1024 B",
-               "definition": "per-dispatch medians; dw2_kx_kernel = the split-bf16 dW2 on the rowpass's k-packed "
-                             "planes (1.07 GFLOP per launch, f32-equivalent); "
+               "definition": "per-dispatch medians; dw2_kx_w1_kernel = the split-bf16 dW2 on the rowpass's k-packed "
+                             "planes (1.07 GFLOP per launch, f32-equivalent) with the reduce's W1 / tail regions; "
                              "mfma_busy_frac as in the rowpass summary, over the --pmc dispatch window (a lower "
                              "bound for short dispatches)",
                "workload": "tools/step_workload.py (eager minibatch steps)"}
