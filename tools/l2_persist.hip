@@ -14,6 +14,10 @@
 //   shifted     touch(slice b) by block b, then chase(slice b) by block b+1
 //               (another XCD)
 //   in-kernel   touch and chase inside one kernel (block b, slice b)
+//   written     block b rewrites slice b with plain stores (the same words),
+//               then chase(slice b) by block b in the next kernel: do lines a
+//               kernel WROTE (dirty at its end) still hit on the same XCD?
+//   written-shifted   the same, chased by block b+1 (another XCD)
 // Output: one JSON object, ns per dependent load (median over blocks).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/l2_persist.hip -o tools/_probe/l2_persist
 #include <hip/hip_runtime.h>
@@ -58,6 +62,15 @@ __device__ __forceinline__ void chase(const unsigned* s, unsigned long long* out
   out[2 * b + 1] = idx;
 }
 
+// rewrites the slice's words with their own values (plain stores: the lines
+// end the kernel dirty in this XCD's L2)
+__global__ void __launch_bounds__(256) write_kernel(unsigned* __restrict__ buf, const unsigned* __restrict__ src) {
+  unsigned* s = buf + (size_t)blockIdx.x * kWords;
+  const unsigned* r = src + (size_t)blockIdx.x * kWords;
+  for (int i = threadIdx.x * 4; i < kWords; i += 256 * 4)
+    *reinterpret_cast<uint4*>(s + i) = *reinterpret_cast<const uint4*>(r + i);
+}
+
 __global__ void __launch_bounds__(256) chase_kernel(const unsigned* __restrict__ buf, int shift,
                                                     unsigned long long* __restrict__ out) {
   const int slice = (blockIdx.x + kBlocks - shift) % kBlocks;   // block b chases slice b - shift
@@ -97,10 +110,12 @@ int main() {
     std::shuffle(order.begin() + 1, order.end(), rng);
     for (int i = 0; i < kLines; ++i) host[(size_t)b * kWords + 32 * order[i]] = 32 * order[(i + 1) % kLines];
   }
-  unsigned *buf, *sink;
+  unsigned *buf, *sink, *copy;
   unsigned long long* out;
   CK(hipMalloc(&buf, host.size() * 4));
   CK(hipMemcpy(buf, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMalloc(&copy, host.size() * 4));
+  CK(hipMemcpy(copy, host.data(), host.size() * 4, hipMemcpyHostToDevice));
   CK(hipMalloc(&sink, kBlocks * 4));
   CK(hipMalloc(&out, kBlocks * 16));
   const size_t big_bytes = 1ull << 30;
@@ -120,16 +135,17 @@ int main() {
     return v[v.size() / 2];
   };
   std::printf("{\"tool\": \"tools/l2_persist.hip\", \"ns_per_dependent_load\": {");
-  const char* names[4] = {"cold", "same", "shifted", "in_kernel"};
-  for (int c = 0; c < 4; ++c) {
+  const char* names[6] = {"cold", "same", "shifted", "in_kernel", "written", "written_shifted"};
+  for (int c = 0; c < 6; ++c) {
     double best = 1e30;
     for (int rep = 0; rep < 5; ++rep) {
       evict();
       if (c == 1 || c == 2) hipLaunchKernelGGL(touch_kernel, dim3(kBlocks), dim3(256), 0, s, buf, sink);
+      if (c == 4 || c == 5) hipLaunchKernelGGL(write_kernel, dim3(kBlocks), dim3(256), 0, s, buf, copy);
       if (c == 3)
         hipLaunchKernelGGL(touch_chase_kernel, dim3(kBlocks), dim3(256), 0, s, buf, out);
       else
-        hipLaunchKernelGGL(chase_kernel, dim3(kBlocks), dim3(256), 0, s, buf, c == 2 ? 1 : 0, out);
+        hipLaunchKernelGGL(chase_kernel, dim3(kBlocks), dim3(256), 0, s, buf, (c == 2 || c == 5) ? 1 : 0, out);
       best = std::min(best, median_ns());
     }
     std::printf("%s\"%s\": %.1f", c ? ", " : "", names[c], best);
